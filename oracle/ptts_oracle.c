@@ -1,0 +1,697 @@
+/* TEST INFRASTRUCTURE ONLY - CPU oracle (checker) for the Pocket TTS hot path.
+ * See ptts_oracle.h. Plain C99 + OpenMP, fp32 everywhere (the reference
+ * computes in fp32: tts_model.rs:190,202-203).
+ *
+ * Citations are to /root/reference (ykevinc/pocket-tts):
+ *   crates/pocket-tts/src/... (Rust/Candle, the behaviour we follow) and
+ *   python-reference/pocket_tts/... (the fixture generator's code path).
+ */
+#include "ptts_oracle.h"
+
+#include <math.h>
+#include <omp.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* ---- configuration: config/b6369a24.yaml:6-56, tts_model.rs:291-293,389-390 ---- */
+enum {
+  D = 1024, NH = 16, HD = 64, NL = 6, FF = 4096, LDIM = 32, VOCAB = 4001,
+  FD = 512, FDEPTH = 6, FREQ = 256,
+  MD = 512, MNH = 8, MNL = 2, MFF = 2048, MCTX = 250, UP = 16, FRAME = 1920,
+  RING = 512 /* >= MCTX + UP */
+};
+
+/* ---------------- synthetic weights (tests/golden/synth.py) ---------------- */
+static uint64_t fnv1a64(const char* s) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (; *s; ++s) { h ^= (unsigned char)*s; h *= 0x100000001B3ull; }
+  return h;
+}
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static int contains(const char* s, const char* t) { return strstr(s, t) != NULL; }
+static int ends_with(const char* s, const char* t) {
+  size_t a = strlen(s), b = strlen(t);
+  return a >= b && strcmp(s + a - b, t) == 0;
+}
+/* init_rule() of synth.py: returns 0 if the tensor is not random (computed buffer). */
+static int init_rule(const char* name, const int64_t* shape, int nd, double* c, double* hw) {
+  const char* leaf = strrchr(name, '.');
+  leaf = leaf ? leaf + 1 : name;
+  if (!strcmp(leaf, "freqs")) return 0;
+  if (ends_with(name, "emb_std")) { *c = 1.0; *hw = 0.1; return 1; }
+  if (ends_with(name, "emb_mean")) { *c = 0.0; *hw = 0.1; return 1; }
+  if (ends_with(name, "bos_emb")) { *c = 0.0; *hw = sqrt(3.0); return 1; }
+  if (ends_with(name, "conditioner.embed.weight")) { *c = 0.0; *hw = 1.0; return 1; }
+  if (!strcmp(leaf, "alpha")) { *c = 1.0; *hw = 0.1; return 1; }
+  if (!strcmp(leaf, "scale") && contains(name, "layer_scale")) { *c = 0.01; *hw = 0.005; return 1; }
+  int is_norm = contains(name, "norm1.") || contains(name, "norm2.") || contains(name, "out_norm.") ||
+                contains(name, "in_ln.");
+  if (is_norm && !strcmp(leaf, "weight")) { *c = 1.0; *hw = 0.1; return 1; }
+  if (is_norm && !strcmp(leaf, "bias")) { *c = 0.0; *hw = 0.1; return 1; }
+  if (!strcmp(leaf, "bias")) { *c = 0.0; *hw = 0.05; return 1; }
+  if (nd >= 2) {
+    int64_t fan = 1;
+    for (int i = 1; i < nd; ++i) fan *= shape[i];
+    *c = 0.0; *hw = 1.0 / sqrt((double)fan);
+    return 1;
+  }
+  return -1;
+}
+static void synth_fill(uint64_t seed, const char* name, const int64_t* shape, int nd, float* out,
+                       int64_t n) {
+  double c = 0, hw = 0;
+  int r = init_rule(name, shape, nd, &c, &hw);
+  if (r <= 0) { fprintf(stderr, "oracle: no init rule for %s\n", name); abort(); }
+  uint64_t base = seed * 0x9E3779B97F4A7C15ull + fnv1a64(name);
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t z = mix64(base + (uint64_t)i * 0xD1B54A32D192ED03ull);
+    double u = (double)(z >> 40) * (1.0 / 16777216.0);
+    out[i] = (float)(c + (2.0 * u - 1.0) * hw);
+  }
+}
+int orc_synth_head(uint64_t seed, const char* name, const int64_t* shape, int ndim, float* out,
+                   int64_t n) {
+  double c, hw;
+  if (init_rule(name, shape, ndim, &c, &hw) <= 0) return -1;
+  synth_fill(seed, name, shape, ndim, out, n);
+  return 0;
+}
+
+/* ---------------- model ---------------- */
+typedef struct { float *in_proj, *out_proj, *n1w, *n1b, *n2w, *n2b, *l1, *l2, *ls1, *ls2; } Layer;
+typedef struct { float *w, *b; int cin, cout, k, stride; } Conv; /* w repacked [cout][k][cin] */
+typedef struct { float *w, *b; int cin, cout, r; } ConvTr;     /* w as torch [cin][cout][2r] */
+
+struct orc_model {
+  uint64_t seed;
+  /* FlowLM (flow_lm.rs:24-37) */
+  float *embed, *bos, *emb_mean, *emb_std, *input_linear, *out_norm_w, *out_norm_b, *eos_w, *eos_b;
+  Layer fl[NL];
+  /* flow head SimpleMLPAdaLN (mlp.rs:215-223) */
+  float *te_l1w[2], *te_l1b[2], *te_l2w[2], *te_l2b[2], *te_alpha[2];
+  float *cond_w, *cond_b, *inproj_w, *inproj_b;
+  float *rb_lnw[FDEPTH], *rb_lnb[FDEPTH], *rb_w0[FDEPTH], *rb_b0[FDEPTH], *rb_w2[FDEPTH], *rb_b2[FDEPTH],
+      *rb_aw[FDEPTH], *rb_ab[FDEPTH];
+  float *fin_w, *fin_b, *fin_aw, *fin_ab;
+  /* Mimi (mimi.rs:39-53) */
+  float *quant_w, *up_w, *down_w, *speaker_proj;
+  Layer mdec[MNL], menc[MNL];
+  Conv dconv0, dres_a[3], dres_b[3], dfinal;
+  ConvTr dtr[3];
+  Conv econv0, eres_a[3], eres_b[3], edown[3], efinal;
+};
+
+static float* orc_getw(const orc_model* m, const char* name, int64_t s0, int64_t s1, int64_t s2) {
+  int64_t shape[3] = {s0, s1, s2};
+  int nd = s2 ? 3 : (s1 ? 2 : 1);
+  int64_t n = s0 * (s1 ? s1 : 1) * (s2 ? s2 : 1);
+  float* p = (float*)malloc(sizeof(float) * (size_t)n);
+  synth_fill(m->seed, name, shape, nd, p, n);
+  return p;
+}
+/* torch Conv1d weight [cout][cin][k] -> [cout][k][cin] */
+static Conv mkconv(const orc_model* m, const char* pfx, int cin, int cout, int k, int stride, int bias) {
+  char nm[256];
+  Conv c = {0};
+  c.cin = cin; c.cout = cout; c.k = k; c.stride = stride;
+  snprintf(nm, sizeof nm, "%s.weight", pfx);
+  float* w = orc_getw(m, nm, cout, cin, k);
+  c.w = (float*)malloc(sizeof(float) * (size_t)cout * cin * k);
+  for (int o = 0; o < cout; ++o)
+    for (int i = 0; i < cin; ++i)
+      for (int j = 0; j < k; ++j) c.w[((size_t)o * k + j) * cin + i] = w[((size_t)o * cin + i) * k + j];
+  free(w);
+  if (bias) { snprintf(nm, sizeof nm, "%s.bias", pfx); c.b = orc_getw(m, nm, cout, 0, 0); }
+  return c;
+}
+static ConvTr mkconvtr(const orc_model* m, const char* pfx, int cin, int cout, int r) {
+  char nm[256];
+  ConvTr c = {0};
+  c.cin = cin; c.cout = cout; c.r = r;
+  snprintf(nm, sizeof nm, "%s.weight", pfx);
+  c.w = orc_getw(m, nm, cin, cout, 2 * r);
+  snprintf(nm, sizeof nm, "%s.bias", pfx);
+  c.b = orc_getw(m, nm, cout, 0, 0);
+  return c;
+}
+static void mklayer(const orc_model* m, Layer* L, const char* pfx, int d, int ff, int ls) {
+  char nm[256];
+#define W_(field, suffix, a, b)                     \
+  snprintf(nm, sizeof nm, "%s.%s", pfx, suffix);    \
+  L->field = orc_getw(m, nm, a, b, 0);
+  W_(in_proj, "self_attn.in_proj.weight", 3 * d, d);
+  W_(out_proj, "self_attn.out_proj.weight", d, d);
+  W_(n1w, "norm1.weight", d, 0);
+  W_(n1b, "norm1.bias", d, 0);
+  W_(n2w, "norm2.weight", d, 0);
+  W_(n2b, "norm2.bias", d, 0);
+  W_(l1, "linear1.weight", ff, d);
+  W_(l2, "linear2.weight", d, ff);
+  if (ls) {
+    W_(ls1, "layer_scale_1.scale", d, 0);
+    W_(ls2, "layer_scale_2.scale", d, 0);
+  } else {
+    L->ls1 = L->ls2 = NULL;
+  }
+#undef W_
+}
+
+orc_model* orc_model_create(uint64_t seed) {
+  orc_model* m = (orc_model*)calloc(1, sizeof(orc_model));
+  char nm[256];
+  m->seed = seed;
+  m->embed = orc_getw(m, "flow_lm.conditioner.embed.weight", VOCAB, D, 0);
+  m->bos = orc_getw(m, "flow_lm.bos_emb", LDIM, 0, 0);
+  m->emb_mean = orc_getw(m, "flow_lm.emb_mean", LDIM, 0, 0);
+  m->emb_std = orc_getw(m, "flow_lm.emb_std", LDIM, 0, 0);
+  m->input_linear = orc_getw(m, "flow_lm.input_linear.weight", D, LDIM, 0);
+  m->out_norm_w = orc_getw(m, "flow_lm.out_norm.weight", D, 0, 0);
+  m->out_norm_b = orc_getw(m, "flow_lm.out_norm.bias", D, 0, 0);
+  m->eos_w = orc_getw(m, "flow_lm.out_eos.weight", 1, D, 0);
+  m->eos_b = orc_getw(m, "flow_lm.out_eos.bias", 1, 0, 0);
+  for (int l = 0; l < NL; ++l) {
+    snprintf(nm, sizeof nm, "flow_lm.transformer.layers.%d", l);
+    mklayer(m, &m->fl[l], nm, D, FF, 0);
+  }
+  for (int i = 0; i < 2; ++i) {
+    snprintf(nm, sizeof nm, "flow_lm.flow_net.time_embed.%d.mlp.0.weight", i);
+    m->te_l1w[i] = orc_getw(m, nm, FD, FREQ, 0);
+    snprintf(nm, sizeof nm, "flow_lm.flow_net.time_embed.%d.mlp.0.bias", i);
+    m->te_l1b[i] = orc_getw(m, nm, FD, 0, 0);
+    snprintf(nm, sizeof nm, "flow_lm.flow_net.time_embed.%d.mlp.2.weight", i);
+    m->te_l2w[i] = orc_getw(m, nm, FD, FD, 0);
+    snprintf(nm, sizeof nm, "flow_lm.flow_net.time_embed.%d.mlp.2.bias", i);
+    m->te_l2b[i] = orc_getw(m, nm, FD, 0, 0);
+    snprintf(nm, sizeof nm, "flow_lm.flow_net.time_embed.%d.mlp.3.alpha", i);
+    m->te_alpha[i] = orc_getw(m, nm, FD, 0, 0);
+  }
+  m->cond_w = orc_getw(m, "flow_lm.flow_net.cond_embed.weight", FD, D, 0);
+  m->cond_b = orc_getw(m, "flow_lm.flow_net.cond_embed.bias", FD, 0, 0);
+  m->inproj_w = orc_getw(m, "flow_lm.flow_net.input_proj.weight", FD, LDIM, 0);
+  m->inproj_b = orc_getw(m, "flow_lm.flow_net.input_proj.bias", FD, 0, 0);
+  for (int i = 0; i < FDEPTH; ++i) {
+#define RB(field, suffix, a, b)                                                   \
+  snprintf(nm, sizeof nm, "flow_lm.flow_net.res_blocks.%d.%s", i, suffix);     \
+  m->field[i] = orc_getw(m, nm, a, b, 0);
+    RB(rb_lnw, "in_ln.weight", FD, 0);
+    RB(rb_lnb, "in_ln.bias", FD, 0);
+    RB(rb_w0, "mlp.0.weight", FD, FD);
+    RB(rb_b0, "mlp.0.bias", FD, 0);
+    RB(rb_w2, "mlp.2.weight", FD, FD);
+    RB(rb_b2, "mlp.2.bias", FD, 0);
+    RB(rb_aw, "adaLN_modulation.1.weight", 3 * FD, FD);
+    RB(rb_ab, "adaLN_modulation.1.bias", 3 * FD, 0);
+#undef RB
+  }
+  m->fin_w = orc_getw(m, "flow_lm.flow_net.final_layer.linear.weight", LDIM, FD, 0);
+  m->fin_b = orc_getw(m, "flow_lm.flow_net.final_layer.linear.bias", LDIM, 0, 0);
+  m->fin_aw = orc_getw(m, "flow_lm.flow_net.final_layer.adaLN_modulation.1.weight", 2 * FD, FD, 0);
+  m->fin_ab = orc_getw(m, "flow_lm.flow_net.final_layer.adaLN_modulation.1.bias", 2 * FD, 0, 0);
+  m->speaker_proj = orc_getw(m, "flow_lm.speaker_proj_weight", D, MD, 0);
+
+  m->quant_w = orc_getw(m, "mimi.quantizer.output_proj.weight", MD, LDIM, 1);
+  m->up_w = orc_getw(m, "mimi.upsample.convtr.convtr.weight", MD, 1, 2 * UP);
+  for (int l = 0; l < MNL; ++l) {
+    snprintf(nm, sizeof nm, "mimi.decoder_transformer.transformer.layers.%d", l);
+    mklayer(m, &m->mdec[l], nm, MD, MFF, 1);
+    snprintf(nm, sizeof nm, "mimi.encoder_transformer.transformer.layers.%d", l);
+    mklayer(m, &m->menc[l], nm, MD, MFF, 1);
+  }
+  /* SEANetDecoder (seanet.rs:307-402; seanet.py:115-180) */
+  m->dconv0 = mkconv(m, "mimi.decoder.model.0.conv", 512, 512, 7, 1, 1);
+  static const int ratios[3] = {6, 5, 4};
+  int ch = 512;
+  for (int i = 0; i < 3; ++i) {
+    int li = 2 + 3 * i;
+    snprintf(nm, sizeof nm, "mimi.decoder.model.%d.convtr", li);
+    m->dtr[i] = mkconvtr(m, nm, ch, ch / 2, ratios[i]);
+    ch /= 2;
+    snprintf(nm, sizeof nm, "mimi.decoder.model.%d.block.1.conv", li + 1);
+    m->dres_a[i] = mkconv(m, nm, ch, ch / 2, 3, 1, 1);
+    snprintf(nm, sizeof nm, "mimi.decoder.model.%d.block.3.conv", li + 1);
+    m->dres_b[i] = mkconv(m, nm, ch / 2, ch, 1, 1, 1);
+  }
+  m->dfinal = mkconv(m, "mimi.decoder.model.11.conv", 64, 1, 3, 1, 1);
+  /* SEANetEncoder (seanet.rs:148-247; seanet.py:55-112), ratios reversed [4,5,6] */
+  m->econv0 = mkconv(m, "mimi.encoder.model.0.conv", 1, 64, 7, 1, 1);
+  static const int eratios[3] = {4, 5, 6};
+  ch = 64;
+  for (int i = 0; i < 3; ++i) {
+    int li = 1 + 3 * i;
+    snprintf(nm, sizeof nm, "mimi.encoder.model.%d.block.1.conv", li);
+    m->eres_a[i] = mkconv(m, nm, ch, ch / 2, 3, 1, 1);
+    snprintf(nm, sizeof nm, "mimi.encoder.model.%d.block.3.conv", li);
+    m->eres_b[i] = mkconv(m, nm, ch / 2, ch, 1, 1, 1);
+    snprintf(nm, sizeof nm, "mimi.encoder.model.%d.conv", li + 2);
+    m->edown[i] = mkconv(m, nm, ch, ch * 2, 2 * eratios[i], eratios[i], 1);
+    ch *= 2;
+  }
+  m->efinal = mkconv(m, "mimi.encoder.model.11.conv", 512, 512, 3, 1, 1);
+  /* ConvDownsample1d: k=32 s=16 no bias (conv.rs:279-312) */
+  m->down_w = NULL;
+  {
+    Conv dc = mkconv(m, "mimi.downsample.conv.conv", 512, 512, 32, 16, 0);
+    m->down_w = dc.w;
+  }
+  return m;
+}
+
+static void free_layer(Layer* L) {
+  free(L->in_proj); free(L->out_proj); free(L->n1w); free(L->n1b); free(L->n2w); free(L->n2b);
+  free(L->l1); free(L->l2); free(L->ls1); free(L->ls2);
+}
+static void free_conv(Conv* c) { free(c->w); free(c->b); }
+void orc_model_destroy(orc_model* m) {
+  if (!m) return;
+  free(m->embed); free(m->bos); free(m->emb_mean); free(m->emb_std); free(m->input_linear);
+  free(m->out_norm_w); free(m->out_norm_b); free(m->eos_w); free(m->eos_b);
+  for (int l = 0; l < NL; ++l) free_layer(&m->fl[l]);
+  for (int i = 0; i < 2; ++i) {
+    free(m->te_l1w[i]); free(m->te_l1b[i]); free(m->te_l2w[i]); free(m->te_l2b[i]); free(m->te_alpha[i]);
+  }
+  free(m->cond_w); free(m->cond_b); free(m->inproj_w); free(m->inproj_b);
+  for (int i = 0; i < FDEPTH; ++i) {
+    free(m->rb_lnw[i]); free(m->rb_lnb[i]); free(m->rb_w0[i]); free(m->rb_b0[i]); free(m->rb_w2[i]);
+    free(m->rb_b2[i]); free(m->rb_aw[i]); free(m->rb_ab[i]);
+  }
+  free(m->fin_w); free(m->fin_b); free(m->fin_aw); free(m->fin_ab); free(m->speaker_proj);
+  free(m->quant_w); free(m->up_w); free(m->down_w);
+  for (int l = 0; l < MNL; ++l) { free_layer(&m->mdec[l]); free_layer(&m->menc[l]); }
+  free_conv(&m->dconv0); free_conv(&m->dfinal); free_conv(&m->econv0); free_conv(&m->efinal);
+  for (int i = 0; i < 3; ++i) {
+    free_conv(&m->dres_a[i]); free_conv(&m->dres_b[i]); free(m->dtr[i].w); free(m->dtr[i].b);
+    free_conv(&m->eres_a[i]); free_conv(&m->eres_b[i]); free_conv(&m->edown[i]);
+  }
+  free(m);
+}
+
+/* ---------------- primitive ops ---------------- */
+/* y[M][N] = x[M][K] . W[N][K]^T (+ b)   (candle Linear: y = x W^T + b) */
+static void linear(float* y, const float* x, const float* W, const float* b, int M, int N, int K) {
+#pragma omp parallel for collapse(2) schedule(static) if ((long)M * N * K > 200000)
+  for (int i = 0; i < M; ++i)
+    for (int n = 0; n < N; ++n) {
+      const float* xr = x + (size_t)i * K;
+      const float* wr = W + (size_t)n * K;
+      float acc = 0.f;
+#pragma omp simd reduction(+ : acc)
+      for (int k = 0; k < K; ++k) acc += xr[k] * wr[k];
+      y[(size_t)i * N + n] = b ? acc + b[n] : acc;
+    }
+}
+/* LayerNorm, biased variance (mlp.rs:29-58 -> candle_nn::LayerNorm; mlp.py:31-48) */
+static void layernorm(float* y, const float* x, const float* w, const float* b, int M, int N, float eps) {
+  for (int i = 0; i < M; ++i) {
+    const float* xr = x + (size_t)i * N;
+    float mean = 0.f, var = 0.f;
+    for (int n = 0; n < N; ++n) mean += xr[n];
+    mean /= (float)N;
+    for (int n = 0; n < N; ++n) { float d = xr[n] - mean; var += d * d; }
+    var /= (float)N;
+    float inv = 1.0f / sqrtf(var + eps);
+    for (int n = 0; n < N; ++n) {
+      float v = (xr[n] - mean) * inv;
+      y[(size_t)i * N + n] = w ? v * w[n] + b[n] : v;
+    }
+  }
+}
+/* Candle Tensor::gelu = tanh approximation (transformer.rs:85) */
+static float gelu_tanh(float x) {
+  return 0.5f * x * (1.0f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
+}
+static float silu(float x) { return x / (1.0f + expf(-x)); }
+static float elu(float x) { return x >= 0.f ? x : expf(x) - 1.0f; } /* seanet.rs:298-305, alpha 1 */
+
+/* RoPE, interleaved pairs (rope.rs:18-60; rope.py:7-55) on rows [T][nh*64], positions p0+t */
+static void rope(float* q, float* k, int T, int nh, int p0) {
+  for (int t = 0; t < T; ++t) {
+    float ts = (float)(p0 + t);
+    for (int h = 0; h < nh; ++h)
+      for (int i = 0; i < HD / 2; ++i) {
+        float freq = expf((float)i * (-logf(10000.0f) * 2.0f / (float)HD));
+        float ang = freq * ts;
+        float c = cosf(ang), s = sinf(ang);
+        float* qp = q + (size_t)t * nh * HD * 3 + h * HD + 2 * i; /* rows are packed qkv */
+        float* kp = k + (size_t)t * nh * HD * 3 + h * HD + 2 * i;
+        float qr = qp[0], qi = qp[1], kr = kp[0], ki = kp[1];
+        qp[0] = qr * c - qi * s; qp[1] = qr * s + qi * c;
+        kp[0] = kr * c - ki * s; kp[1] = kr * s + ki * c;
+      }
+  }
+}
+
+/* ---------------- state ---------------- */
+struct orc_state {
+  int max_ctx, pos;
+  float* kv; /* [NL][2][NH][max_ctx][HD] */
+  int mpos;
+  float* ring;          /* [MNL][2][MNH][RING][HD] absolute position p stored at p % RING */
+  float up_partial[MD * UP];         /* upsample convtr partial [512][16] (conv.rs:202-267) */
+  float hist0[6 * 512];              /* decoder.model.0 previous [6][512] (time-major) */
+  float tr_partial[3][256 * 6];      /* decoder convtr partials [cout][r] */
+  float res_hist[3][2 * 256];        /* resblock conv3 previous [2][C] */
+  float fin_hist[2 * 64];            /* decoder.model.11 previous [2][64] */
+};
+
+orc_state* orc_state_create(const orc_model* m, int max_ctx) {
+  (void)m;
+  orc_state* s = (orc_state*)calloc(1, sizeof(orc_state));
+  s->max_ctx = max_ctx;
+  s->kv = (float*)calloc((size_t)NL * 2 * NH * max_ctx * HD, sizeof(float));
+  s->ring = (float*)calloc((size_t)MNL * 2 * MNH * RING * HD, sizeof(float));
+  return s;
+}
+void orc_state_destroy(orc_state* s) {
+  if (!s) return;
+  free(s->kv); free(s->ring); free(s);
+}
+int orc_state_pos(const orc_state* s) { return s->pos; }
+
+/* softmax attention of one query against keys K[j], j in [j0, j1] (absolute), key j at kbase + (j % cap)*HD */
+static void attend(float* out, const float* q, const float* kb, const float* vb, int j0, int j1, int cap) {
+  int n = j1 - j0 + 1;
+  float* sc = (float*)malloc(sizeof(float) * (size_t)n);
+  float mx = -INFINITY;
+  for (int j = j0; j <= j1; ++j) {
+    const float* kr = kb + (size_t)(j % cap) * HD;
+    float acc = 0.f;
+#pragma omp simd reduction(+ : acc)
+    for (int d = 0; d < HD; ++d) acc += q[d] * kr[d];
+    acc *= 0.125f; /* 1/sqrt(64): attention.rs:191,229 */
+    sc[j - j0] = acc;
+    if (acc > mx) mx = acc;
+  }
+  float sum = 0.f;
+  for (int i = 0; i < n; ++i) { sc[i] = expf(sc[i] - mx); sum += sc[i]; }
+  for (int d = 0; d < HD; ++d) out[d] = 0.f;
+  for (int j = j0; j <= j1; ++j) {
+    const float* vr = vb + (size_t)(j % cap) * HD;
+    float p = sc[j - j0] / sum;
+    for (int d = 0; d < HD; ++d) out[d] += p * vr[d];
+  }
+  free(sc);
+}
+
+/* One pre-LN transformer layer over T rows (transformer.rs:66-90; mimi_transformer.py:188-206).
+ * kv: per-layer cache base [2][nh][cap][HD]; positions p0..p0+T-1; window (0 = none). */
+static void tlayer(const Layer* L, float* x, int T, int d, int nh, int ff, float* kvl, int cap, int p0,
+                   int window) {
+  float* h = (float*)malloc(sizeof(float) * (size_t)T * d);
+  float* qkv = (float*)malloc(sizeof(float) * (size_t)T * 3 * d);
+  float* o = (float*)malloc(sizeof(float) * (size_t)T * d);
+  float* u = (float*)malloc(sizeof(float) * (size_t)T * ff);
+  layernorm(h, x, L->n1w, L->n1b, T, d, 1e-5f);
+  linear(qkv, h, L->in_proj, NULL, T, 3 * d, d);
+  rope(qkv, qkv + d, T, nh, p0);
+  /* KV append (attention.rs:211-264) */
+  for (int t = 0; t < T; ++t)
+    for (int hh = 0; hh < nh; ++hh) {
+      int slot = (p0 + t) % cap;
+      memcpy(kvl + ((size_t)(0 * nh + hh) * cap + slot) * HD, qkv + (size_t)t * 3 * d + d + hh * HD,
+             sizeof(float) * HD);
+      memcpy(kvl + ((size_t)(1 * nh + hh) * cap + slot) * HD, qkv + (size_t)t * 3 * d + 2 * d + hh * HD,
+             sizeof(float) * HD);
+    }
+  /* causal (+ context window) mask: sdpa.rs:128-171 */
+#pragma omp parallel for collapse(2) schedule(static) if (T * nh > 8)
+  for (int t = 0; t < T; ++t)
+    for (int hh = 0; hh < nh; ++hh) {
+      int p = p0 + t;
+      int j0 = window ? (p - window + 1 > 0 ? p - window + 1 : 0) : 0;
+      attend(o + (size_t)t * d + hh * HD, qkv + (size_t)t * 3 * d + hh * HD,
+             kvl + (size_t)(0 * nh + hh) * cap * HD, kvl + (size_t)(1 * nh + hh) * cap * HD, j0, p, cap);
+    }
+  linear(h, o, L->out_proj, NULL, T, d, d);
+  for (int i = 0; i < T * d; ++i) x[i] += L->ls1 ? L->ls1[i % d] * h[i] : h[i];
+  layernorm(h, x, L->n2w, L->n2b, T, d, 1e-5f);
+  linear(u, h, L->l1, NULL, T, ff, d);
+  for (int i = 0; i < T * ff; ++i) u[i] = gelu_tanh(u[i]);
+  linear(h, u, L->l2, NULL, T, d, ff);
+  for (int i = 0; i < T * d; ++i) x[i] += L->ls2 ? L->ls2[i % d] * h[i] : h[i];
+  free(h); free(qkv); free(o); free(u);
+}
+
+static void flow_transformer(const orc_model* m, orc_state* s, float* x, int T) {
+  if (s->pos + T > s->max_ctx) { fprintf(stderr, "oracle: context overflow\n"); abort(); }
+  for (int l = 0; l < NL; ++l)
+    tlayer(&m->fl[l], x, T, D, NH, FF, s->kv + (size_t)l * 2 * NH * s->max_ctx * HD, s->max_ctx, s->pos, 0);
+  s->pos += T;
+}
+
+void orc_prefill(const orc_model* m, orc_state* s, const float* x, int T) {
+  float* buf = (float*)malloc(sizeof(float) * (size_t)T * D);
+  memcpy(buf, x, sizeof(float) * (size_t)T * D);
+  flow_transformer(m, s, buf, T);
+  free(buf);
+}
+void orc_embed_tokens(const orc_model* m, const int32_t* ids, int S, float* out) {
+  for (int i = 0; i < S; ++i) memcpy(out + (size_t)i * D, m->embed + (size_t)ids[i] * D, sizeof(float) * D);
+}
+void orc_prefill_tokens(const orc_model* m, orc_state* s, const int32_t* ids, int S) {
+  float* buf = (float*)malloc(sizeof(float) * (size_t)S * D);
+  orc_embed_tokens(m, ids, S, buf);
+  flow_transformer(m, s, buf, S);
+  free(buf);
+}
+
+/* TimestepEmbedder (mlp.rs:76-133; mlp.py:51-79); RMSNorm uses unbiased variance (mlp.rs:18-26) */
+static void timestep_embed(const orc_model* m, int which, float tau, float* out) {
+  float emb[FREQ], h[FD];
+  for (int k = 0; k < FREQ / 2; ++k) {
+    float f = expf(-logf(10000.0f) * (float)k / (float)(FREQ / 2));
+    float a = tau * f;
+    emb[k] = cosf(a);
+    emb[FREQ / 2 + k] = sinf(a);
+  }
+  linear(h, emb, m->te_l1w[which], m->te_l1b[which], 1, FD, FREQ);
+  for (int i = 0; i < FD; ++i) h[i] = silu(h[i]);
+  linear(out, h, m->te_l2w[which], m->te_l2b[which], 1, FD, FD);
+  float mean = 0.f, var = 0.f;
+  for (int i = 0; i < FD; ++i) mean += out[i];
+  mean /= FD;
+  for (int i = 0; i < FD; ++i) { float dd = out[i] - mean; var += dd * dd; }
+  var /= (float)(FD - 1);
+  float inv = 1.0f / sqrtf(var + 1e-5f);
+  for (int i = 0; i < FD; ++i) out[i] = out[i] * inv * m->te_alpha[which][i];
+}
+void orc_time_embeddings(const orc_model* m, int n, float* out) {
+  for (int i = 0; i < n; ++i) {
+    float a[FD], b[FD];
+    timestep_embed(m, 0, (float)((double)i / n), a);
+    timestep_embed(m, 1, (float)((double)(i + 1) / n), b);
+    for (int k = 0; k < FD; ++k) out[(size_t)i * FD + k] = (a[k] + b[k]) / 2.0f;
+  }
+}
+
+/* SimpleMLPAdaLN.forward_step_cached (mlp.rs:370-383) + ResBlock/FinalLayer */
+static void flow_head(const orc_model* m, const float* c_emb, const float* tvec, const float* xin, float* out) {
+  float y[FD], mod[3 * FD], x[FD], h[FD], u[FD];
+  for (int i = 0; i < FD; ++i) y[i] = silu(tvec[i] + c_emb[i]); /* mlp.rs:329-330 */
+  linear(x, xin, m->inproj_w, m->inproj_b, 1, FD, LDIM);
+  for (int b = 0; b < FDEPTH; ++b) {
+    linear(mod, y, m->rb_aw[b], m->rb_ab[b], 1, 3 * FD, FD);
+    layernorm(h, x, m->rb_lnw[b], m->rb_lnb[b], 1, FD, 1e-6f);
+    for (int i = 0; i < FD; ++i) h[i] = h[i] * (1.0f + mod[FD + i]) + mod[i]; /* modulate mlp.rs:135 */
+    linear(u, h, m->rb_w0[b], m->rb_b0[b], 1, FD, FD);
+    for (int i = 0; i < FD; ++i) u[i] = silu(u[i]);
+    linear(h, u, m->rb_w2[b], m->rb_b2[b], 1, FD, FD);
+    for (int i = 0; i < FD; ++i) x[i] = x[i] + h[i] * mod[2 * FD + i];
+  }
+  linear(mod, y, m->fin_aw, m->fin_ab, 1, 2 * FD, FD);
+  layernorm(h, x, NULL, NULL, 1, FD, 1e-6f);
+  for (int i = 0; i < FD; ++i) h[i] = h[i] * (1.0f + mod[FD + i]) + mod[i];
+  linear(out, h, m->fin_w, m->fin_b, 1, LDIM, FD);
+}
+
+/* streaming conv, channels-last: x [T][cin], hist [P][cin] (P = k - stride) updated in place.
+ * StreamingConv1d::forward (conv.rs:90-136) */
+static void sconv(const Conv* c, const float* x, int T, float* hist, float* y, int apply_elu) {
+  int P = c->k - c->stride;
+  int Tp = P + T;
+  float* xp = (float*)malloc(sizeof(float) * (size_t)Tp * c->cin);
+  if (P) memcpy(xp, hist, sizeof(float) * (size_t)P * c->cin);
+  for (int i = 0; i < T * c->cin; ++i) xp[(size_t)P * c->cin + i] = apply_elu ? elu(x[i]) : x[i];
+  int To = T / c->stride;
+#pragma omp parallel for collapse(2) schedule(static) if ((long)To * c->cout * c->k * c->cin > 200000)
+  for (int t = 0; t < To; ++t)
+    for (int o = 0; o < c->cout; ++o) {
+      float acc = 0.f;
+      for (int j = 0; j < c->k; ++j) {
+        const float* xr = xp + (size_t)(t * c->stride + j) * c->cin;
+        const float* wr = c->w + ((size_t)o * c->k + j) * c->cin;
+#pragma omp simd reduction(+ : acc)
+        for (int i = 0; i < c->cin; ++i) acc += xr[i] * wr[i];
+      }
+      y[(size_t)t * c->cout + o] = c->b ? acc + c->b[o] : acc;
+    }
+  if (P) memcpy(hist, xp + (size_t)T * c->cin, sizeof(float) * (size_t)P * c->cin);
+  free(xp);
+}
+/* streaming transposed conv with overlap-add partial (conv.rs:219-267), input ELU'd.
+ * x [T][cin] -> y [T*r][cout]; partial [cout][r] */
+static void sconvtr(const ConvTr* c, const float* x, int T, float* partial, float* y) {
+  int r = c->r, K = 2 * r, To = T * r + r;
+  float* full = (float*)calloc((size_t)To * c->cout, sizeof(float));
+  float* e = (float*)malloc(sizeof(float) * (size_t)T * c->cin);
+  for (int i = 0; i < T * c->cin; ++i) e[i] = elu(x[i]);
+#pragma omp parallel for schedule(static) if ((long)T * c->cout * c->cin * K > 200000)
+  for (int o = 0; o < c->cout; ++o)
+    for (int t = 0; t < T; ++t)
+      for (int j = 0; j < K; ++j) {
+        float acc = 0.f;
+        for (int i = 0; i < c->cin; ++i) acc += e[(size_t)t * c->cin + i] * c->w[((size_t)i * c->cout + o) * K + j];
+        full[(size_t)(t * r + j) * c->cout + o] += acc;
+      }
+  for (int t = 0; t < To; ++t)
+    for (int o = 0; o < c->cout; ++o) full[(size_t)t * c->cout + o] += c->b[o];
+  for (int j = 0; j < r; ++j)
+    for (int o = 0; o < c->cout; ++o) full[(size_t)j * c->cout + o] += partial[o * r + j];
+  for (int j = 0; j < r; ++j)
+    for (int o = 0; o < c->cout; ++o) partial[o * r + j] = full[(size_t)(T * r + j) * c->cout + o] - c->b[o];
+  memcpy(y, full, sizeof(float) * (size_t)T * r * c->cout);
+  free(full); free(e);
+}
+
+void orc_mimi_decode_ex(const orc_model* m, orc_state* s, const float* latent, float* pcm, float* quantized,
+                        float* after_up, float* after_tr) {
+  float z[LDIM], q[MD];
+  /* denorm + DummyQuantizer 1x1 conv (tts_model.rs:1033-1038; mimi.rs:8-37) */
+  for (int k = 0; k < LDIM; ++k) z[k] = latent[k] * m->emb_std[k] + m->emb_mean[k];
+  linear(q, z, m->quant_w, NULL, 1, MD, LDIM);
+  if (quantized) memcpy(quantized, q, sizeof q);
+  /* ConvTrUpsample1d depthwise k32 s16, partial overlap-add (conv.rs:315-346) */
+  float* x = (float*)malloc(sizeof(float) * UP * MD);
+  for (int c = 0; c < MD; ++c) {
+    for (int r = 0; r < UP; ++r) x[r * MD + c] = q[c] * m->up_w[c * 2 * UP + r] + s->up_partial[c * UP + r];
+    for (int r = 0; r < UP; ++r) s->up_partial[c * UP + r] = q[c] * m->up_w[c * 2 * UP + UP + r];
+  }
+  if (after_up) memcpy(after_up, x, sizeof(float) * UP * MD);
+  /* decoder transformer, ring context 250 (transformer.rs:227-251, attention.rs:167-264) */
+  for (int l = 0; l < MNL; ++l)
+    tlayer(&m->mdec[l], x, UP, MD, MNH, MFF, s->ring + (size_t)l * 2 * MNH * RING * HD, RING, s->mpos, MCTX);
+  s->mpos += UP;
+  if (after_tr) memcpy(after_tr, x, sizeof(float) * UP * MD);
+  /* SEANetDecoder (seanet.rs:396-402) */
+  float* a = (float*)malloc(sizeof(float) * FRAME * 64);
+  float* b = (float*)malloc(sizeof(float) * FRAME * 64);
+  float* v = (float*)malloc(sizeof(float) * FRAME * 64);
+  sconv(&m->dconv0, x, UP, s->hist0, a, 0);
+  int T = UP, ch = 512;
+  for (int i = 0; i < 3; ++i) {
+    sconvtr(&m->dtr[i], a, T, s->tr_partial[i], b);
+    T *= m->dtr[i].r;
+    ch /= 2;
+    sconv(&m->dres_a[i], b, T, s->res_hist[i], v, 1);
+    sconv(&m->dres_b[i], v, T, NULL, a, 1);
+    for (int k = 0; k < T * ch; ++k) a[k] += b[k]; /* SEANetResnetBlock skip (seanet.py:35) */
+  }
+  sconv(&m->dfinal, a, T, s->fin_hist, pcm, 1);
+  free(x); free(a); free(b); free(v);
+}
+void orc_mimi_decode(const orc_model* m, orc_state* s, const float* latent, float* pcm) {
+  orc_mimi_decode_ex(m, s, latent, pcm, NULL, NULL, NULL);
+}
+
+void orc_step(const orc_model* m, orc_state* s, const float* latent_in, const float* noise, int lsd_steps,
+              float* tout_o, float* eos_o, float* latent_o, float* pcm_o, float* quant_o, float* up_o,
+              float* tr_o) {
+  float x[D], tout[D], cemb[FD], cur[LDIM], flow[LDIM], eos;
+  /* FlowLMModel::forward (flow_lm.rs:98-164) */
+  linear(x, latent_in ? latent_in : m->bos, m->input_linear, NULL, 1, D, LDIM);
+  flow_transformer(m, s, x, 1);
+  layernorm(tout, x, m->out_norm_w, m->out_norm_b, 1, D, 1e-5f);
+  linear(&eos, tout, m->eos_w, m->eos_b, 1, 1, D);
+  linear(cemb, tout, m->cond_w, m->cond_b, 1, FD, D);
+  float* te = (float*)malloc(sizeof(float) * (size_t)lsd_steps * FD);
+  orc_time_embeddings(m, lsd_steps, te);
+  for (int k = 0; k < LDIM; ++k) cur[k] = noise ? noise[k] : 0.f;
+  /* lsd_decode (flow_lm.rs:7-22) */
+  for (int i = 0; i < lsd_steps; ++i) {
+    flow_head(m, cemb, te + (size_t)i * FD, cur, flow);
+    for (int k = 0; k < LDIM; ++k) cur[k] += flow[k] * (1.0f / (float)lsd_steps);
+  }
+  free(te);
+  if (tout_o) memcpy(tout_o, tout, sizeof tout);
+  if (eos_o) *eos_o = eos;
+  if (latent_o) memcpy(latent_o, cur, sizeof cur);
+  float pcm[FRAME];
+  orc_mimi_decode_ex(m, s, cur, pcm, quant_o, up_o, tr_o);
+  if (pcm_o) memcpy(pcm_o, pcm, sizeof pcm);
+}
+
+/* ---------------- encoder (voice cloning) ---------------- */
+void orc_encode(const orc_model* m, const float* pcm, int n, float* cond, float* after_enc, float* after_tr,
+                float* latent_o) {
+  int T = n;
+  float* a = (float*)malloc(sizeof(float) * (size_t)T * 64);
+  float* b = (float*)malloc(sizeof(float) * (size_t)T * 64);
+  float* v = (float*)malloc(sizeof(float) * (size_t)T * 64);
+  float hist[32 * 512];
+  memset(hist, 0, sizeof hist);
+  sconv(&m->econv0, pcm, T, hist, a, 0); /* fresh zero state: model_state=None (mimi.py:106) */
+  int ch = 64;
+  for (int i = 0; i < 3; ++i) {
+    memset(hist, 0, sizeof hist);
+    sconv(&m->eres_a[i], a, T, hist, v, 1);
+    sconv(&m->eres_b[i], v, T, NULL, b, 1);
+    for (int k = 0; k < T * ch; ++k) b[k] += a[k];
+    memset(hist, 0, sizeof hist);
+    sconv(&m->edown[i], b, T, hist, a, 1);
+    T /= m->edown[i].stride;
+    ch *= 2;
+  }
+  memset(hist, 0, sizeof hist);
+  sconv(&m->efinal, a, T, hist, b, 1);
+  if (after_enc) memcpy(after_enc, b, sizeof(float) * (size_t)T * 512);
+  /* encoder transformer: whole sequence, positions 0..T-1, context 250 (mimi_transformer.py:30-38,107-118) */
+  float* ring = (float*)calloc((size_t)2 * MNH * (size_t)T * HD, sizeof(float));
+  for (int l = 0; l < MNL; ++l) tlayer(&m->menc[l], b, T, MD, MNH, MFF, ring, T, 0, MCTX);
+  free(ring);
+  if (after_tr) memcpy(after_tr, b, sizeof(float) * (size_t)T * 512);
+  /* ConvDownsample1d, replicate padding on the first frame (conv.rs:116-123; conv.py:103-108) */
+  Conv dc = {m->down_w, NULL, 512, 512, 32, 16};
+  for (int t = 0; t < 16; ++t) memcpy(hist + t * 512, b, sizeof(float) * 512);
+  sconv(&dc, b, T, hist, a, 0);
+  int F = T / 16;
+  if (latent_o) memcpy(latent_o, a, sizeof(float) * (size_t)F * 512);
+  /* speaker projection (tts_model.rs:543-553) */
+  linear(cond, a, m->speaker_proj, NULL, F, D, MD);
+  free(a); free(b); free(v);
+}
+
+/* ---------------- CPU baseline driver ---------------- */
+double orc_bench(const orc_model* m, int n_utt, int F, int S, int n_frames, int threads) {
+  orc_state** st = (orc_state**)malloc(sizeof(orc_state*) * (size_t)n_utt);
+  float* prompt = (float*)malloc(sizeof(float) * (size_t)F * D);
+  for (int i = 0; i < F * D; ++i) prompt[i] = 0.11f * (float)sin(0.37 * i);
+  int32_t* ids = (int32_t*)malloc(sizeof(int32_t) * (size_t)S);
+  for (int i = 0; i < S; ++i) ids[i] = (i * 97 + 13) % 4000;
+  omp_set_num_threads(threads);
+  for (int u = 0; u < n_utt; ++u) {
+    st[u] = orc_state_create(m, F + S + n_frames + 8);
+    if (u == 0) { orc_prefill(m, st[0], prompt, F); orc_prefill_tokens(m, st[0], ids, S); }
+    else {
+      memcpy(st[u]->kv, st[0]->kv, sizeof(float) * (size_t)NL * 2 * NH * st[0]->max_ctx * HD);
+      st[u]->pos = st[0]->pos;
+    }
+  }
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  /* one utterance per thread; nested parallel regions inside the ops stay serial */
+  omp_set_max_active_levels(1);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+  for (int u = 0; u < n_utt; ++u) {
+    float lat[LDIM], pcm[FRAME];
+    for (int f = 0; f < n_frames; ++f) orc_step(m, st[u], f ? lat : NULL, NULL, 1, NULL, NULL, lat, pcm, NULL, NULL, NULL);
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  for (int u = 0; u < n_utt; ++u) orc_state_destroy(st[u]);
+  free(st); free(prompt); free(ids);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Generate the golden parity fixtures from the reference's own Python modules.
+
+RUN HERE ONLY (needs /root/reference, which does not exist on the GPU box).
+The fixtures it writes (tests/golden/*.safetensors) are data: inputs and the
+reference's outputs for them. The reference itself never ships.
+
+Recipe:
+  * stub the absent `beartype` package, import `python-reference/pocket_tts`;
+  * build FlowLMModel / MimiModel from `config/b6369a24.yaml` without
+    `TTSModel.load_model` (which downloads);
+  * fill every parameter from the shared PRNG in `synth.py`;
+  * "Candle semantics" switch: the Rust reference's
+    FFN uses Candle's tanh-approximate GELU (`models/transformer.rs:85`), so
+    `F.gelu` inside `modules/mimi_transformer.py:174` is swapped for the tanh
+    form;
+  * drive the loop the way `tts_model.rs:935-1071` does: voice prompt prefill
+    (`tts_model.rs:580-599`), text prefill (`:958-964`), then per step
+    FlowLM forward with empty text (`:1016-1030`), denorm + quantize
+    (`:1033-1038`) and Mimi decode (`:1039-1045`), temperature 0.
+
+Usage:  python tests/golden/gen_golden.py   (takes ~1 min on 8 cores)
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+import types
+import typing
+from functools import partial
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE))
+import synth  # noqa: E402
+
+REF = Path(os.environ.get("PTTS_REFERENCE", "/root/reference/python-reference"))
+SEED = 0x5EED
+
+
+def _import_reference():
+    bt = types.ModuleType("beartype")
+    bt.BeartypeConf = lambda **k: None
+    claw = types.ModuleType("beartype.claw")
+    claw.beartype_this_package = lambda **k: None
+    btt = types.ModuleType("beartype.typing")
+    btt.Callable = typing.Callable
+    btt.Iterator = typing.Iterator
+    bt.claw, bt.typing = claw, btt
+    sys.modules.update({"beartype": bt, "beartype.claw": claw, "beartype.typing": btt})
+    sys.path.insert(0, str(REF))
+    import torch
+
+    import pocket_tts.modules.mimi_transformer as mt
+
+    shim = types.SimpleNamespace(**{k: getattr(torch.nn.functional, k) for k in dir(torch.nn.functional) if not k.startswith("__")})
+    shim.gelu = lambda x: torch.nn.functional.gelu(x, approximate="tanh")
+    mt.F = shim
+    return torch
+
+
+def build_models(torch):
+    from pocket_tts.models.flow_lm import FlowLMModel
+    from pocket_tts.models.mimi import MimiModel
+    from pocket_tts.modules.dummy_quantizer import DummyQuantizer
+    from pocket_tts.modules.mimi_transformer import ProjectedTransformer, StreamingTransformer
+    from pocket_tts.modules.mlp import SimpleMLPAdaLN
+    from pocket_tts.modules.seanet import SEANetDecoder, SEANetEncoder
+    from pocket_tts.utils.config import load_config
+
+    cfg = load_config(REF / "pocket_tts/config/b6369a24.yaml")
+    flow_net = SimpleMLPAdaLN.from_pydantic_config(cfg.flow_lm, 32, 1024)
+    tr = StreamingTransformer.from_pydantic_config(cfg.flow_lm.transformer)
+
+    class Cond(torch.nn.Module):  # stands in for LUTConditioner (which downloads a tokenizer)
+        def __init__(self):
+            super().__init__()
+            self.embed = torch.nn.Embedding(4001, 1024)
+
+    flm = FlowLMModel(Cond(), flow_net, tr, dim=1024, ldim=32, dtype=torch.float32)
+    m = cfg.mimi.model_dump()
+    enc = SEANetEncoder(**m["seanet"])
+    dec = SEANetDecoder(**m["seanet"])
+    mimi = MimiModel(
+        enc, dec, DummyQuantizer(**m["quantizer"]), channels=1, sample_rate=24000,
+        frame_rate=12.5, encoder_frame_rate=24000 / enc.hop_length,
+        encoder_transformer=ProjectedTransformer(**m["transformer"]),
+        decoder_transformer=ProjectedTransformer(**m["transformer"]),
+    )
+    for prefix, mod in (("flow_lm.", flm), ("mimi.", mimi)):
+        sd = mod.state_dict()
+        for k, v in sd.items():
+            t = synth.synth_tensor(SEED, prefix + k, tuple(v.shape))
+            if t is not None:
+                sd[k] = torch.from_numpy(t)
+        mod.load_state_dict(sd, strict=True)
+        mod.eval()
+    speaker_proj = torch.from_numpy(synth.synth_tensor(SEED, "flow_lm.speaker_proj_weight", (1024, 512)))
+    return flm, mimi, speaker_proj
+
+
+def run_e2e(torch, flm, mimi, F, S, N, lsd_steps, tag):
+    from pocket_tts.modules.stateful_module import increment_steps, init_states
+
+    prompt = synth.gaussian(1, f"{tag}/prompt", F * 1024, 0.11).reshape(F, 1024)
+    ids = (synth.uniform01(2, f"{tag}/ids", S) * 4000).astype(np.int32)
+    caps = {}
+    h1 = flm.out_norm.register_forward_hook(lambda m, i, o: caps.__setitem__("tout", o[:, -1].clone()))
+    h2 = flm.out_eos.register_forward_hook(lambda m, i, o: caps.__setitem__("eos", o.clone()))
+    out = {"prompt": prompt, "text_ids": ids}
+    with torch.no_grad():
+        state = init_states(flm, batch_size=1, sequence_length=1000)
+        flm.transformer(torch.from_numpy(prompt)[None], state)
+        increment_steps(flm, state, increment=F)
+        emb = flm.conditioner.embed(torch.from_numpy(ids.astype(np.int64)))[None]
+        flm.transformer(emb, state)
+        increment_steps(flm, state, increment=S)
+        mimi_state = init_states(mimi, batch_size=1, sequence_length=1000)
+        backbone = torch.full((1, 1, 32), float("nan"))
+        empty = torch.empty((1, 0, 1024))
+        touts, eos, lats, pcms, quant, ups, trs = [], [], [], [], [], [], []
+        for step in range(N):
+            lat, _ = flm._sample_next_latent(backbone, empty, model_state=state, lsd_decode_steps=lsd_steps,
+                                             temp=0.0, noise_clamp=None, eos_threshold=-4.0)
+            increment_steps(flm, state, increment=1)
+            touts.append(caps["tout"][0].numpy().copy())
+            eos.append(float(caps["eos"][0, 0]))
+            lats.append(lat[0].numpy().copy())
+            x = lat * flm.emb_std + flm.emb_mean
+            q = mimi.quantizer(x[:, :, None])
+            up = mimi.upsample(q, mimi_state)
+            (tr_out,) = mimi.decoder_transformer(up, mimi_state)
+            pcm = mimi.decoder(tr_out, mimi_state)
+            increment_steps(mimi, mimi_state, increment=16)
+            pcms.append(pcm[0, 0].numpy().copy())
+            if step < 3:
+                quant.append(q[0, :, 0].numpy().copy())
+                ups.append(up[0].numpy().copy())
+                trs.append(tr_out[0].numpy().copy())
+            backbone = lat[:, None, :]
+    h1.remove()
+    h2.remove()
+    out.update(
+        tout=np.stack(touts), eos_logit=np.array(eos, np.float32), latent=np.stack(lats),
+        pcm=np.stack(pcms), quantized=np.stack(quant), after_upsample=np.stack(ups),
+        after_decoder_transformer=np.stack(trs),
+        meta=np.array([SEED, F, S, N, lsd_steps], np.int64),
+    )
+    return out
+
+
+def run_encoder(torch, mimi, speaker_proj, n_frames, tag):
+    """Voice cloning front half: PCM -> Mimi latent -> speaker projection (tts_model.py:258-262)."""
+    pcm = synth.gaussian(3, f"{tag}/pcm", n_frames * 1920, 0.1)
+    with torch.no_grad():
+        x = torch.from_numpy(pcm)[None, None]
+        emb = mimi.encoder(x, model_state=None)
+        (tr,) = mimi.encoder_transformer(emb, model_state=None)
+        lat = mimi._to_framerate(tr)
+        cond = torch.nn.functional.linear(lat.transpose(-1, -2), speaker_proj)
+    return {"pcm": pcm, "after_encoder": emb[0].numpy(), "after_encoder_transformer": tr[0].numpy(),
+            "latent": lat[0].numpy(), "conditioning": cond[0].numpy(),
+            "meta": np.array([SEED, n_frames], np.int64)}
+
+
+def main():
+    torch = _import_reference()
+    torch.set_num_threads(8)
+    from safetensors.numpy import save_file
+
+    flm, mimi, speaker_proj = build_models(torch)
+    fx = run_e2e(torch, flm, mimi, F=20, S=10, N=12, lsd_steps=1, tag="e2e_lsd1")
+    save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / "e2e_lsd1.safetensors"))
+    fx = run_e2e(torch, flm, mimi, F=8, S=6, N=4, lsd_steps=2, tag="e2e_lsd2")
+    save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / "e2e_lsd2.safetensors"))
+    fx = run_encoder(torch, mimi, speaker_proj, n_frames=4, tag="enc4")
+    save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / "encoder_4f.safetensors"))
+    # a few individual weights, to pin the PRNG restatement in C against numpy
+    names = ["flow_lm.transformer.layers.0.self_attn.in_proj.weight", "flow_lm.bos_emb",
+             "mimi.decoder.model.2.convtr.weight", "flow_lm.transformer.layers.3.norm2.bias",
+             "mimi.decoder_transformer.transformer.layers.1.layer_scale_2.scale"]
+    sd = {**{"flow_lm." + k: v for k, v in flm.state_dict().items()},
+          **{"mimi." + k: v for k, v in mimi.state_dict().items()}}
+    save_file({n: np.ascontiguousarray(sd[n].numpy().reshape(-1)[:4096]) for n in names},
+              str(HERE / "synth_weights_head.safetensors"))
+    print("fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
