@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Throughput bench of the Pocket TTS generation hot path (BASELINE.json configs[2]).
+
+Workload per GPU: 32 concurrent utterances (batch rows), each a synthetic "10 s" utterance:
+voice prompt [125 x 1024] ~ N(0, 0.11^2), 40 text tokens, generation forced to W+K frames
+(eos_threshold = +inf), temperature 0.7, lsd_decode_steps 1, synthetic weights (seed 0x5EED;
+real checkpoints are gated/offline). One "step" = one batched iteration of the
+generate_stream_segment loop body (tts_model.rs:1006-1070) for all 32 rows: FlowLM step +
+flow head + Mimi decode -> 32 x 1920 PCM samples (32 x 80 ms of audio).
+
+value = audio seconds produced by all ranks / max-over-ranks wall time of the K timed steps,
+with inputs and outputs resident in HBM (the PCIe copy of PCM is not in the timed region).
+Multi-GPU: replicas (independent utterances per GPU, no per-step collective); rank 0 builds the
+weights and broadcasts the packed blob over RCCL once at load time.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "pocket-tts_amd"))
+sys.path.insert(0, str(ROOT / "tests"))
+
+METRIC = "audio-sec/wall-sec (RTF) per GPU at batch=32 + p50 first-chunk latency"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8 TB/s spec
+F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix/vector peak
+BATCH, PROMPT_FRAMES, TEXT_TOKENS = 32, 125, 40
+
+
+def synth_prompt(n=PROMPT_FRAMES):
+    return (0.11 * np.random.default_rng(1).standard_normal((n, 1024))).astype(np.float32)
+
+
+def text_ids(slot):
+    return np.array([(i * 97 + 13 + 7 * slot) % 4000 for i in range(TEXT_TOKENS)], np.int32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=120)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    import pocket_tts_amd as pt
+
+    B, K, W = args.batch, args.steps, args.warmup
+    frames = W + K
+    max_ctx = PROMPT_FRAMES + TEXT_TOKENS + frames + 8
+
+    # ---- engine (+ one RCCL broadcast of the packed weights at load time)
+    if dist is None:
+        eng = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED)
+    else:
+        import torch
+
+        blob = torch.empty(pt.Engine.weight_blob_bytes() // 4, dtype=torch.float32, device=f"cuda:{local_rank}")
+        eng = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
+                        weight_blob=blob.data_ptr(), defer_weights=(rank != 0))
+        torch.cuda.synchronize()
+        dist.broadcast(blob, src=0)
+        torch.cuda.synchronize()
+        if rank != 0:
+            eng.finalize()
+
+    voice = eng.voice_from_prompt(synth_prompt())
+    for b in range(B):
+        eng.open(b, voice, text_ids(b), pt.GenerationParams(temp=0.7, eos_threshold=float("inf"),
+                                                             frames_after_eos=3, max_frames=frames,
+                                                             seed=1000 * rank + b + 1))
+    for _ in range(W):
+        eng.step_async(B)
+    eng.sync()
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        eng.step_async(B)
+    eng.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    r = eng.fetch(B)
+    assert r.valid.all() and np.isfinite(r.pcm).all(), "bench produced invalid frames"
+
+    audio_sec = world * B * K * 1920 / 24000.0
+    value = audio_sec / elapsed
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    # ---- dominant kernel: time every op of the step plan on the engine stream (HIP events)
+    plan = eng.plan(B)
+    seen, per_op = set(), []
+    for name, fl, by in plan:
+        if name in seen:
+            continue
+        seen.add(name)
+        us = eng.time_kernel(B, name, reps=20)
+        per_op.append((us, name, fl, by))
+    per_op.sort(reverse=True)
+    us, name, fl, by = per_op[0]
+    intensity = fl / by if by else 0.0
+    ridge = F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if by and intensity < ridge:
+        roof = {"bound": "hbm", "achieved": round(by / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    else:
+        roof = {"bound": "mfma", "achieved": round(fl / (us * 1e-6) / 1e12, 2), "peak": F32_PEAK_TFLOPS,
+                "unit": "TFLOP/s"}
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    roof["traffic"] = None
+    roof["kernel"] = name
+    roof["avg_us"] = round(us, 2)
+    roof["algorithmic_bytes"] = by
+    roof["algorithmic_flops"] = fl
+    top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
+    sum_ops_ms = sum(u for u, _, _, _ in per_op) / 1000.0
+
+    # ---- p50 first-chunk latency (config 2): text prefill + 1 step, voice precomputed
+    p50 = None
+    if not args.no_latency:
+        e1 = pt.Engine(device=local_rank, max_slots=1, max_ctx=PROMPT_FRAMES + TEXT_TOKENS + 16, seed=0x5EED)
+        v1 = e1.voice_from_prompt(synth_prompt())
+        lat = []
+        for i in range(55):
+            t = time.perf_counter()
+            e1.open(0, v1, text_ids(0), pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), max_frames=4,
+                                                             seed=i + 1))
+            rr = e1.step(1)
+            lat.append(time.perf_counter() - t)
+            assert rr.valid[0]
+        p50 = float(np.median(lat[5:]) * 1000.0)
+        e1.close()
+
+    # ---- CPU baseline: the oracle (C port of the reference algorithm) on the host cores
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        from _oracle import Oracle
+
+        threads = min(16, os.cpu_count() or 1)
+        o = Oracle(0x5EED)
+        n_frames = 4
+        secs = o.bench(B, PROMPT_FRAMES, TEXT_TOKENS, n_frames, threads)
+        cpu = {"value": round(B * n_frames * 0.08 / secs, 3), "unit": "audio-sec/wall-sec", "cores": threads,
+               "kind": "port",
+               "sample": f"{B} utterances x {n_frames} frames after a {PROMPT_FRAMES}+{TEXT_TOKENS} prefill, "
+                         f"fp32 C oracle, one utterance per OpenMP thread"}
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "audio-sec/wall-sec",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(1000.0 * elapsed / K, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded weights and prompts; real checkpoints are gated offline)",
+        "config": {"workload": "b6369a24 batch=32 concurrent 10 s utterances per GPU, lsd_decode_steps=1 "
+                               "(BASELINE configs[2])",
+                   "global_batch": B * world, "utterance_frames": frames, "prompt_frames": PROMPT_FRAMES,
+                   "text_tokens": TEXT_TOKENS, "temp": 0.7, "parallelism": f"replicas x{world}"},
+        "p50_first_chunk_ms": None if p50 is None else round(p50, 3),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "top_ops": top,
+        "sum_op_ms": round(sum_ops_ms, 3),
+    }
+    print(json.dumps(out))
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

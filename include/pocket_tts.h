@@ -1,0 +1,130 @@
+/* pocket_tts.h - C ABI of the MI355X-native Pocket TTS engine (variant b6369a24).
+ *
+ * This is the drop-in boundary for the reference's generation hot path. The
+ * reference (ykevinc/pocket-tts, Rust/Candle) has no operator registry; the
+ * seams it exposes are the model-level API of `TTSModel`
+ * (crates/pocket-tts/src/tts_model.rs) and the kernel-level forwards of
+ * `FlowLMModel` / `MimiModel`. Each entry point below names the reference
+ * interface it replaces. Plain pointers and sizes only; the engine owns all
+ * device memory, the caller owns host buffers. Every function returns 0 on
+ * success or a PTTS_ERR_* code; `ptts_last_error()` gives a thread-local
+ * message (the reference maps its anyhow::Error the same way at the FFI edge:
+ * crates/pocket-tts-bindings/src/lib.rs:17).
+ *
+ * Threading: calls on one engine are externally serialized, as in the
+ * reference (tts_model.py:315-316; server state.rs:69). One engine per GPU.
+ */
+#ifndef POCKET_TTS_H
+#define POCKET_TTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTTS_OK 0
+#define PTTS_ERR_INVALID 1 /* bad argument / shape */
+#define PTTS_ERR_HIP 2     /* HIP runtime error (no GPU, OOM, launch failure) */
+#define PTTS_ERR_STATE 3   /* call not valid in the current slot/engine state */
+#define PTTS_ERR_IO 4      /* weights file missing or malformed */
+
+#define PTTS_FRAME_SAMPLES 1920 /* 24 kHz / 12.5 Hz (config/b6369a24.yaml:24-27) */
+#define PTTS_LATENT_DIM 32
+#define PTTS_MODEL_DIM 1024
+#define PTTS_SAMPLE_RATE 24000
+
+typedef struct ptts_engine ptts_engine;
+typedef struct ptts_voice ptts_voice;
+
+typedef struct ptts_engine_config {
+  int device;           /* HIP device ordinal (one engine per GPU) */
+  int max_slots;        /* concurrent utterances (batch rows) */
+  int max_ctx;          /* FlowLM KV capacity per slot, positions (voice + text + frames) */
+  int lsd_decode_steps; /* TTSModel.lsd_decode_steps (tts_model.rs:22-49), engine-wide */
+  uint64_t synth_seed;  /* synthetic weights (tests/golden/synth.py rule) if weights_path == NULL */
+  const char* weights_path; /* local safetensors with TTSModel state-dict names, or NULL */
+  void* weight_blob;        /* optional caller-owned device buffer of ptts_weight_blob_bytes() */
+  int defer_weights;        /* 1: leave the blob unfilled; caller fills it (e.g. RCCL broadcast)
+                               and then calls ptts_engine_finalize() */
+} ptts_engine_config;
+
+/* Per-utterance generation parameters: TTSModel's public fields temp / eos_threshold /
+ * noise_clamp (tts_model.rs:22-49) plus what generate_stream_segment derives from the text
+ * (max_gen_len = (words+2)*13, frames_after_eos: tts_model.rs:968-969,1230-1237). */
+typedef struct ptts_gen_params {
+  float temp;            /* noise std = sqrt(temp); 0 = deterministic (flow_lm.rs:39-65) */
+  float eos_threshold;   /* EOS when out_eos logit > threshold (flow_lm.rs:139-145) */
+  float noise_clamp;     /* <= 0: None; else truncated normal |x| <= clamp */
+  int frames_after_eos;  /* frames yielded after the EOS step (5 if <=4 words else 3) */
+  int max_frames;        /* max_gen_len */
+  uint64_t seed;         /* noise stream seed for this utterance */
+} ptts_gen_params;
+
+/* Size of the packed device weight blob (all tensors, engine layout). */
+size_t ptts_weight_blob_bytes(void);
+
+/* TTSModel::load / load_with_params_device (tts_model.rs:59-106,182-236). */
+int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out);
+/* Second half of create when cfg->defer_weights = 1 (derived tables, time embeddings). */
+int ptts_engine_finalize(ptts_engine* e);
+void ptts_engine_destroy(ptts_engine* e);
+/* Device pointer of the packed weight blob (for the caller's RCCL broadcast). */
+void* ptts_engine_weight_blob(ptts_engine* e);
+
+/* TTSModel::get_voice_state_from_prompt_tensor (tts_model.rs:490-501): prefill an
+ * `audio_prompt` [n_frames x 1024] (row-major, host) into an immutable voice KV prefix. */
+int ptts_voice_from_prompt(ptts_engine* e, const float* prompt, int n_frames, ptts_voice** out);
+/* TTSModel::get_voice_state_from_tensor (tts_model.rs:504-560): 24 kHz mono PCM ->
+ * Mimi encoder -> speaker projection -> FlowLM prefill. n_samples is zero-padded to a
+ * multiple of 1920. */
+int ptts_voice_from_pcm(ptts_engine* e, const float* pcm, int n_samples, ptts_voice** out);
+/* Conditioning rows the voice holds (frames). */
+int ptts_voice_len(const ptts_voice* v);
+/* The [n_frames x 1024] conditioning a PCM voice was built from (host copy); for tests. */
+int ptts_voice_conditioning(const ptts_voice* v, float* out, int max_rows);
+void ptts_voice_destroy(ptts_voice* v);
+
+/* Admission of one utterance into batch row `slot` = the per-segment prologue of
+ * generate_stream_segment (tts_model.rs:938-1004): copy the voice KV prefix, embed and
+ * prefill `n_ids` text tokens (text.rs:289-303), reset the Mimi state, backbone = bos_emb. */
+int ptts_slot_open(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* ids, int n_ids,
+                   const ptts_gen_params* p);
+int ptts_slot_close(ptts_engine* e, int slot);
+
+/* THE batched hot path: one iteration of the loop body of generate_stream_segment
+ * (tts_model.rs:1006-1070) for rows [0, n_rows): FlowLM step -> EOS -> flow sampling ->
+ * denorm/quantize -> Mimi decode -> 1920 PCM samples per active row.
+ * Host outputs (each may be NULL):
+ *   pcm [n_rows x 1920], frame_valid [n_rows] (row was active this step),
+ *   last [n_rows] (this was the row's final frame: EOS tail reached or max_frames),
+ *   eos_logits [n_rows], latents [n_rows x 32] (the sampled latent of this step). */
+int ptts_step(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
+              float* eos_logits, float* latents);
+/* Same step, enqueued only (outputs stay in HBM); use ptts_sync() + ptts_fetch(). */
+int ptts_step_async(ptts_engine* e, int n_rows);
+int ptts_sync(ptts_engine* e);
+int ptts_fetch(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
+               float* eos_logits, float* latents);
+/* Test hook (teacher forcing): overwrite the backbone input latent of `slot`. */
+int ptts_slot_set_latent(ptts_engine* e, int slot, const float* latent32);
+
+/* TTSModel::generate for one segment (tts_model.rs:687-703) on row `slot`: loops ptts_step
+ * until the row's last frame. pcm_out receives up to max_samples samples. */
+int ptts_generate(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* ids, int n_ids,
+                  const ptts_gen_params* p, float* pcm_out, int max_samples, int* n_samples);
+
+/* Measurement: replay one named kernel of the step plan `reps` times between HIP events on
+ * the engine stream; returns the average duration in microseconds. */
+int ptts_time_kernel(ptts_engine* e, int n_rows, const char* name, int reps, double* avg_us);
+/* The step plan for n_rows: one line per op, "name<TAB>flops<TAB>bytes" (algorithmic cost of one
+ * launch; 0 where not modelled). */
+int ptts_plan_ops(ptts_engine* e, int n_rows, char* buf, int buflen);
+
+const char* ptts_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

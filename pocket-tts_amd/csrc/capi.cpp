@@ -1,0 +1,171 @@
+// extern "C" boundary (include/pocket_tts.h): exceptions -> status codes + thread-local message.
+#include <cstring>
+#include <string>
+
+#include "engine.h"
+#include "pocket_tts.h"
+
+struct ptts_engine {
+  ptts::Engine* impl = nullptr;
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <class F>
+int guard(F&& f) {
+  try {
+    f();
+    g_err.clear();
+    return PTTS_OK;
+  } catch (const ptts::Error& e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "host out of memory";
+    return PTTS_ERR_HIP;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return PTTS_ERR_INVALID;
+  }
+}
+ptts::Engine& eng(ptts_engine* e) {
+  if (!e || !e->impl) throw ptts::Error(PTTS_ERR_INVALID, "null engine");
+  return *e->impl;
+}
+}  // namespace
+
+extern "C" {
+
+size_t ptts_weight_blob_bytes(void) { return ptts::pack_weights(nullptr, nullptr).total * sizeof(float); }
+
+int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out) {
+  return guard([&] {
+    if (!cfg || !out) throw ptts::Error(PTTS_ERR_INVALID, "null argument");
+    *out = nullptr;
+    auto* h = new ptts_engine();
+    try {
+      h->impl = new ptts::Engine(*cfg);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int ptts_engine_finalize(ptts_engine* e) { return guard([&] { eng(e).finalize(); }); }
+
+void ptts_engine_destroy(ptts_engine* e) {
+  if (!e) return;
+  delete e->impl;
+  delete e;
+}
+
+void* ptts_engine_weight_blob(ptts_engine* e) { return (e && e->impl) ? e->impl->blob() : nullptr; }
+
+int ptts_voice_from_prompt(ptts_engine* e, const float* prompt, int n_frames, ptts_voice** out) {
+  return guard([&] {
+    if (!out) throw ptts::Error(PTTS_ERR_INVALID, "null out");
+    *out = eng(e).voice_from_prompt(prompt, n_frames);
+  });
+}
+
+int ptts_voice_from_pcm(ptts_engine* e, const float* pcm, int n_samples, ptts_voice** out) {
+  return guard([&] {
+    if (!out) throw ptts::Error(PTTS_ERR_INVALID, "null out");
+    *out = eng(e).voice_from_pcm(pcm, n_samples);
+  });
+}
+
+int ptts_voice_len(const ptts_voice* v) { return v ? v->F : 0; }
+
+int ptts_voice_conditioning(const ptts_voice* v, float* out, int max_rows) {
+  return guard([&] {
+    if (!v || !out) throw ptts::Error(PTTS_ERR_INVALID, "null argument");
+    if (v->cond.empty()) throw ptts::Error(PTTS_ERR_STATE, "voice was not built from PCM");
+    const int rows = std::min(max_rows, v->F);
+    memcpy(out, v->cond.data(), sizeof(float) * rows * ptts::D);
+  });
+}
+
+void ptts_voice_destroy(ptts_voice* v) {
+  if (!v) return;
+  if (v->kv) (void)hipFree(v->kv);
+  delete v;
+}
+
+int ptts_slot_open(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* ids, int n_ids,
+                   const ptts_gen_params* p) {
+  return guard([&] {
+    if (!p) throw ptts::Error(PTTS_ERR_INVALID, "null params");
+    eng(e).slot_open(slot, v, ids, n_ids, *p);
+  });
+}
+
+int ptts_slot_close(ptts_engine* e, int slot) { return guard([&] { eng(e).slot_close(slot); }); }
+
+int ptts_slot_set_latent(ptts_engine* e, int slot, const float* latent32) {
+  return guard([&] { eng(e).set_latent(slot, latent32); });
+}
+
+int ptts_step(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last, float* eos_logits,
+              float* latents) {
+  return guard([&] {
+    auto& E = eng(e);
+    E.step_async(n_rows);
+    E.fetch(n_rows, pcm, frame_valid, last, eos_logits, latents);
+  });
+}
+
+int ptts_step_async(ptts_engine* e, int n_rows) { return guard([&] { eng(e).step_async(n_rows); }); }
+
+int ptts_sync(ptts_engine* e) { return guard([&] { eng(e).sync(); }); }
+
+int ptts_fetch(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last, float* eos_logits,
+               float* latents) {
+  return guard([&] { eng(e).fetch(n_rows, pcm, frame_valid, last, eos_logits, latents); });
+}
+
+int ptts_generate(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* ids, int n_ids,
+                  const ptts_gen_params* p, float* pcm_out, int max_samples, int* n_samples) {
+  return guard([&] {
+    if (!p || !n_samples) throw ptts::Error(PTTS_ERR_INVALID, "null argument");
+    auto& E = eng(e);
+    E.slot_open(slot, v, ids, n_ids, *p);
+    const int B = slot + 1;
+    std::vector<float> pcm((size_t)B * ptts::FRAME);
+    std::vector<uint8_t> valid(B), last(B);
+    int total = 0;
+    for (int it = 0; it < p->max_frames; ++it) {
+      E.step_async(B);
+      E.fetch(B, pcm.data(), valid.data(), last.data(), nullptr, nullptr);
+      if (!valid[slot]) break;
+      const int take = std::max(0, std::min(ptts::FRAME, max_samples - total));
+      if (pcm_out && take > 0) memcpy(pcm_out + total, pcm.data() + (size_t)slot * ptts::FRAME, sizeof(float) * take);
+      total += ptts::FRAME;
+      if (last[slot]) break;
+    }
+    *n_samples = total;
+  });
+}
+
+int ptts_time_kernel(ptts_engine* e, int n_rows, const char* name, int reps, double* avg_us) {
+  return guard([&] {
+    if (!name || !avg_us) throw ptts::Error(PTTS_ERR_INVALID, "null argument");
+    *avg_us = eng(e).time_op(n_rows, name, reps);
+  });
+}
+
+int ptts_plan_ops(ptts_engine* e, int n_rows, char* buf, int buflen) {
+  return guard([&] {
+    std::string s;
+    for (auto& n : eng(e).plan_names(n_rows)) s += n + "\n";
+    if (!buf || buflen <= (int)s.size()) throw ptts::Error(PTTS_ERR_INVALID, "buffer too small");
+    memcpy(buf, s.c_str(), s.size() + 1);
+  });
+}
+
+const char* ptts_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

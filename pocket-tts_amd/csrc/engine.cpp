@@ -1,0 +1,818 @@
+// Engine: device memory, step plan, HIP graphs, voice and slot management.
+//
+// Data layout in HBM (fp32):
+//   weight blob                packed by weights.cpp (one allocation; RCCL-broadcastable)
+//   FlowLM KV                  [slot][layer][k|v][head][max_ctx][64]   (attention.rs:211-231, preallocated)
+//   Mimi KV ring               [slot][layer][k|v][head][512][64]       (attention.rs:167-264, ctx 250)
+//   conv histories             [slot][P][C] per streaming conv          (conv.rs:71-136, time-major)
+//   activations                row-major [rows][features]; Mimi/SEANet channels-last [slot][time][ch]
+#include "engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace ptts {
+
+namespace {
+int pick_splits(int M, int N, int K) {
+  const int tiles = ((N + 31) / 32) * ((M + 31) / 32);
+  const int chunks = K / 32;
+  int s = std::max(1, 768 / std::max(1, tiles));
+  s = std::min(s, std::max(1, chunks / 4));
+  return s;
+}
+}  // namespace
+
+float* Engine::dalloc(size_t n) {
+  void* p = nullptr;
+  PTTS_HIP(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(float)));
+  PTTS_HIP(hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(float)));
+  allocs_.push_back(p);
+  return (float*)p;
+}
+
+Engine::Engine(const ptts_engine_config& cfg) {
+  PTTS_REQUIRE(cfg.max_slots >= 1 && cfg.max_slots <= 256, "max_slots must be in [1, 256]");
+  PTTS_REQUIRE(cfg.max_ctx >= 16 && cfg.max_ctx <= 8192, "max_ctx must be in [16, 8192]");
+  PTTS_REQUIRE(cfg.lsd_decode_steps >= 1 && cfg.lsd_decode_steps <= 64, "lsd_decode_steps must be in [1, 64]");
+  dev_ = cfg.device;
+  max_slots_ = cfg.max_slots;
+  max_ctx_ = cfg.max_ctx;
+  lsd_ = cfg.lsd_decode_steps;
+  int ndev = 0;
+  PTTS_HIP(hipGetDeviceCount(&ndev));
+  PTTS_REQUIRE(dev_ >= 0 && dev_ < ndev, "HIP device ordinal out of range");
+  PTTS_HIP(hipSetDevice(dev_));
+  PTTS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+
+  L_ = pack_weights(nullptr, nullptr);
+  if (cfg.weight_blob) {
+    blob_ = (float*)cfg.weight_blob;
+    own_blob_ = false;
+  } else {
+    blob_ = dalloc(L_.total);
+  }
+
+  const int B = max_slots_;
+  kv_layer_ = (long)2 * NH * max_ctx_ * 64;
+  kv_slot_ = kv_layer_ * NL;
+  kv_ = dalloc((size_t)kv_slot_ * (B + 1));
+  ring_layer_ = (long)2 * MNH * RING * 64;
+  ring_slot_ = ring_layer_ * MNL;
+  ring_ = dalloc((size_t)ring_slot_ * B);
+  fpos_ = (int*)dalloc(B + 1);
+  mpos_ = (int*)dalloc(B + 1);
+  st_ = (SlotState*)dalloc((sizeof(SlotState) * B + 3) / 4);
+  lat_in_ = dalloc((size_t)B * LDIM);
+  cur_ = dalloc((size_t)B * LDIM);
+  qprev_ = dalloc((size_t)B * MD);
+  eos_ = dalloc(B);
+
+  // streaming conv histories (SEANetDecoder, seanet.rs:307-402): source T, channels, rows kept
+  const int hT[8] = {16, 16, 96, 96, 480, 480, 1920, 1920};
+  const int hC[8] = {512, 512, 256, 256, 128, 128, 64, 64};
+  const int hP[8] = {6, 1, 2, 1, 2, 1, 2, 2};
+  for (int i = 0; i < 8; ++i) {
+    hist_T_[i] = hT[i];
+    hist_C_[i] = hC[i];
+    hist_P_[i] = hP[i];
+    hist_[i] = dalloc((size_t)B * hP[i] * hC[i]);
+  }
+
+  const int R = std::max(B, PREFILL);
+  x_ = dalloc((size_t)R * D);
+  h_ = dalloc((size_t)R * D);
+  q_ = dalloc((size_t)R * D);
+  o_ = dalloc((size_t)R * D);
+  u_ = dalloc((size_t)R * FF);
+  pcap_ = (size_t)4 << 20;
+  partial_ = dalloc(pcap_);
+  ids_dev_ = (int*)dalloc(PREFILL);
+  ysilu_ = dalloc((size_t)lsd_ * B * FD);
+  mods_ = dalloc((size_t)lsd_ * B * NADA);
+  xf_ = dalloc((size_t)B * FD);
+  hf_ = dalloc((size_t)B * FD);
+  uf_ = dalloc((size_t)B * FD);
+  mx_ = dalloc((size_t)B * UP * MD);
+  mh_ = dalloc((size_t)B * UP * MD);
+  mq_ = dalloc((size_t)B * UP * MD);
+  mo_ = dalloc((size_t)B * UP * MD);
+  mqkv_ = dalloc((size_t)B * UP * 3 * MD);
+  mu_ = dalloc((size_t)B * UP * MFF);
+  a0_ = dalloc((size_t)B * 16 * 512);
+  int T = 16, ch = 512;
+  for (int i = 0; i < 3; ++i) {
+    T *= RATIOS[i];
+    ch /= 2;
+    cb_[i] = dalloc((size_t)B * T * ch);
+    cv_[i] = dalloc((size_t)B * T * (ch / 2));
+    ca_[i] = dalloc((size_t)B * T * ch);
+  }
+  pcm_ = dalloc((size_t)B * FRAME);
+  temb_ = dalloc((size_t)lsd_ * FD);
+  temb_tmp_ = dalloc((size_t)2 * lsd_ * FD);
+
+  PTTS_HIP(hipHostMalloc((void**)&h_pcm_, sizeof(float) * B * FRAME, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_eos_, sizeof(float) * B, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_lat_, sizeof(float) * B * LDIM, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_st_, sizeof(SlotState) * B, hipHostMallocDefault));
+
+  if (!cfg.defer_weights) {
+    std::unique_ptr<TensorSource> src = cfg.weights_path && cfg.weights_path[0]
+                                            ? make_safetensors_source(cfg.weights_path)
+                                            : make_synth_source(cfg.synth_seed);
+    upload_weights(src.get());
+    finalize();
+  }
+}
+
+Engine::~Engine() {
+  (void)hipSetDevice(dev_);
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
+  for (void* p : allocs_) (void)hipFree(p);
+  if (h_pcm_) (void)hipHostFree(h_pcm_);
+  if (h_eos_) (void)hipHostFree(h_eos_);
+  if (h_lat_) (void)hipHostFree(h_lat_);
+  if (h_st_) (void)hipHostFree(h_st_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Engine::upload_weights(TensorSource* src) {
+  std::vector<float> host(L_.total, 0.f);
+  pack_weights(src, host.data());
+  PTTS_HIP(hipMemcpy(blob_, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+}
+
+void Engine::finalize() {
+  PTTS_HIP(hipSetDevice(dev_));
+  TimeEmbedWeights tw;
+  for (int i = 0; i < 2; ++i) {
+    tw.l1w[i] = W(L_.te_l1w[i]);
+    tw.l1b[i] = W(L_.te_l1b[i]);
+    tw.l2w[i] = W(L_.te_l2w[i]);
+    tw.l2b[i] = W(L_.te_l2b[i]);
+    tw.alpha[i] = W(L_.te_alpha[i]);
+  }
+  time_embeddings(tw, lsd_, temb_tmp_, temb_, stream_);
+  PTTS_HIP(hipGetLastError());
+  PTTS_HIP(hipStreamSynchronize(stream_));
+  ready_ = true;
+}
+
+void Engine::run_ops(const std::vector<Op>& ops) {
+  for (const Op& op : ops) {
+    op.fn(stream_);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw Error(PTTS_ERR_HIP, "launch of " + op.name + " failed: " + hipGetErrorString(e));
+  }
+}
+
+// ------------------------------------------------------------------ op builders
+void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M,
+                          const float* Wt, int N, int K, int* S_out) {
+  PTTS_REQUIRE(K % 32 == 0, "GEMM K must be a multiple of 32");
+  int S = pick_splits(M, N, K);
+  while (S > 1 && (size_t)S * M * N > pcap_) --S;
+  PTTS_REQUIRE((size_t)S * M * N <= pcap_, "split-K partial buffer too small");
+  GemmArgs a{};
+  a.mode = 0;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.X = X;
+  a.ldx = ldx;
+  a.W = Wt;
+  a.S = S;
+  a.partial = partial_;
+  ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
+                 4.0 * ((double)N * K + (double)M * K + (double)S * M * N)});
+  *S_out = S;
+}
+
+void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,
+                      int K, const float* bias, int act, const float* rscale, const float* R, float* Y) {
+  PTTS_REQUIRE(K % 32 == 0, "GEMM K must be a multiple of 32");
+  GemmArgs a{};
+  a.mode = 0;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.X = X;
+  a.ldx = K;
+  a.W = Wt;
+  a.S = 1;
+  a.bias = bias;
+  a.act = act;
+  a.rscale = rscale;
+  a.R = R;
+  a.ldr = N;
+  a.Y = Y;
+  a.ldy = N;
+  ops.push_back({name, [a](hipStream_t s) { gemm(a, 1, s); }, 2.0 * M * N * K,
+                 4.0 * ((double)N * K + (double)M * K + (double)M * N * (R ? 2 : 1))});
+}
+
+void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float* X, int B, int T_in, int cin,
+                     const float* H, int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases,
+                     const float* bias, const float* R, float* Y, int T_out, int tstride) {
+  PTTS_REQUIRE(cin % 32 == 0, "conv cin must be a multiple of 32");
+  GemmArgs a{};
+  a.mode = 1;
+  a.Tq = T_in / stride;
+  a.M = B * a.Tq;
+  a.N = cout;
+  a.K = ktaps * cin;
+  a.X = X;
+  a.ldx = cin;
+  a.H = H;
+  a.P = P;
+  a.T_in = T_in;
+  a.stride_in = stride;
+  a.cin = cin;
+  a.elu_in = elu;
+  a.W = Wt;
+  a.w_phase_stride = (long)cout * ktaps * cin;
+  a.S = 1;
+  a.bias = bias;
+  a.R = R;
+  a.ldr = cout;
+  a.Y = Y;
+  a.ldy = cout;
+  a.T_out = T_out;
+  a.out_tstride = tstride;
+  ops.push_back({name, [a, phases](hipStream_t s) { gemm(a, phases, s); }, 2.0 * a.M * a.N * a.K * phases,
+                 4.0 * ((double)phases * a.N * a.K + (double)B * T_in * cin +
+                        (double)B * T_out * cout * (R ? 2 : 1))});
+}
+
+// FlowLM transformer layers over M rows (x_ holds the residual stream, h_ = norm1_0(x_)).
+// StreamingTransformerLayer::forward (transformer.rs:66-90).
+void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag) {
+  for (int l = 0; l < NL; ++l) {
+    const Layout::TL& t = L_.fl[l];
+    const std::string p = tag + ".l" + std::to_string(l);
+    KvStore kv{kv_ + (long)l * kv_layer_, kv_slot_, max_ctx_};
+    int S = 1;
+    linear_split(ops, p + ".qkv_gemm", h_, D, M, W(t.in_proj), 3 * D, D, &S);
+    {
+      const float* P = partial_;
+      float* Q = q_;
+      ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(P, S, nullptr, M, NH, map, kv, Q, s); }});
+    }
+    {
+      const float* Q = q_;
+      float* O = o_;
+      ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, M, NH, map, kv, 0, qg, O, s); }});
+    }
+    auto rr = [&](const std::string& name, int S2, int N, int act, bool resid, float* Y, const float* lnw,
+                  const float* lnb, bool ln, float* Hout) {
+      RowReduceArgs a{};
+      a.P = partial_;
+      a.S = S2;
+      a.M = M;
+      a.N = N;
+      a.act = act;
+      if (resid) {
+        a.R = x_;
+        a.ldr = D;
+      }
+      a.Y = Y;
+      a.ldy = N;
+      a.ln = ln ? 1 : 0;
+      a.ln_w = lnw;
+      a.ln_b = lnb;
+      a.eps = 1e-5f;
+      a.Hout = Hout;
+      a.ldh = N;
+      ops.push_back({name, [a](hipStream_t s) { row_reduce(a, s); }});
+    };
+    linear_split(ops, p + ".out_gemm", o_, D, M, W(t.out_proj), D, D, &S);
+    rr(p + ".out_reduce_ln2", S, D, ACT_NONE, true, x_, W(t.n2w), W(t.n2b), true, h_);
+    linear_split(ops, p + ".ff1_gemm", h_, D, M, W(t.l1), FF, D, &S);
+    rr(p + ".ff1_reduce_gelu", S, FF, ACT_GELU, false, u_, nullptr, nullptr, false, nullptr);
+    linear_split(ops, p + ".ff2_gemm", u_, FF, M, W(t.l2), D, FF, &S);
+    if (l + 1 < NL)
+      rr(p + ".ff2_reduce_ln1", S, D, ACT_NONE, true, x_, W(L_.fl[l + 1].n1w), W(L_.fl[l + 1].n1b), true, h_);
+    else
+      rr(p + ".ff2_reduce_outnorm", S, D, ACT_NONE, true, x_, W(L_.out_norm_w), W(L_.out_norm_b), out_norm, h_);
+  }
+}
+
+// Prefill T rows already in x_ into slot `slot` at positions p0.. (tts_model.rs:580-599, 958-964).
+void Engine::prefill_rows(std::vector<Op>& ops, int slot, int T, int p0) {
+  {
+    float* x = x_;
+    float* h = h_;
+    const float* w = W(L_.fl[0].n1w);
+    const float* b = W(L_.fl[0].n1b);
+    ops.push_back({"prefill.ln1", [=](hipStream_t s) { layernorm(x, D, h, D, T, D, w, b, 1e-5f, s); }});
+  }
+  RowMap map{slot, T, p0, nullptr};
+  flow_layers(ops, T, map, 16, false, "prefill");
+}
+
+std::vector<Op> Engine::build_step(int B) {
+  std::vector<Op> ops;
+  int S = 1;
+  // ---- FlowLM step (flow_lm.rs:98-164): input_linear -> transformer -> out_norm
+  linear_split(ops, "flow.input_gemm", lat_in_, LDIM, B, W(L_.input_linear), D, LDIM, &S);
+  {
+    RowReduceArgs a{};
+    a.P = partial_;
+    a.S = S;
+    a.M = B;
+    a.N = D;
+    a.Y = x_;
+    a.ldy = D;
+    a.ln = 1;
+    a.ln_w = W(L_.fl[0].n1w);
+    a.ln_b = W(L_.fl[0].n1b);
+    a.eps = 1e-5f;
+    a.Hout = h_;
+    a.ldh = D;
+    ops.push_back({"flow.input_reduce_ln1", [a](hipStream_t s) { row_reduce(a, s); }});
+  }
+  flow_layers(ops, B, RowMap{0, 1, 0, fpos_}, 1, true, "flow");
+  // ---- flow head (mlp.rs:215-383): cond_embed | out_eos, EOS bookkeeping, noise
+  linear_split(ops, "head.cond_eos_gemm", h_, D, B, W(L_.cond_eos_w), NCOND, D, &S);
+  {
+    const float* P = partial_;
+    const float* bias = W(L_.cond_eos_b);
+    const float* temb = temb_;
+    const int lsd = lsd_;
+    SlotState* st = st_;
+    float *ys = ysilu_, *cur = cur_, *eos = eos_;
+    ops.push_back({"head.flow_cond", [=](hipStream_t s) { flow_cond(P, S, B, bias, temb, lsd, st, ys, cur, eos, s); }});
+  }
+  // all adaLN modulations of all lsd steps in one GEMM (mlp.rs:322-368)
+  linear_split(ops, "head.ada_gemm", ysilu_, FD, lsd_ * B, W(L_.ada_w), NADA, FD, &S);
+  {
+    RowReduceArgs a{};
+    a.P = partial_;
+    a.S = S;
+    a.M = lsd_ * B;
+    a.N = NADA;
+    a.bias = W(L_.ada_b);
+    a.Y = mods_;
+    a.ldy = NADA;
+    ops.push_back({"head.ada_reduce", [a](hipStream_t s) { row_reduce(a, s); }});
+  }
+  // lsd_decode Euler steps (flow_lm.rs:7-22) over ResBlocks (mlp.rs:146-213)
+  for (int st = 0; st < lsd_; ++st) {
+    const float* mods = mods_ + (size_t)st * B * NADA;
+    const std::string p = "head.s" + std::to_string(st);
+    linear_split(ops, p + ".inproj_gemm", cur_, LDIM, B, W(L_.inproj_w), FD, LDIM, &S);
+    {
+      RowReduceArgs a{};
+      a.P = partial_;
+      a.S = S;
+      a.M = B;
+      a.N = FD;
+      a.bias = W(L_.inproj_b);
+      a.Y = xf_;
+      a.ldy = FD;
+      a.ln = 1;
+      a.ln_w = W(L_.rb_lnw[0]);
+      a.ln_b = W(L_.rb_lnb[0]);
+      a.eps = 1e-6f;
+      a.mshift = mods + 0;
+      a.mscale = mods + FD;
+      a.ldm = NADA;
+      a.Hout = hf_;
+      a.ldh = FD;
+      ops.push_back({p + ".inproj_reduce", [a](hipStream_t s) { row_reduce(a, s); }});
+    }
+    for (int i = 0; i < FDEPTH; ++i) {
+      const std::string pb = p + ".rb" + std::to_string(i);
+      linear_split(ops, pb + ".mlp0_gemm", hf_, FD, B, W(L_.rb_w0[i]), FD, FD, &S);
+      {
+        RowReduceArgs a{};
+        a.P = partial_;
+        a.S = S;
+        a.M = B;
+        a.N = FD;
+        a.bias = W(L_.rb_b0[i]);
+        a.act = ACT_SILU;
+        a.Y = uf_;
+        a.ldy = FD;
+        ops.push_back({pb + ".mlp0_reduce", [a](hipStream_t s) { row_reduce(a, s); }});
+      }
+      linear_split(ops, pb + ".mlp2_gemm", uf_, FD, B, W(L_.rb_w2[i]), FD, FD, &S);
+      {
+        RowReduceArgs a{};
+        a.P = partial_;
+        a.S = S;
+        a.M = B;
+        a.N = FD;
+        a.bias = W(L_.rb_b2[i]);
+        a.gate = mods + (size_t)i * 3 * FD + 2 * FD;
+        a.ldg = NADA;
+        a.R = xf_;
+        a.ldr = FD;
+        a.Y = xf_;
+        a.ldy = FD;
+        a.ln = 1;
+        a.eps = 1e-6f;
+        if (i + 1 < FDEPTH) {
+          a.ln_w = W(L_.rb_lnw[i + 1]);
+          a.ln_b = W(L_.rb_lnb[i + 1]);
+          a.mshift = mods + (size_t)(i + 1) * 3 * FD;
+          a.mscale = mods + (size_t)(i + 1) * 3 * FD + FD;
+        } else {  // FinalLayer: non-affine LN + final adaLN (mlp.rs:182-213)
+          a.mshift = mods + (size_t)FDEPTH * 3 * FD;
+          a.mscale = mods + (size_t)FDEPTH * 3 * FD + FD;
+        }
+        a.ldm = NADA;
+        a.Hout = hf_;
+        a.ldh = FD;
+        ops.push_back({pb + ".mlp2_reduce", [a](hipStream_t s) { row_reduce(a, s); }});
+      }
+    }
+    linear_split(ops, p + ".final_gemm", hf_, FD, B, W(L_.fin_w), LDIM, FD, &S);
+    {
+      RowReduceArgs a{};
+      a.P = partial_;
+      a.S = S;
+      a.M = B;
+      a.N = LDIM;
+      a.bias = W(L_.fin_b);
+      a.euler = cur_;
+      a.euler_scale = 1.0f / (float)lsd_;
+      ops.push_back({p + ".euler", [a](hipStream_t s) { row_reduce(a, s); }});
+    }
+  }
+  // ---- Mimi decode (mimi.rs:143-157): quantize + upsample, decoder transformer, SEANet decoder
+  {
+    const float *lat = cur_, *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w), *wu = W(L_.up_w);
+    const float *lw = W(L_.mdec[0].n1w), *lb = W(L_.mdec[0].n1b);
+    float *qp = qprev_, *x = mx_, *h = mh_;
+    const SlotState* st = st_;
+    ops.push_back({"mimi.quant_upsample",
+                   [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qp, st, x, h, lw, lb, s); }});
+  }
+  const int MR = B * UP;
+  RowMap mmap{0, UP, 0, mpos_};
+  for (int l = 0; l < MNL; ++l) {
+    const Layout::TL& t = L_.mdec[l];
+    const std::string p = "mimi.l" + std::to_string(l);
+    KvStore kv{ring_ + (long)l * ring_layer_, ring_slot_, RING};
+    dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_);
+    {
+      const float* qkv = mqkv_;
+      float* Q = mq_;
+      ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(nullptr, 0, qkv, MR, MNH, mmap, kv, Q, s); }});
+    }
+    {
+      const float* Q = mq_;
+      float* O = mo_;
+      ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, MR, MNH, mmap, kv, MCTX, UP, O, s); }});
+    }
+    dense_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, nullptr, ACT_NONE, W(t.ls1), mx_, mx_);
+    {
+      const float *x = mx_, *w = W(t.n2w), *b = W(t.n2b);
+      float* h = mh_;
+      ops.push_back({p + ".ln2", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
+    }
+    dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_);
+    dense_op(ops, p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, nullptr, ACT_NONE, W(t.ls2), mx_, mx_);
+    if (l + 1 < MNL) {
+      const float *x = mx_, *w = W(L_.mdec[l + 1].n1w), *b = W(L_.mdec[l + 1].n1b);
+      float* h = mh_;
+      ops.push_back({p + ".ln1_next", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
+    }
+  }
+  // SEANetDecoder (seanet.rs:396-402): conv0 -> [ELU, convtr(r), resblock] x3 -> ELU, conv(64->1)
+  conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, W(L_.dc0_b), nullptr, a0_,
+          16, 1);
+  const float* cin_buf = a0_;
+  int T = 16, ch = 512;
+  for (int i = 0; i < 3; ++i) {
+    const int r = RATIOS[i];
+    const std::string p = "seanet.up" + std::to_string(i);
+    conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 1, W(L_.dtr_w[i]), ch / 2, 2, r,
+            W(L_.dtr_b[i]), nullptr, cb_[i], T * r, r);
+    T *= r;
+    ch /= 2;
+    conv_op(ops, p + ".res_conv3", cb_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 1, W(L_.dra_w[i]), ch / 2, 3, 1,
+            W(L_.dra_b[i]), nullptr, cv_[i], T, 1);
+    conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 1, W(L_.drb_w[i]), ch, 1, 1, W(L_.drb_b[i]),
+            cb_[i], ca_[i], T, 1);
+    cin_buf = ca_[i];
+  }
+  {
+    const float *X = ca_[2], *H = hist_[7], *w = W(L_.dfin_w), *b = W(L_.dfin_b);
+    float* Y = pcm_;
+    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, FRAME, 64, 3, w, b, Y, s); }});
+  }
+  // ---- commit: conv histories, positions, next backbone input
+  {
+    CommitArgs c{};
+    const float* srcs[8] = {mx_, a0_, cb_[0], ca_[0], cb_[1], ca_[1], cb_[2], ca_[2]};
+    for (int i = 0; i < 8; ++i) c.h[i] = HistDesc{srcs[i], hist_[i], hist_T_[i], hist_C_[i], hist_P_[i]};
+    c.nh = 8;
+    c.B = B;
+    c.st = st_;
+    c.latent_next = lat_in_;
+    c.latent = cur_;
+    c.fpos = fpos_;
+    c.mpos = mpos_;
+    ops.push_back({"commit", [c](hipStream_t s) { step_commit(c, s); }});
+  }
+  return ops;
+}
+
+std::vector<std::string> Engine::plan_names(int B) {
+  PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
+  std::vector<std::string> v;
+  char buf[64];
+  for (auto& op : build_step(B)) {
+    snprintf(buf, sizeof buf, "\t%.6g\t%.6g", op.flops, op.bytes);
+    v.push_back(op.name + buf);
+  }
+  return v;
+}
+
+void Engine::step_async(int B) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
+  PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
+  PTTS_HIP(hipSetDevice(dev_));
+  auto it = graphs_.find(B);
+  if (it == graphs_.end()) {
+    std::vector<Op> ops = build_step(B);
+    hipGraph_t g = nullptr;
+    PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    try {
+      for (const Op& op : ops) op.fn(stream_);
+    } catch (...) {
+      (void)hipStreamEndCapture(stream_, &g);
+      throw;
+    }
+    PTTS_HIP(hipStreamEndCapture(stream_, &g));
+    hipGraphExec_t ge = nullptr;
+    PTTS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    graph_defs_[B] = g;
+    it = graphs_.emplace(B, ge).first;
+  }
+  PTTS_HIP(hipGraphLaunch(it->second, stream_));
+}
+
+void Engine::sync() {
+  PTTS_HIP(hipSetDevice(dev_));
+  PTTS_HIP(hipStreamSynchronize(stream_));
+}
+
+void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat) {
+  PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
+  PTTS_HIP(hipSetDevice(dev_));
+  if (pcm) PTTS_HIP(hipMemcpyAsync(h_pcm_, pcm_, sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, stream_));
+  if (eos) PTTS_HIP(hipMemcpyAsync(h_eos_, eos_, sizeof(float) * B, hipMemcpyDeviceToHost, stream_));
+  if (lat) PTTS_HIP(hipMemcpyAsync(h_lat_, cur_, sizeof(float) * B * LDIM, hipMemcpyDeviceToHost, stream_));
+  PTTS_HIP(hipMemcpyAsync(h_st_, st_, sizeof(SlotState) * B, hipMemcpyDeviceToHost, stream_));
+  PTTS_HIP(hipStreamSynchronize(stream_));
+  if (pcm) memcpy(pcm, h_pcm_, sizeof(float) * B * FRAME);
+  if (eos) memcpy(eos, h_eos_, sizeof(float) * B);
+  if (lat) memcpy(lat, h_lat_, sizeof(float) * B * LDIM);
+  for (int b = 0; b < B; ++b) {
+    if (valid) valid[b] = (uint8_t)(h_st_[b].valid != 0);
+    if (last) last[b] = (uint8_t)(h_st_[b].valid && h_st_[b].last);
+  }
+}
+
+double Engine::time_op(int B, const std::string& name, int reps) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
+  PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
+  PTTS_REQUIRE(reps >= 1, "reps must be >= 1");
+  PTTS_HIP(hipSetDevice(dev_));
+  std::vector<Op> ops = build_step(B);
+  const Op* sel = nullptr;
+  for (const Op& op : ops)
+    if (op.name == name) sel = &op;
+  PTTS_REQUIRE(sel != nullptr, "no op named " + name + " in the step plan");
+  hipEvent_t e0, e1;
+  PTTS_HIP(hipEventCreate(&e0));
+  PTTS_HIP(hipEventCreate(&e1));
+  sel->fn(stream_);  // warm
+  PTTS_HIP(hipEventRecord(e0, stream_));
+  for (int i = 0; i < reps; ++i) sel->fn(stream_);
+  PTTS_HIP(hipEventRecord(e1, stream_));
+  PTTS_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  PTTS_HIP(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 1000.0 * ms / reps;
+}
+
+// ------------------------------------------------------------------ voices and slots
+ptts_voice* Engine::voice_from_prompt(const float* prompt, int F) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
+  PTTS_REQUIRE(prompt != nullptr && F >= 1, "empty prompt");
+  PTTS_REQUIRE(F < max_ctx_, "prompt longer than max_ctx");
+  PTTS_HIP(hipSetDevice(dev_));
+  PTTS_HIP(hipStreamSynchronize(stream_));
+  const int scratch = max_slots_;
+  for (int c0 = 0; c0 < F; c0 += PREFILL) {
+    const int T = std::min(PREFILL, F - c0);
+    PTTS_HIP(hipMemcpyAsync(x_, prompt + (size_t)c0 * D, sizeof(float) * T * D, hipMemcpyHostToDevice, stream_));
+    std::vector<Op> ops;
+    prefill_rows(ops, scratch, T, c0);
+    run_ops(ops);
+  }
+  ptts_voice* v = new ptts_voice();
+  v->F = F;
+  v->owner = this;
+  try {
+    PTTS_HIP(hipMalloc(&v->kv, sizeof(float) * (size_t)NL * 2 * NH * F * 64));
+    PTTS_HIP(hipMemcpy2DAsync(v->kv, sizeof(float) * F * 64, kv_ + (size_t)scratch * kv_slot_,
+                              sizeof(float) * max_ctx_ * 64, sizeof(float) * F * 64, NL * 2 * NH,
+                              hipMemcpyDeviceToDevice, stream_));
+    PTTS_HIP(hipStreamSynchronize(stream_));
+  } catch (...) {
+    if (v->kv) (void)hipFree(v->kv);
+    delete v;
+    throw;
+  }
+  return v;
+}
+
+void Engine::encoder_transformer(std::vector<Op>& ops, float* x, int T, float* h, float* qkv, float* q, float* o,
+                                 float* u, float* ring) {
+  RowMap map{0, T, 0, nullptr};
+  {
+    const float *w = W(L_.menc[0].n1w), *b = W(L_.menc[0].n1b);
+    ops.push_back({"enc.ln1", [=](hipStream_t s) { layernorm(x, MD, h, MD, T, MD, w, b, 1e-5f, s); }});
+  }
+  for (int l = 0; l < MNL; ++l) {
+    const Layout::TL& t = L_.menc[l];
+    KvStore kv{ring + (size_t)l * 2 * MNH * T * 64, 0, T};
+    dense_op(ops, "enc.qkv", h, T, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, qkv);
+    ops.push_back({"enc.rope", [=](hipStream_t s) { qkv_rope_append(nullptr, 0, qkv, T, MNH, map, kv, q, s); }});
+    ops.push_back({"enc.attn", [=](hipStream_t s) { attention(q, T, MNH, map, kv, MCTX, 16, o, s); }});
+    dense_op(ops, "enc.out", o, T, W(t.out_proj), MD, MD, nullptr, ACT_NONE, W(t.ls1), x, x);
+    {
+      const float *w = W(t.n2w), *b = W(t.n2b);
+      ops.push_back({"enc.ln2", [=](hipStream_t s) { layernorm(x, MD, h, MD, T, MD, w, b, 1e-5f, s); }});
+    }
+    dense_op(ops, "enc.ff1", h, T, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, u);
+    dense_op(ops, "enc.ff2", u, T, W(t.l2), MD, MFF, nullptr, ACT_NONE, W(t.ls2), x, x);
+    if (l + 1 < MNL) {
+      const float *w = W(L_.menc[l + 1].n1w), *b = W(L_.menc[l + 1].n1b);
+      ops.push_back({"enc.ln1", [=](hipStream_t s) { layernorm(x, MD, h, MD, T, MD, w, b, 1e-5f, s); }});
+    }
+  }
+}
+
+// Mimi encoder + speaker projection (tts_model.rs:504-553, mimi.rs:113-141), then prompt prefill.
+ptts_voice* Engine::voice_from_pcm(const float* pcm, int n) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
+  PTTS_REQUIRE(pcm != nullptr && n >= 1, "empty PCM");
+  PTTS_HIP(hipSetDevice(dev_));
+  const int Np = (n + FRAME - 1) / FRAME * FRAME;  // zero-pad to whole frames (mimi.py:103)
+  const int F = Np / FRAME, Te = Np / 120;
+  PTTS_REQUIRE(F < max_ctx_, "voice prompt longer than max_ctx");
+  std::vector<void*> tmp;
+  auto talloc = [&](size_t cnt) {
+    void* p = nullptr;
+    PTTS_HIP(hipMalloc(&p, std::max<size_t>(cnt, 1) * sizeof(float)));
+    tmp.push_back(p);
+    return (float*)p;
+  };
+  ptts_voice* v = nullptr;
+  try {
+    float* dpcm = talloc(Np);
+    float* A = talloc((size_t)Np * 64);
+    float* Bf = talloc((size_t)Np * 64);
+    float* V = talloc((size_t)Np * 32);
+    float* zeros = talloc(16 * 512);
+    PTTS_HIP(hipMemsetAsync(dpcm, 0, sizeof(float) * Np, stream_));
+    PTTS_HIP(hipMemsetAsync(zeros, 0, sizeof(float) * 16 * 512, stream_));
+    PTTS_HIP(hipMemcpyAsync(dpcm, pcm, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+    std::vector<Op> ops;
+    {
+      const float *w = W(L_.ec0_w), *b = W(L_.ec0_b);
+      ops.push_back({"enc.conv0", [=](hipStream_t s) { conv_cin1(dpcm, Np, 64, 7, w, b, A, s); }});
+    }
+    int T = Np, ch = 64;
+    for (int i = 0; i < 3; ++i) {
+      const int r = RATIOS[2 - i];
+      conv_op(ops, "enc.res_conv3", A, 1, T, ch, zeros, 2, 1, 1, W(L_.era_w[i]), ch / 2, 3, 1, W(L_.era_b[i]),
+              nullptr, V, T, 1);
+      conv_op(ops, "enc.res_conv1", V, 1, T, ch / 2, nullptr, 0, 1, 1, W(L_.erb_w[i]), ch, 1, 1, W(L_.erb_b[i]), A,
+              Bf, T, 1);
+      conv_op(ops, "enc.down", Bf, 1, T, ch, zeros, r, r, 1, W(L_.edn_w[i]), 2 * ch, 2 * r, 1, W(L_.edn_b[i]),
+              nullptr, A, T / r, 1);
+      T /= r;
+      ch *= 2;
+    }
+    conv_op(ops, "enc.conv_final", A, 1, T, 512, zeros, 2, 1, 1, W(L_.efin_w), 512, 3, 1, W(L_.efin_b), nullptr, Bf,
+            T, 1);
+    // encoder transformer on Bf rows [Te][512]
+    float* h = talloc((size_t)Te * MD);
+    float* qkv = talloc((size_t)Te * 3 * MD);
+    float* q = talloc((size_t)Te * MD);
+    float* o = talloc((size_t)Te * MD);
+    float* u = talloc((size_t)Te * MFF);
+    float* ring = talloc((size_t)MNL * 2 * MNH * Te * 64);
+    encoder_transformer(ops, Bf, Te, h, qkv, q, o, u, ring);
+    // ConvDownsample1d k32 s16, replicate padding of the first frame (conv.rs:116-123)
+    float* Hd = talloc(16 * 512);
+    ops.push_back({"enc.replicate", [=](hipStream_t s) { copy2d(Bf, 0, Hd, 512, 16, 512, s); }});
+    float* lat = talloc((size_t)F * 512);
+    conv_op(ops, "enc.downsample", Bf, 1, Te, 512, Hd, 16, 16, 0, W(L_.down_w), 512, 32, 1, nullptr, nullptr, lat, F,
+            1);
+    float* cond = talloc((size_t)F * D);
+    dense_op(ops, "enc.speaker_proj", lat, F, W(L_.speaker_proj), D, MD, nullptr, ACT_NONE, nullptr, nullptr, cond);
+    run_ops(ops);
+    std::vector<float> hcond((size_t)F * D);
+    PTTS_HIP(hipMemcpyAsync(hcond.data(), cond, sizeof(float) * hcond.size(), hipMemcpyDeviceToHost, stream_));
+    PTTS_HIP(hipStreamSynchronize(stream_));
+    for (void* p : tmp) (void)hipFree(p);
+    tmp.clear();
+    v = voice_from_prompt(hcond.data(), F);
+    v->cond = std::move(hcond);
+  } catch (...) {
+    (void)hipStreamSynchronize(stream_);
+    for (void* p : tmp) (void)hipFree(p);
+    throw;
+  }
+  return v;
+}
+
+void Engine::slot_open(int slot, const ptts_voice* v, const int32_t* ids, int n, const ptts_gen_params& p) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
+  PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
+  PTTS_REQUIRE(v != nullptr && v->owner == this, "voice belongs to another engine");
+  PTTS_REQUIRE(n >= 0 && (n == 0 || ids != nullptr), "bad token ids");
+  PTTS_REQUIRE(p.max_frames >= 1, "max_frames must be >= 1");
+  PTTS_REQUIRE(p.frames_after_eos >= 0, "frames_after_eos must be >= 0");
+  PTTS_REQUIRE((long)v->F + n + p.max_frames <= max_ctx_, "voice + text + max_frames exceeds max_ctx");
+  for (int i = 0; i < n; ++i) PTTS_REQUIRE(ids[i] >= 0 && ids[i] < VOCAB, "token id out of range");
+  PTTS_HIP(hipSetDevice(dev_));
+  PTTS_HIP(hipStreamSynchronize(stream_));
+  // copy-on-admit of the immutable voice prefix
+  PTTS_HIP(hipMemcpy2DAsync(kv_ + (size_t)slot * kv_slot_, sizeof(float) * max_ctx_ * 64, v->kv,
+                            sizeof(float) * v->F * 64, sizeof(float) * v->F * 64, NL * 2 * NH,
+                            hipMemcpyDeviceToDevice, stream_));
+  // fresh Mimi decoder state (init_states(1, 1000) per segment, tts_model.rs:941)
+  for (int i = 0; i < 8; ++i)
+    PTTS_HIP(hipMemsetAsync(hist_[i] + (size_t)slot * hist_P_[i] * hist_C_[i], 0,
+                            sizeof(float) * hist_P_[i] * hist_C_[i], stream_));
+  PTTS_HIP(hipMemsetAsync(qprev_ + (size_t)slot * MD, 0, sizeof(float) * MD, stream_));
+  PTTS_HIP(hipMemcpyAsync(lat_in_ + (size_t)slot * LDIM, W(L_.bos), sizeof(float) * LDIM, hipMemcpyDeviceToDevice,
+                          stream_));
+  // text prefill (tts_model.rs:947-964)
+  int pos = v->F;
+  for (int c0 = 0; c0 < n; c0 += PREFILL) {
+    const int T = std::min(PREFILL, n - c0);
+    PTTS_HIP(hipMemcpyAsync(ids_dev_, ids + c0, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    std::vector<Op> ops;
+    {
+      const int* idp = ids_dev_;
+      const float* tab = W(L_.embed);
+      float* x = x_;
+      ops.push_back({"prefill.embed", [=](hipStream_t s) { embed_gather(idp, T, tab, D, x, s); }});
+    }
+    prefill_rows(ops, slot, T, pos);
+    run_ops(ops);
+    PTTS_HIP(hipStreamSynchronize(stream_));  // ids_dev_ is reused by the next chunk
+    pos += T;
+  }
+  SlotState s{};
+  s.active = 1;
+  s.step = 0;
+  s.eos_step = -1;
+  s.last = 0;
+  s.frames_after_eos = p.frames_after_eos;
+  s.max_frames = p.max_frames;
+  s.temp = p.temp;
+  s.eos_threshold = p.eos_threshold;
+  s.noise_clamp = p.noise_clamp;
+  s.valid = 0;
+  s.seed = p.seed;
+  const int zero = 0;
+  PTTS_HIP(hipMemcpy(st_ + slot, &s, sizeof s, hipMemcpyHostToDevice));
+  PTTS_HIP(hipMemcpy(fpos_ + slot, &pos, sizeof(int), hipMemcpyHostToDevice));
+  PTTS_HIP(hipMemcpy(mpos_ + slot, &zero, sizeof(int), hipMemcpyHostToDevice));
+  PTTS_HIP(hipStreamSynchronize(stream_));
+}
+
+void Engine::slot_close(int slot) {
+  PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
+  PTTS_HIP(hipSetDevice(dev_));
+  PTTS_HIP(hipStreamSynchronize(stream_));
+  SlotState s{};
+  s.eos_step = -1;
+  PTTS_HIP(hipMemcpy(st_ + slot, &s, sizeof s, hipMemcpyHostToDevice));
+}
+
+void Engine::set_latent(int slot, const float* lat) {
+  PTTS_REQUIRE(slot >= 0 && slot < max_slots_ && lat != nullptr, "bad slot / latent");
+  PTTS_HIP(hipSetDevice(dev_));
+  PTTS_HIP(hipStreamSynchronize(stream_));
+  PTTS_HIP(hipMemcpy(lat_in_ + (size_t)slot * LDIM, lat, sizeof(float) * LDIM, hipMemcpyHostToDevice));
+}
+
+}  // namespace ptts

@@ -1,0 +1,113 @@
+// Batched Pocket TTS engine: owns device weights, per-slot streaming state and the step plan.
+#pragma once
+#include <functional>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+#include "weights.h"
+
+// Immutable voice prefix (the reference's ModelState after the prompt prefill,
+// tts_model.rs:490-501 / 504-560): FlowLM KV for F conditioning positions.
+struct ptts_voice {
+  int F = 0;
+  float* kv = nullptr;      // device [NL][2][NH][F][64]
+  std::vector<float> cond;  // conditioning rows [F][1024] (kept for PCM voices)
+  const void* owner = nullptr;
+};
+
+namespace ptts {
+
+struct Op {
+  std::string name;
+  std::function<void(hipStream_t)> fn;
+  double flops = 0, bytes = 0;  // algorithmic cost of one launch (GEMM/conv ops)
+};
+
+class Engine {
+ public:
+  explicit Engine(const ptts_engine_config& cfg);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  void finalize();
+  float* blob() { return blob_; }
+  int max_slots() const { return max_slots_; }
+
+  ptts_voice* voice_from_prompt(const float* prompt, int F);
+  ptts_voice* voice_from_pcm(const float* pcm, int n);
+  void slot_open(int slot, const ptts_voice* v, const int32_t* ids, int n, const ptts_gen_params& p);
+  void slot_close(int slot);
+  void set_latent(int slot, const float* lat);
+
+  void step_async(int B);
+  void sync();
+  void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat);
+
+  double time_op(int B, const std::string& name, int reps);
+  std::vector<std::string> plan_names(int B);
+
+ private:
+  float* dalloc(size_t n);
+  const float* W(size_t off) const { return blob_ + off; }
+  void upload_weights(TensorSource* src);
+  void prefill_rows(std::vector<Op>& ops, int slot, int T, int p0);
+  void run_ops(const std::vector<Op>& ops);
+  std::vector<Op> build_step(int B);
+  void flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag);
+  void linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M, const float* Wt,
+                    int N, int K, int* S_out);
+  void conv_op(std::vector<Op>& ops, const std::string& name, const float* X, int B, int T_in, int cin, const float* H,
+               int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases, const float* bias,
+               const float* R, float* Y, int T_out, int tstride);
+  void dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N, int K,
+                const float* bias, int act, const float* rscale, const float* R, float* Y);
+  void encoder_transformer(std::vector<Op>& ops, float* x, int T, float* h, float* qkv, float* q, float* o, float* u,
+                           float* ring);
+
+  // configuration
+  int dev_ = 0, max_slots_ = 0, max_ctx_ = 0, lsd_ = 1;
+  bool own_blob_ = true, ready_ = false;
+  hipStream_t stream_ = nullptr;
+  Layout L_{};
+  float* blob_ = nullptr;
+  std::vector<void*> allocs_;
+
+  // per-slot streaming state
+  float* kv_ = nullptr;  // [(max_slots+1)][NL][2][NH][max_ctx][64] (last slot = prefill scratch)
+  long kv_slot_ = 0, kv_layer_ = 0;
+  float* ring_ = nullptr;  // [max_slots][MNL][2][MNH][RING][64]
+  long ring_slot_ = 0, ring_layer_ = 0;
+  int* fpos_ = nullptr;
+  int* mpos_ = nullptr;
+  SlotState* st_ = nullptr;
+  float *lat_in_ = nullptr, *cur_ = nullptr, *qprev_ = nullptr, *eos_ = nullptr;
+  float* hist_[8] = {};
+  int hist_T_[8] = {}, hist_C_[8] = {}, hist_P_[8] = {};
+
+  // activations
+  static constexpr int PREFILL = 256;
+  size_t pcap_ = 0;
+  float *x_ = nullptr, *h_ = nullptr, *q_ = nullptr, *o_ = nullptr, *u_ = nullptr, *partial_ = nullptr;
+  int* ids_dev_ = nullptr;
+  float *ysilu_ = nullptr, *mods_ = nullptr, *xf_ = nullptr, *hf_ = nullptr, *uf_ = nullptr;
+  float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;
+  float* a0_ = nullptr;
+  float *cb_[3] = {}, *cv_[3] = {}, *ca_[3] = {};
+  float* pcm_ = nullptr;
+  float *temb_ = nullptr, *temb_tmp_ = nullptr;
+
+  // pinned host staging
+  float* h_pcm_ = nullptr;
+  float* h_eos_ = nullptr;
+  float* h_lat_ = nullptr;
+  SlotState* h_st_ = nullptr;
+
+  std::map<int, hipGraphExec_t> graphs_;
+  std::map<int, hipGraph_t> graph_defs_;
+};
+
+}  // namespace ptts

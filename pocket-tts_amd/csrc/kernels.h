@@ -1,0 +1,171 @@
+// Device kernels of the Pocket TTS hot path (gfx950 / CDNA4), launch-side declarations.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ptts {
+
+// ---------------------------------------------------------------------------------------------
+// GEMM: Y[M][N] = epilogue(A[M][K] . W[N][K]^T), fp32 in / fp32 accumulate on
+// v_mfma_f32_32x32x2_f32 (exact fp32 FMA chain). A is either a dense row-major matrix
+// (mode 0) or the implicit im2col of a streaming conv1d over channels-last activations
+// (mode 1): row m = (b, q), k = (tap j, ci) reads X[b][q*stride + j - P][ci], or the
+// per-slot history H[b][P + t][ci] when that time index is negative (t < 0).
+// W rows are padded to a multiple of 32; K must be a multiple of 32 (and cin % 32 == 0).
+// grid = (ceil(N/32), ceil(M/32), S) ; S > 1 = split-K partial slabs (mode 0 only),
+// or the transposed-conv phase index (mode 1).
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2 };
+
+struct GemmArgs {
+  int mode;  // 0 dense, 1 conv
+  int M, N, K;
+  // A operand
+  const float* X;
+  long ldx;
+  const float* H;  // conv history [B][P][cin]
+  int P, T_in, Tq, stride_in, cin, elu_in;
+  // B operand
+  const float* W;
+  long w_phase_stride;  // floats between polyphase weight blocks (mode 1)
+  // split-K
+  int S;
+  float* partial;  // [S][M][N] when S > 1
+  // epilogue (S == 1)
+  const float* bias;
+  int act;
+  const float* R;  // residual (same row mapping as Y), may alias Y
+  long ldr;
+  const float* rscale;  // per-column scale of the update (LayerScale) or nullptr
+  float* Y;
+  long ldy;
+  int T_out, out_tstride;  // mode 1 output row = b*T_out + q*out_tstride + phase
+};
+void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// Row reduce / epilogue of a split-K GEMM, fused with residual, gate, LayerNorm and modulate:
+//   v = sum_z P[z][m][n] (+bias[n]) ; v = act(v) ; v *= gate[m][n] ; v += R[m][n] ;
+//   Y[m][n] = v ; (euler) cur[m][n] += v*euler_scale
+//   if ln: h = LN(v)*w+b (or non-affine) ; h = h*(1+mscale[m][n]) + mshift[m][n] ; H[m][n] = h
+struct RowReduceArgs {
+  const float* P;
+  int S, M, N;
+  const float* bias;
+  int act;
+  const float* gate;  // [M][ldg] or nullptr
+  long ldg;
+  const float* R;  // residual [M][ldr] or nullptr (may alias Y)
+  long ldr;
+  float* Y;  // [M][ldy] or nullptr
+  long ldy;
+  float* euler;  // cur [M][32]: cur += v * euler_scale (N must be 32)
+  float euler_scale;
+  // LayerNorm of the final row (N <= 1024)
+  int ln;
+  const float* ln_w;
+  const float* ln_b;
+  float eps;
+  const float* mshift;  // modulate (mlp.rs:135): [M][ldm] or nullptr
+  const float* mscale;
+  long ldm;
+  float* Hout;
+  long ldh;
+};
+void row_reduce(const RowReduceArgs& a, hipStream_t s);
+
+// LayerNorm over rows of width N (<= 1024), biased variance (candle_nn::LayerNorm).
+void layernorm(const float* x, long ldx, float* y, long ldy, int M, int N, const float* w, const float* b,
+               float eps, hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// Packed QKV (sum of S partials, or dense) -> RoPE(q,k) -> q to Q[M][d], k/v into the KV store.
+// Row r belongs to slot = slot0 + r / rps at position pos = (pos_arr ? pos_arr[slot] : p0) + r % rps.
+// KV layout per slot: base + slot*slot_stride + (kv*nh + h)*cap*64 + (pos % cap)*64.
+struct RowMap {
+  int slot0, rps, p0;
+  const int* pos_arr;
+};
+struct KvStore {
+  float* base;
+  long slot_stride;
+  int cap;
+};
+void qkv_rope_append(const float* P, int S, const float* dense, int M, int nh, RowMap map, KvStore kv,
+                     float* Q, hipStream_t s);
+
+// Causal (optionally windowed) softmax attention for rows mapped as above; rows are processed
+// in groups of qg (<= 16) consecutive rows of one slot. O[M][nh*64].
+void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O,
+               hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// Per-slot generation bookkeeping (device resident so the step can be replayed as a graph).
+struct SlotState {
+  int active;  // row takes part in this step
+  int step;    // generation step index within the segment
+  int eos_step;
+  int last;  // set by the step that yields the final frame
+  int frames_after_eos, max_frames;
+  float temp, eos_threshold, noise_clamp;
+  int valid;  // this step produced a frame for the row
+  unsigned long long seed;
+};
+
+// After the cond_embed|out_eos split-K GEMM: c = sum + b, eos logit, EOS state machine,
+// y_s = silu(temb[s] + c) for each lsd step, x0 noise -> cur.
+void flow_cond(const float* P, int S, int B, const float* bias, const float* temb, int lsd_steps,
+               SlotState* st, float* ysilu, float* cur, float* eos_out, hipStream_t s);
+
+// Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0.
+// latent [B][32] -> x [B*16][512], h = LN(x); qprev [B][512] carries the overlap-add history.
+void quant_upsample(const float* latent, int B, const float* emb_std, const float* emb_mean,
+                    const float* wq, const float* wup, float* qprev, const SlotState* st, float* x, float* h,
+                    const float* ln_w, const float* ln_b, hipStream_t s);
+
+// Copy the last P rows of each conv input into its history, and advance per-slot counters.
+struct HistDesc {
+  const float* src;  // [B][T][C]
+  float* dst;        // [B][P][C]
+  int T, C, P;
+};
+struct CommitArgs {
+  HistDesc h[10];
+  int nh;
+  int B;
+  SlotState* st;
+  float* latent_next;   // [B][32] backbone input for the next step
+  const float* latent;  // [B][32] this step's latent
+  int* fpos;            // FlowLM positions in cache, += 1
+  int* mpos;            // Mimi decoder positions, += 16
+};
+void step_commit(const CommitArgs& a, hipStream_t s);
+
+// TimestepEmbedder pair + RMSNorm + average (mlp.rs:76-133,296-319): out [n][512].
+// tmp: scratch [2][n][512].
+struct TimeEmbedWeights {
+  const float* l1w[2];
+  const float* l1b[2];
+  const float* l2w[2];
+  const float* l2b[2];
+  const float* alpha[2];
+};
+void time_embeddings(const TimeEmbedWeights& w, int n, float* tmp, float* out, hipStream_t s);
+
+// Token embedding gather: out[i] = table[ids[i]].
+void embed_gather(const int* ids, int n, const float* table, int dim, float* out, hipStream_t s);
+
+// Strided copy: dst[r][c] = src[r][c] for rows x cols (used for small packing jobs).
+void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, hipStream_t s);
+
+// out[m] = sum_k x[m*ldx + k] * w[k] + b  (tiny GEMV column, e.g. the N=1 final conv)
+// Streaming conv with Cout == 1: pcm[b][t] = bias + sum_{j,ci} elu(xin)[...] * w[j][ci].
+void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, const float* w, const float* bias,
+                float* Y, hipStream_t s);
+
+// Encoder first conv (Cin == 1): Y[b][t][co] = bias[co] + sum_j w[co][j] * xpad[t + j], with
+// the 6-sample zero history (constant padding, conv.py:90-108).
+void conv_cin1(const float* X, int T, int cout, int k, const float* w, const float* bias, float* Y,
+               hipStream_t s);
+
+}  // namespace ptts

@@ -1,0 +1,8 @@
+"""MI355X-native Pocket TTS (variant b6369a24): HIP engine + host mirror of the reference API."""
+
+from ._lib import FRAME, LIB_PATH, SAMPLE_RATE, PocketTTSError, lib
+from .engine import Engine, GenerationParams, StepResult, Voice
+from .tts_model import TTSModel, estimate_frames_after_eos, max_gen_len, prepare_text_prompt
+
+__all__ = ["Engine", "GenerationParams", "StepResult", "Voice", "TTSModel", "PocketTTSError", "FRAME",
+           "SAMPLE_RATE", "LIB_PATH", "lib", "prepare_text_prompt", "estimate_frames_after_eos", "max_gen_len"]

@@ -1,0 +1,110 @@
+"""ctypes binding of libpocket_tts_hip.so (include/pocket_tts.h). No CPU fallback exists:
+if the HIP library is missing or no GPU is visible, every entry point raises."""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parents[1]
+LIB_PATH = Path(os.environ.get("PTTS_LIB", PKG_ROOT / "lib" / "libpocket_tts_hip.so"))
+
+PTTS_OK = 0
+ERRORS = {1: "invalid argument", 2: "HIP error", 3: "invalid state", 4: "I/O error"}
+FRAME = 1920
+LDIM = 32
+DIM = 1024
+SAMPLE_RATE = 24000
+
+F32P = C.POINTER(C.c_float)
+U8P = C.POINTER(C.c_uint8)
+I32P = C.POINTER(C.c_int32)
+
+
+class EngineConfig(C.Structure):
+    _fields_ = [
+        ("device", C.c_int),
+        ("max_slots", C.c_int),
+        ("max_ctx", C.c_int),
+        ("lsd_decode_steps", C.c_int),
+        ("synth_seed", C.c_uint64),
+        ("weights_path", C.c_char_p),
+        ("weight_blob", C.c_void_p),
+        ("defer_weights", C.c_int),
+    ]
+
+
+class GenParams(C.Structure):
+    _fields_ = [
+        ("temp", C.c_float),
+        ("eos_threshold", C.c_float),
+        ("noise_clamp", C.c_float),
+        ("frames_after_eos", C.c_int),
+        ("max_frames", C.c_int),
+        ("seed", C.c_uint64),
+    ]
+
+
+# (name, restype, argtypes) for every symbol include/pocket_tts.h declares
+SIGNATURES = [
+    ("ptts_weight_blob_bytes", C.c_size_t, []),
+    ("ptts_engine_create", C.c_int, [C.POINTER(EngineConfig), C.POINTER(C.c_void_p)]),
+    ("ptts_engine_finalize", C.c_int, [C.c_void_p]),
+    ("ptts_engine_destroy", None, [C.c_void_p]),
+    ("ptts_engine_weight_blob", C.c_void_p, [C.c_void_p]),
+    ("ptts_voice_from_prompt", C.c_int, [C.c_void_p, F32P, C.c_int, C.POINTER(C.c_void_p)]),
+    ("ptts_voice_from_pcm", C.c_int, [C.c_void_p, F32P, C.c_int, C.POINTER(C.c_void_p)]),
+    ("ptts_voice_len", C.c_int, [C.c_void_p]),
+    ("ptts_voice_conditioning", C.c_int, [C.c_void_p, F32P, C.c_int]),
+    ("ptts_voice_destroy", None, [C.c_void_p]),
+    ("ptts_slot_open", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, I32P, C.c_int, C.POINTER(GenParams)]),
+    ("ptts_slot_close", C.c_int, [C.c_void_p, C.c_int]),
+    ("ptts_step", C.c_int, [C.c_void_p, C.c_int, F32P, U8P, U8P, F32P, F32P]),
+    ("ptts_step_async", C.c_int, [C.c_void_p, C.c_int]),
+    ("ptts_sync", C.c_int, [C.c_void_p]),
+    ("ptts_fetch", C.c_int, [C.c_void_p, C.c_int, F32P, U8P, U8P, F32P, F32P]),
+    ("ptts_slot_set_latent", C.c_int, [C.c_void_p, C.c_int, F32P]),
+    ("ptts_generate", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, I32P, C.c_int, C.POINTER(GenParams), F32P, C.c_int,
+                                C.POINTER(C.c_int)]),
+    ("ptts_time_kernel", C.c_int, [C.c_void_p, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_double)]),
+    ("ptts_plan_ops", C.c_int, [C.c_void_p, C.c_int, C.c_char_p, C.c_int]),
+    ("ptts_last_error", C.c_char_p, []),
+]
+
+_LIB: C.CDLL | None = None
+
+
+class PocketTTSError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, 'error')} ({code}): {msg}")
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"HIP extension {LIB_PATH} is missing: build it with `make -C pocket-tts_amd` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(str(LIB_PATH))
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int) -> None:
+    if rc != PTTS_OK:
+        raise PocketTTSError(rc, lib().ptts_last_error().decode(errors="replace"))
+
+
+def fptr(a):
+    return None if a is None else a.ctypes.data_as(F32P)
+
+
+def u8ptr(a):
+    return None if a is None else a.ctypes.data_as(U8P)

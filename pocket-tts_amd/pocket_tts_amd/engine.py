@@ -1,0 +1,182 @@
+"""Batched engine over the C ABI: one engine per GPU, `max_slots` concurrent utterances."""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import (DIM, FRAME, LDIM, EngineConfig, GenParams, check, fptr, lib, u8ptr)
+
+
+@dataclass
+class GenerationParams:
+    """Per-utterance knobs; field meaning follows TTSModel (tts_model.rs:22-49, 968-969)."""
+
+    temp: float = 0.7
+    eos_threshold: float = -4.0
+    noise_clamp: float | None = None
+    frames_after_eos: int = 3
+    max_frames: int = 250
+    seed: int = 0
+
+    def to_c(self) -> GenParams:
+        return GenParams(float(self.temp), float(self.eos_threshold),
+                         float(self.noise_clamp) if self.noise_clamp is not None else 0.0,
+                         int(self.frames_after_eos), int(self.max_frames), int(self.seed) & (2**64 - 1))
+
+
+class Voice:
+    """Immutable FlowLM KV prefix of a voice prompt (the reference's ModelState)."""
+
+    def __init__(self, engine: "Engine", handle: int):
+        self._engine = engine
+        self.handle = C.c_void_p(handle)
+
+    @property
+    def n_frames(self) -> int:
+        return lib().ptts_voice_len(self.handle)
+
+    def conditioning(self) -> np.ndarray:
+        out = np.zeros((self.n_frames, DIM), np.float32)
+        check(lib().ptts_voice_conditioning(self.handle, fptr(out), out.shape[0]))
+        return out
+
+    def close(self):
+        if self.handle:
+            lib().ptts_voice_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class StepResult:
+    pcm: np.ndarray  # [n_rows, 1920]
+    valid: np.ndarray  # [n_rows] bool, row produced a frame this step
+    last: np.ndarray  # [n_rows] bool, that frame was the row's final one
+    eos_logits: np.ndarray  # [n_rows]
+    latents: np.ndarray  # [n_rows, 32]
+
+
+class Engine:
+    def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
+                 seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
+                 defer_weights: bool = False):
+        cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
+                           weights_path.encode() if weights_path else None,
+                           C.c_void_p(weight_blob) if weight_blob else None, int(defer_weights))
+        h = C.c_void_p()
+        check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
+        self.handle = h
+        self.max_slots = max_slots
+        self.max_ctx = max_ctx
+        self.lsd_decode_steps = lsd_decode_steps
+
+    @staticmethod
+    def weight_blob_bytes() -> int:
+        return int(lib().ptts_weight_blob_bytes())
+
+    def weight_blob(self) -> int:
+        return int(lib().ptts_engine_weight_blob(self.handle) or 0)
+
+    def finalize(self):
+        check(lib().ptts_engine_finalize(self.handle))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().ptts_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- voices
+    def voice_from_prompt(self, prompt: np.ndarray) -> Voice:
+        p = np.ascontiguousarray(prompt, np.float32).reshape(-1, DIM)
+        h = C.c_void_p()
+        check(lib().ptts_voice_from_prompt(self.handle, fptr(p), p.shape[0], C.byref(h)))
+        return Voice(self, h.value)
+
+    def voice_from_pcm(self, pcm: np.ndarray) -> Voice:
+        x = np.ascontiguousarray(pcm, np.float32).reshape(-1)
+        h = C.c_void_p()
+        check(lib().ptts_voice_from_pcm(self.handle, fptr(x), x.size, C.byref(h)))
+        return Voice(self, h.value)
+
+    # -- slots
+    def open(self, slot: int, voice: Voice, ids, params: GenerationParams):
+        a = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1))
+        cp = params.to_c()
+        check(lib().ptts_slot_open(self.handle, slot, voice.handle, a.ctypes.data_as(C.POINTER(C.c_int32)), a.size,
+                                   C.byref(cp)))
+
+    def close_slot(self, slot: int):
+        check(lib().ptts_slot_close(self.handle, slot))
+
+    def set_latent(self, slot: int, latent: np.ndarray):
+        v = np.ascontiguousarray(latent, np.float32).reshape(LDIM)
+        check(lib().ptts_slot_set_latent(self.handle, slot, fptr(v)))
+
+    # -- the batched hot path
+    def step(self, n_rows: int) -> StepResult:
+        r = StepResult(np.zeros((n_rows, FRAME), np.float32), np.zeros(n_rows, np.uint8), np.zeros(n_rows, np.uint8),
+                       np.zeros(n_rows, np.float32), np.zeros((n_rows, LDIM), np.float32))
+        check(lib().ptts_step(self.handle, n_rows, fptr(r.pcm), u8ptr(r.valid), u8ptr(r.last), fptr(r.eos_logits),
+                              fptr(r.latents)))
+        r.valid = r.valid.astype(bool)
+        r.last = r.last.astype(bool)
+        return r
+
+    def step_async(self, n_rows: int):
+        check(lib().ptts_step_async(self.handle, n_rows))
+
+    def sync(self):
+        check(lib().ptts_sync(self.handle))
+
+    def fetch(self, n_rows: int) -> StepResult:
+        r = StepResult(np.zeros((n_rows, FRAME), np.float32), np.zeros(n_rows, np.uint8), np.zeros(n_rows, np.uint8),
+                       np.zeros(n_rows, np.float32), np.zeros((n_rows, LDIM), np.float32))
+        check(lib().ptts_fetch(self.handle, n_rows, fptr(r.pcm), u8ptr(r.valid), u8ptr(r.last), fptr(r.eos_logits),
+                               fptr(r.latents)))
+        r.valid = r.valid.astype(bool)
+        r.last = r.last.astype(bool)
+        return r
+
+    def generate(self, slot: int, voice: Voice, ids, params: GenerationParams) -> np.ndarray:
+        a = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1))
+        cap = params.max_frames * FRAME
+        out = np.zeros(cap, np.float32)
+        n = C.c_int(0)
+        cp = params.to_c()
+        check(lib().ptts_generate(self.handle, slot, voice.handle, a.ctypes.data_as(C.POINTER(C.c_int32)), a.size,
+                                  C.byref(cp), fptr(out), cap, C.byref(n)))
+        return out[: n.value]
+
+    # -- measurement
+    def plan(self, n_rows: int) -> list[tuple[str, float, float]]:
+        """The step plan: (op name, algorithmic flops, algorithmic bytes) per launch."""
+        buf = C.create_string_buffer(1 << 17)
+        check(lib().ptts_plan_ops(self.handle, n_rows, buf, len(buf)))
+        out = []
+        for line in buf.value.decode().split("\n"):
+            if line:
+                name, fl, by = line.split("\t")
+                out.append((name, float(fl), float(by)))
+        return out
+
+    def plan_ops(self, n_rows: int) -> list[str]:
+        return [n for n, _, _ in self.plan(n_rows)]
+
+    def time_kernel(self, n_rows: int, name: str, reps: int = 50) -> float:
+        us = C.c_double(0)
+        check(lib().ptts_time_kernel(self.handle, n_rows, name.encode(), reps, C.byref(us)))
+        return us.value

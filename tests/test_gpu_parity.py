@@ -1,0 +1,197 @@
+"""GPU parity: the HIP engine through the C ABI against the reference's golden vectors
+(tests/golden, produced by the reference's own Python modules) and the C oracle.
+
+Tolerances (north_star: latents/codes at temperature 0, PCM within 1e-4 RMS):
+  eos logit and latent  <= 1e-4 max abs
+  PCM                   <= 1e-4 RMS of the difference, 1e-3 max abs
+All arithmetic is fp32 on both sides; differences are reduction order only."""
+
+import numpy as np
+import pytest
+from conftest import load_golden, rms
+
+pytestmark = pytest.mark.gpu
+
+INF = float("inf")
+
+
+def params(**kw):
+    from pocket_tts_amd import GenerationParams
+
+    base = dict(temp=0.0, eos_threshold=INF, noise_clamp=None, frames_after_eos=3, max_frames=64, seed=1)
+    base.update(kw)
+    return GenerationParams(**base)
+
+
+def check_step(r, row, d, i):
+    assert r.valid[row]
+    assert abs(r.eos_logits[row] - d["eos_logit"][i]) <= 1e-4, (i, r.eos_logits[row], d["eos_logit"][i])
+    np.testing.assert_allclose(r.latents[row], d["latent"][i], atol=1e-4)
+    diff = r.pcm[row] - d["pcm"][i]
+    assert rms(diff) <= 1e-4 and np.abs(diff).max() <= 1e-3, (i, rms(diff), np.abs(diff).max())
+
+
+def test_e2e_matches_reference_golden(gpu_engine):
+    d = load_golden("e2e_lsd1.safetensors")
+    v = gpu_engine.voice_from_prompt(d["prompt"])
+    assert v.n_frames == d["prompt"].shape[0]
+    n = d["latent"].shape[0]
+    gpu_engine.open(0, v, d["text_ids"], params(max_frames=n))
+    for i in range(n):
+        r = gpu_engine.step(1)
+        check_step(r, 0, d, i)
+        assert bool(r.last[0]) == (i == n - 1)
+    r = gpu_engine.step(1)
+    assert not r.valid[0]
+
+
+def test_e2e_lsd2_matches_reference_golden():
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd2.safetensors")
+    eng = pt.Engine(device=0, max_slots=1, max_ctx=128, lsd_decode_steps=2, seed=0x5EED)
+    try:
+        v = eng.voice_from_prompt(d["prompt"])
+        eng.open(0, v, d["text_ids"], params(max_frames=8))
+        for i in range(d["latent"].shape[0]):
+            check_step(eng.step(1), 0, d, i)
+    finally:
+        eng.close()
+
+
+def test_voice_cloning_encoder_matches_reference(gpu_engine):
+    d = load_golden("encoder_4f.safetensors")
+    v = gpu_engine.voice_from_pcm(d["pcm"])
+    assert v.n_frames == 4
+    np.testing.assert_allclose(v.conditioning(), d["conditioning"], atol=1e-5)
+
+
+def test_ragged_batch_matches_oracle(gpu_engine, oracle):
+    """8 slots with different voice lengths and text lengths (ragged KV positions) stepped
+    together; every row must equal its own single-utterance oracle run."""
+    d = load_golden("e2e_lsd1.safetensors")
+    rng = np.random.default_rng(7)
+    B, steps = 8, 4
+    orc, voices = [], []
+    for b in range(B):
+        F = 4 + 3 * b
+        prompt = (d["prompt"][:F] * (1.0 + 0.1 * b)).astype(np.float32)
+        ids = rng.integers(0, 4000, size=2 + b).astype(np.int32)
+        v = gpu_engine.voice_from_prompt(prompt)
+        voices.append(v)
+        gpu_engine.open(b, v, ids, params(max_frames=steps))
+        s = oracle.new_state(128)
+        s.prefill(prompt)
+        s.prefill_tokens(ids)
+        orc.append(s)
+    lat = [None] * B
+    for i in range(steps):
+        r = gpu_engine.step(B)
+        for b in range(B):
+            o = orc[b].step(lat[b])
+            lat[b] = o["latent"]
+            assert r.valid[b]
+            assert abs(r.eos_logits[b] - o["eos_logit"]) <= 1e-4
+            np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
+            assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+
+
+def test_eos_termination_rule(gpu_engine):
+    """tts_model.rs:1055-1063: the step reaching eos_step + frames_after_eos is yielded and is
+    the last; without EOS the segment ends after max_gen_len frames."""
+    d = load_golden("e2e_lsd1.safetensors")
+    logits = d["eos_logit"]
+    v = gpu_engine.voice_from_prompt(d["prompt"])
+    for thr, fae, max_frames in [(-0.5, 2, 12), (-0.36, 1, 12), (10.0, 3, 5), (-0.6, 0, 12)]:
+        above = np.nonzero(logits > thr)[0]
+        assert np.min(np.abs(logits - thr)) > 1e-3
+        expect = min(above[0] + fae + 1, max_frames) if above.size else max_frames
+        gpu_engine.open(0, v, d["text_ids"], params(eos_threshold=thr, frames_after_eos=fae, max_frames=max_frames))
+        got = 0
+        while True:
+            r = gpu_engine.step(1)
+            if not r.valid[0]:
+                break
+            got += 1
+            if r.last[0]:
+                break
+            assert got < 50
+        assert got == expect, (thr, fae, got, expect)
+
+
+def _mix64(z):
+    z = np.uint64(z)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def _normal_at(seed, step, k, att):
+    M = 2**64
+    base = _mix64((seed * 0x9E3779B97F4A7C15 + step * 0xD1B54A32D192ED03 + (k * 64 + att) * 0x8CB92BA72F3D8DD7) % M)
+    f = np.float32
+    u1 = (f(int(base) >> 41) + f(0.5)) * f(1.0 / 8388608.0)
+    u2 = f(int(_mix64(int(base) ^ 0x5851F42D4C957F2D)) >> 40) * f(1.0 / 16777216.0)
+    return np.sqrt(f(-2.0) * np.log(u1)) * np.cos(f(6.283185307179586) * u2)
+
+
+def _noise(seed, step, temp, clamp):
+    sd = np.sqrt(np.float32(temp))
+    out = np.zeros(32, np.float32)
+    for k in range(32):
+        x = sd * _normal_at(seed, step, k, 0)
+        if clamp:
+            att = 1
+            while abs(x) > clamp and att < 64:
+                x = sd * _normal_at(seed, step, k, att)
+                att += 1
+            x = min(max(x, -clamp), clamp)
+        out[k] = x
+    return out
+
+
+@pytest.mark.parametrize("clamp", [None, 0.5])
+def test_temperature_sampling_matches_oracle(gpu_engine, oracle, clamp):
+    """temp > 0: the engine's counter-based N(0, sqrt(temp)) (optionally truncated,
+    flow_lm.rs:39-65) replayed on the host and fed to the oracle as x_0."""
+    d = load_golden("e2e_lsd1.safetensors")
+    seed, temp = 1234, 0.7
+    v = gpu_engine.voice_from_prompt(d["prompt"][:10])
+    gpu_engine.open(0, v, d["text_ids"][:5], params(temp=temp, noise_clamp=clamp, seed=seed, max_frames=4))
+    s = oracle.new_state(64)
+    s.prefill(d["prompt"][:10])
+    s.prefill_tokens(d["text_ids"][:5])
+    lat = None
+    for i in range(3):
+        r = gpu_engine.step(1)
+        o = s.step(lat, noise=_noise(seed, i, temp, clamp))
+        lat = o["latent"]
+        np.testing.assert_allclose(r.latents[0], o["latent"], atol=1e-4)
+        assert rms(r.pcm[0] - o["pcm"]) <= 1e-4
+
+
+def test_steps_are_deterministic_and_slots_reset(gpu_engine):
+    d = load_golden("e2e_lsd1.safetensors")
+    v = gpu_engine.voice_from_prompt(d["prompt"])
+    runs = []
+    for _ in range(2):
+        gpu_engine.open(3, v, d["text_ids"], params(max_frames=3))
+        runs.append(np.stack([gpu_engine.step(4).pcm[3] for _ in range(3)]))
+    assert np.array_equal(runs[0], runs[1])
+    np.testing.assert_allclose(runs[0], d["pcm"][:3], atol=1e-3)
+
+
+def test_generate_convenience(gpu_engine):
+    d = load_golden("e2e_lsd1.safetensors")
+    v = gpu_engine.voice_from_prompt(d["prompt"])
+    pcm = gpu_engine.generate(0, v, d["text_ids"], params(eos_threshold=-4.0, frames_after_eos=2, max_frames=12))
+    # EOS fires at step 0 (every golden logit > -4), so frames 0..2 are produced
+    assert pcm.size == 3 * 1920
+    assert rms(pcm - d["pcm"][:3].reshape(-1)) <= 1e-4
+
+
+def test_plan_and_kernel_timer(gpu_engine):
+    names = gpu_engine.plan_ops(8)
+    assert "flow.l0.qkv_gemm" in names and "seanet.conv0" in names and names[-1] == "commit"
+    assert gpu_engine.time_kernel(8, "flow.l0.ff1_gemm", reps=5) > 0
