@@ -70,7 +70,7 @@ class Engine:
                  defer_weights: bool = False):
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
-                           C.c_void_p(weight_blob) if weight_blob else None, int(defer_weights))
+                           weight_blob or None, int(defer_weights))
         h = C.c_void_p()
         check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
         self.handle = h
