@@ -86,7 +86,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
   q_ = dalloc((size_t)R * D);
   o_ = dalloc((size_t)R * D);
   u_ = dalloc((size_t)R * FF);
-  pcap_ = (size_t)4 << 20;
+  // split-K slabs: skinny FlowLM/head GEMMs, and the 2-way split Mimi QKV (B*16 rows x 1536)
+  pcap_ = std::max((size_t)4 << 20, (size_t)2 * B * UP * 3 * MD);
   partial_ = dalloc(pcap_);
   ids_dev_ = (int*)dalloc(PREFILL);
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
@@ -175,13 +176,22 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
                           const float* Wt, int N, int K, int* S_out) {
   PTTS_REQUIRE(K % 32 == 0, "GEMM K must be a multiple of 32");
   int S = pick_splits(M, N, K);
+  int layout = 0;
+  // wide skinny GEMMs (FlowLM qkv/ff1, flow-head adaLN): 32x128 LDS-DMA tiles, 8-way split-K
+  // (tools/gemm_bench.hip on MI355X: qkv 6.7 -> 6.3 us, ff1 7.9 -> 6.5 us, ada 10.1 -> 8.7 us)
+  if (M <= 64 && N >= 3072) {
+    layout = 13;
+    S = std::max(1, std::min(8, K / 64));
+  }
   while (S > 1 && (size_t)S * M * N > pcap_) --S;
   PTTS_REQUIRE((size_t)S * M * N <= pcap_, "split-K partial buffer too small");
   GemmArgs a{};
   a.mode = 0;
+  a.layout = layout;
   a.M = M;
   a.N = N;
   a.K = K;
+  a.Nw = (N + 31) / 32 * 32;
   a.X = X;
   a.ldx = ldx;
   a.W = Wt;
@@ -193,13 +203,16 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
 }
 
 void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,
-                      int K, const float* bias, int act, const float* rscale, const float* R, float* Y) {
+                      int K, const float* bias, int act, const float* rscale, const float* R, float* Y, int layout) {
   PTTS_REQUIRE(K % 32 == 0, "GEMM K must be a multiple of 32");
+  PTTS_REQUIRE(layout != 15 || K % 64 == 0, "layout 15 needs K % 64 == 0");
   GemmArgs a{};
   a.mode = 0;
+  a.layout = layout;
   a.M = M;
   a.N = N;
   a.K = K;
+  a.Nw = (N + 31) / 32 * 32;
   a.X = X;
   a.ldx = K;
   a.W = Wt;
@@ -217,14 +230,16 @@ void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float
 
 void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float* X, int B, int T_in, int cin,
                      const float* H, int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases,
-                     const float* bias, const float* R, float* Y, int T_out, int tstride) {
+                     const float* bias, const float* R, float* Y, int T_out, int tstride, int layout) {
   PTTS_REQUIRE(cin % 32 == 0, "conv cin must be a multiple of 32");
   GemmArgs a{};
   a.mode = 1;
+  a.layout = layout;
   a.Tq = T_in / stride;
   a.M = B * a.Tq;
   a.N = cout;
   a.K = ktaps * cin;
+  a.Nw = (cout + 31) / 32 * 32;
   a.X = X;
   a.ldx = cin;
   a.H = H;
@@ -459,8 +474,31 @@ std::vector<Op> Engine::build_step(int B) {
     const Layout::TL& t = L_.mdec[l];
     const std::string p = "mimi.l" + std::to_string(l);
     KvStore kv{ring_ + (long)l * ring_layer_, ring_slot_, RING};
-    dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_);
-    {
+    // fat GEMMs (B*16 rows): 64x64 LDS-DMA tiles once there are enough rows to fill the chip;
+    // QKV runs 2-way split-K and the RoPE/append kernel sums the two slabs
+    const bool fat = MR >= 256;
+    if (fat) {
+      int S = 2;
+      GemmArgs a{};
+      a.mode = 0;
+      a.layout = 12;
+      a.M = MR;
+      a.N = 3 * MD;
+      a.K = MD;
+      a.Nw = 3 * MD;
+      a.X = mh_;
+      a.ldx = MD;
+      a.W = W(t.in_proj);
+      a.S = S;
+      a.partial = partial_;
+      PTTS_REQUIRE((size_t)S * MR * 3 * MD <= pcap_, "split-K partial buffer too small");
+      ops.push_back({p + ".qkv_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * 3 * MD * MD,
+                     4.0 * (3.0 * MD * MD + (double)MR * MD + (double)S * MR * 3 * MD)});
+      const float* P = partial_;
+      float* Q = mq_;
+      ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(P, S, nullptr, MR, MNH, mmap, kv, Q, s); }});
+    } else {
+      dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_);
       const float* qkv = mqkv_;
       float* Q = mq_;
       ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(nullptr, 0, qkv, MR, MNH, mmap, kv, Q, s); }});
@@ -476,7 +514,8 @@ std::vector<Op> Engine::build_step(int B) {
       float* h = mh_;
       ops.push_back({p + ".ln2", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
     }
-    dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_);
+    dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
+             fat ? 15 : 0);
     dense_op(ops, p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, nullptr, ACT_NONE, W(t.ls2), mx_, mx_);
     if (l + 1 < MNL) {
       const float *x = mx_, *w = W(L_.mdec[l + 1].n1w), *b = W(L_.mdec[l + 1].n1b);
@@ -492,14 +531,20 @@ std::vector<Op> Engine::build_step(int B) {
   for (int i = 0; i < 3; ++i) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
+    // per-stage tile choice (tools/gemm_bench.hip at B=32): the short-K, many-row late stages
+    // run the LDS-DMA kernels; the first stage keeps the K-split register kernel
+    const bool big = B >= 16;
+    const int l_tr = big ? (i == 1 ? 13 : (i == 2 ? 6 : 0)) : 0;
+    const int l_r3 = big && i == 2 ? 14 : 0;
+    const int l_r1 = big && i == 2 ? 6 : 0;
     conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 1, W(L_.dtr_w[i]), ch / 2, 2, r,
-            W(L_.dtr_b[i]), nullptr, cb_[i], T * r, r);
+            W(L_.dtr_b[i]), nullptr, cb_[i], T * r, r, l_tr);
     T *= r;
     ch /= 2;
     conv_op(ops, p + ".res_conv3", cb_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 1, W(L_.dra_w[i]), ch / 2, 3, 1,
-            W(L_.dra_b[i]), nullptr, cv_[i], T, 1);
+            W(L_.dra_b[i]), nullptr, cv_[i], T, 1, l_r3);
     conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 1, W(L_.drb_w[i]), ch, 1, 1, W(L_.drb_b[i]),
-            cb_[i], ca_[i], T, 1);
+            cb_[i], ca_[i], T, 1, l_r1);
     cin_buf = ca_[i];
   }
   {

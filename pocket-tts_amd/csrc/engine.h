@@ -62,9 +62,10 @@ class Engine {
                     int N, int K, int* S_out);
   void conv_op(std::vector<Op>& ops, const std::string& name, const float* X, int B, int T_in, int cin, const float* H,
                int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases, const float* bias,
-               const float* R, float* Y, int T_out, int tstride);
+               const float* R, float* Y, int T_out, int tstride, int layout = 0);
   void dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N, int K,
-                const float* bias, int act, const float* rscale, const float* R, float* Y);
+                const float* bias, int act, const float* rscale, const float* R, float* Y,
+                int layout = 0);
   void encoder_transformer(std::vector<Op>& ops, float* x, int T, float* h, float* qkv, float* q, float* o, float* u,
                            float* ring);
 

@@ -18,8 +18,10 @@ namespace ptts {
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2 };
 
 struct GemmArgs {
-  int mode;  // 0 dense, 1 conv
+  int mode;    // 0 dense, 1 conv
+  int layout;  // workgroup layout, see kernels.hip (0 ksplit 32x32, 1: 64x64, 2: 32x128, 3: 128x32)
   int M, N, K;
+  int Nw;  // rows present in W (N rounded up to 32)
   // A operand
   const float* X;
   long ldx;

@@ -44,13 +44,28 @@ __device__ __forceinline__ float wave_max(float v) {
 // Lane (r, h) loads 16 consecutive k of its A row and of its W row (k0 + 16h ... +15);
 // MFMA #j of a chunk consumes element j of both, i.e. k-pair {k0 + j, k0 + 16 + j}.
 // =============================================================================================
-template <int MODE>
+// Workgroup layouts (4 waves, each accumulating one 32x32 tile):
+//   LAYOUT 0  "ksplit": WG tile 32x32, the tile's K chunks dealt round-robin to the 4 waves,
+//             partial tiles summed through LDS (skinny M <= 32 GEMMs: more waves per tile)
+//   LAYOUT 1  2x2 waves = WG tile 64x64     LAYOUT 2  1x4 = 32x128     LAYOUT 3  4x1 = 128x32
+//   (each wave runs the whole K chain of its z-slice; neighbours share A rows / W rows in L1/L2)
+template <int LAYOUT>
+struct Lay {
+  static constexpr int WM = LAYOUT == 1 ? 2 : (LAYOUT == 3 ? 4 : 1);
+  static constexpr int WN = LAYOUT == 1 ? 2 : (LAYOUT == 2 ? 4 : 1);
+};
+
+template <int MODE, int LAYOUT>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
-  __shared__ float red[4 * 16 * 64];
+  __shared__ float red[LAYOUT == 0 ? 4 * 16 * 64 : 1];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  // wave-uniform (SGPR) so that the chunk loop is a scalar loop: no exec-masked joins, and
+  // the compiler can keep the next chunk's loads in flight across the MFMAs (counted vmcnt)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32, z = blockIdx.z;
+  constexpr int WM = Lay<LAYOUT>::WM, WN = Lay<LAYOUT>::WN;
+  const int wm = LAYOUT == 0 ? 0 : wave / WN, wn = LAYOUT == 0 ? 0 : wave % WN;
+  const int n0 = (blockIdx.x * WN + wn) * 32, m0 = (blockIdx.y * WM + wm) * 32, z = blockIdx.z;
   const int nchunks = a.K >> 5;
   int cb = 0, ce = nchunks, phase = 0;
   if (MODE == 0) {
@@ -59,7 +74,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
   } else {
     phase = z;
   }
-  const float* wrow = a.W + (long)phase * a.w_phase_stride + (long)(n0 + r) * a.K + 16 * h;
+  // waves whose tile lies wholly outside W's padded rows or outside M have nothing to do
+  // (wave-uniform; LAYOUT 0 never has such waves)
+  const bool wave_live = n0 < a.Nw && m0 < a.M;
+  const float* wrow = a.W + (long)phase * a.w_phase_stride + (long)(wave_live ? n0 + r : r) * a.K + 16 * h;
   const int m = m0 + r;
   const bool mvalid = m < a.M;
   const float* xrow = nullptr;
@@ -84,57 +102,408 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 #pragma unroll
   for (int g = 0; g < 16; ++g) acc[g] = 0.f;
 
-  float4 av[4], bv[4], an[4], bn[4];
-  int c = cb + wave;
-  if (c < ce) {
-    const float* ap = a_ptr(c << 5);
+  // Rows >= M were clamped to a valid row above: their garbage only reaches output rows that
+  // are never stored, so the loads are unconditional (no exec-masked branches around them).
+  (void)mvalid;
+  const bool elu = MODE == 1 && a.elu_in;
+  auto load = [&](int cc, float4 (&A)[4], float4 (&Bv)[4]) {
+    const float* ap = a_ptr(cc << 5);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      bv[i] = *reinterpret_cast<const float4*>(wrow + (c << 5) + 4 * i);
-      av[i] = mvalid ? *reinterpret_cast<const float4*>(ap + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      Bv[i] = *reinterpret_cast<const float4*>(wrow + (cc << 5) + 4 * i);
+      A[i] = *reinterpret_cast<const float4*>(ap + 4 * i);
     }
-  }
-  for (; c < ce; c += 4) {
-    const int cn = c + 4;
-    if (cn < ce) {  // prefetch the wave's next chunk while this one is multiplied
-      const float* ap = a_ptr(cn << 5);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        bn[i] = *reinterpret_cast<const float4*>(wrow + (cn << 5) + 4 * i);
-        an[i] = mvalid ? *reinterpret_cast<const float4*>(ap + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
+  };
+  auto mma = [&](float4 (&A)[4], float4 (&Bv)[4]) {
     float af[16], bf[16];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      af[4 * i + 0] = av[i].x; af[4 * i + 1] = av[i].y; af[4 * i + 2] = av[i].z; af[4 * i + 3] = av[i].w;
-      bf[4 * i + 0] = bv[i].x; bf[4 * i + 1] = bv[i].y; bf[4 * i + 2] = bv[i].z; bf[4 * i + 3] = bv[i].w;
+      af[4 * i + 0] = A[i].x; af[4 * i + 1] = A[i].y; af[4 * i + 2] = A[i].z; af[4 * i + 3] = A[i].w;
+      bf[4 * i + 0] = Bv[i].x; bf[4 * i + 1] = Bv[i].y; bf[4 * i + 2] = Bv[i].z; bf[4 * i + 3] = Bv[i].w;
     }
-    if (MODE == 1 && a.elu_in) {
+    if (elu) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) af[j] = elu1(af[j]);
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      av[i] = an[i];
-      bv[i] = bn[i];
+  };
+  // ping-pong register sets: chunk c is multiplied while chunk c+CSTEP is in flight
+  float4 a0[4], b0[4], a1[4], b1[4];
+  constexpr int CSTEP = LAYOUT == 0 ? 4 : 1;
+  int c = LAYOUT == 0 ? cb + wave : cb;
+  if (!wave_live) c = ce;
+  // The prefetch is unconditional (past the end it re-reads the last chunk, never used), so no
+  // control-flow join sits between a load and the MFMAs that must not wait for it.
+  if (c < ce) {
+    load(c, a0, b0);
+    for (;;) {
+      const int c1 = c + CSTEP;
+      load(c1 < ce ? c1 : c, a1, b1);
+      mma(a0, b0);
+      if (c1 >= ce) break;
+      const int c2 = c1 + CSTEP;
+      load(c2 < ce ? c2 : c1, a0, b0);
+      mma(a1, b1);
+      if (c2 >= ce) break;
+      c = c2;
     }
   }
 
-#pragma unroll
-  for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[g];
-  __syncthreads();
-#pragma unroll
-  for (int gg = 0; gg < 4; ++gg) {
-    const int g = wave * 4 + gg;
-    float v = red[(0 * 16 + g) * 64 + lane] + red[(1 * 16 + g) * 64 + lane];
-    v += red[(2 * 16 + g) * 64 + lane];
-    v += red[(3 * 16 + g) * 64 + lane];
+  auto store = [&](int g, float v) {
     const int row = m0 + (g & 3) + 8 * (g >> 2) + 4 * h;
     const int col = n0 + r;
+    if (row >= a.M || col >= a.N) return;
+    if (a.partial) {
+      a.partial[((long)z * a.M + row) * a.N + col] = v;
+      return;
+    }
+    if (a.bias) v += a.bias[col];
+    if (a.act == ACT_GELU) v = gelu_tanh(v);
+    else if (a.act == ACT_SILU) v = silu(v);
+    long yrow = row;
+    if (MODE == 1) {
+      const int b2 = row / a.Tq;
+      const int q2 = row - b2 * a.Tq;
+      yrow = (long)b2 * a.T_out + (long)q2 * a.out_tstride + phase;
+    }
+    if (a.rscale) v *= a.rscale[col];
+    if (a.R) v += a.R[yrow * a.ldr + col];
+    a.Y[yrow * a.ldy + col] = v;
+  };
+  if (LAYOUT == 0) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[g];
+    __syncthreads();
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int g = wave * 4 + gg;
+      float v = red[(0 * 16 + g) * 64 + lane] + red[(1 * 16 + g) * 64 + lane];
+      v += red[(2 * 16 + g) * 64 + lane];
+      v += red[(3 * 16 + g) * 64 + lane];
+      store(g, v);
+    }
+  } else if (wave_live) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) store(g, acc[g]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-staged variant: operands are fetched with fully coalesced float4 loads (8 lanes cover one
+// 128-byte row segment of a 32-wide K chunk), written to LDS rows padded to 36 floats
+// (conflict-free ds_read_b128 in the MFMA fragment order), and read back per lane as the
+// 32x32x2 fragments. The next chunk's global loads are in flight while the current one is
+// multiplied.
+//   SHARED 0 (layout 4): WG tile 32x32, 4 waves split K, wave-private LDS, LDS reduce at the end.
+//   SHARED 1 (layout 5): WG tile 64x64, 2x2 waves share the A/B chunk through double-buffered
+//                        LDS (one barrier per chunk), each wave runs the full K chain.
+// ---------------------------------------------------------------------------------------------
+constexpr int LROW = 36;  // padded LDS row (floats)
+
+template <int MODE, int SHARED>
+__global__ __launch_bounds__(256) void k_gemm_lds(GemmArgs a) {
+  // SHARED 0: 4 waves x (A 32 rows + B 32 rows) x LROW ; SHARED 1: 2 buffers x (A 64 + B 64) x LROW
+  __shared__ __attribute__((aligned(16))) float lds[SHARED ? 2 * 128 * LROW : 4 * 64 * LROW];
+  __shared__ float red[SHARED ? 1 : 4 * 16 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int TM = SHARED ? 64 : 32, TN = SHARED ? 64 : 32;
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM, z = blockIdx.z;
+  const int nchunks = a.K >> 5;
+  int cb = 0, ce = nchunks, phase = 0;
+  if (MODE == 0) {
+    cb = (int)((long)nchunks * z / a.S);
+    ce = (int)((long)nchunks * (z + 1) / a.S);
+  } else {
+    phase = z;
+  }
+  const float* W = a.W + (long)phase * a.w_phase_stride;
+  // loader mapping: row = base + lane/8 (+8 per instruction), 4 floats at col 4*(lane&7)
+  const int lrow = SHARED ? (tid >> 3) : (lane >> 3);  // 0..31 (SHARED) / 0..7 (per wave)
+  const int lcol = 4 * (tid & 7);
+  constexpr int NLD = SHARED ? 2 : 4;  // float4 loads per operand per chunk per thread
+  constexpr int RSTEP = SHARED ? 32 : 8;
+  // A and W rows this thread loads
+  const float* wp[NLD];
+  bool wv[NLD];
+  const float* ap_dense[NLD];
+  int abq[NLD], aqq[NLD];
+  bool av_ok[NLD];
+#pragma unroll
+  for (int i = 0; i < NLD; ++i) {
+    const int row = lrow + RSTEP * i;
+    const int m = m0 + row;
+    av_ok[i] = m < a.M;
+    const int mm = av_ok[i] ? m : 0;
+    if (MODE == 0) {
+      ap_dense[i] = a.X + (long)mm * a.ldx + lcol;
+    } else {
+      abq[i] = mm / a.Tq;
+      aqq[i] = mm - abq[i] * a.Tq;
+    }
+    const int n = n0 + row;
+    wv[i] = n < a.Nw;
+    wp[i] = W + (long)(wv[i] ? n : 0) * a.K + lcol;
+  }
+  auto a_src = [&](int i, int k0) -> const float* {
+    if (MODE == 0) return ap_dense[i] + k0;
+    const int j = k0 / a.cin;
+    const int ci = k0 - j * a.cin + lcol;
+    const int t = aqq[i] * a.stride_in + j - a.P;
+    if (t >= 0) return a.X + ((long)abq[i] * a.T_in + t) * a.ldx + ci;
+    return a.H + ((long)abq[i] * a.P + (a.P + t)) * a.cin + ci;
+  };
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 ra[NLD], rb[NLD];
+  auto gload = [&](int c) {
+    const int k0 = c << 5;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      ra[i] = av_ok[i] ? *reinterpret_cast<const float4*>(a_src(i, k0)) : zero4;
+      rb[i] = wv[i] ? *reinterpret_cast<const float4*>(wp[i] + k0) : zero4;
+      if (MODE == 1 && a.elu_in)
+        ra[i] = make_float4(elu1(ra[i].x), elu1(ra[i].y), elu1(ra[i].z), elu1(ra[i].w));
+    }
+  };
+  // LDS regions
+  const int wm = SHARED ? wave >> 1 : 0, wn = SHARED ? wave & 1 : 0;
+  auto lds_a = [&](int buf) -> float* { return SHARED ? lds + buf * 128 * LROW : lds + wave * 64 * LROW; };
+  auto lds_b = [&](int buf) -> float* { return lds_a(buf) + (SHARED ? 64 : 32) * LROW; };
+
+  floatx16 acc;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+  const int cstep = SHARED ? 1 : 4;
+  int c = SHARED ? cb : cb + wave;
+  int buf = 0;
+  if (c < ce) gload(c);
+  for (; c < ce; c += cstep) {
+    float* la = lds_a(buf);
+    float* lb = lds_b(buf);
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      *reinterpret_cast<float4*>(la + (lrow + RSTEP * i) * LROW + lcol) = ra[i];
+      *reinterpret_cast<float4*>(lb + (lrow + RSTEP * i) * LROW + lcol) = rb[i];
+    }
+    if (SHARED) __syncthreads();
+    if (c + cstep < ce) gload(c + cstep);
+    float af[16], bf[16];
+    const float* pa = la + (32 * wm + r) * LROW + 16 * h;
+    const float* pb = lb + (32 * wn + r) * LROW + 16 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 x = *reinterpret_cast<const float4*>(pa + 4 * i);
+      const float4 y = *reinterpret_cast<const float4*>(pb + 4 * i);
+      af[4 * i + 0] = x.x; af[4 * i + 1] = x.y; af[4 * i + 2] = x.z; af[4 * i + 3] = x.w;
+      bf[4 * i + 0] = y.x; bf[4 * i + 1] = y.y; bf[4 * i + 2] = y.z; bf[4 * i + 3] = y.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
+    if (SHARED) buf ^= 1;
+  }
+
+  const int tm0 = m0 + 32 * wm, tn0 = n0 + 32 * wn;
+  auto store = [&](int g, float v) {
+    const int row = tm0 + (g & 3) + 8 * (g >> 2) + 4 * h;
+    const int col = tn0 + r;
+    if (row >= a.M || col >= a.N) return;
+    if (a.partial) {
+      a.partial[((long)z * a.M + row) * a.N + col] = v;
+      return;
+    }
+    if (a.bias) v += a.bias[col];
+    if (a.act == ACT_GELU) v = gelu_tanh(v);
+    else if (a.act == ACT_SILU) v = silu(v);
+    long yrow = row;
+    if (MODE == 1) {
+      const int b2 = row / a.Tq;
+      const int q2 = row - b2 * a.Tq;
+      yrow = (long)b2 * a.T_out + (long)q2 * a.out_tstride + phase;
+    }
+    if (a.rscale) v *= a.rscale[col];
+    if (a.R) v += a.R[yrow * a.ldr + col];
+    a.Y[yrow * a.ldy + col] = v;
+  };
+  if (!SHARED) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[g];
+    __syncthreads();
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int g = wave * 4 + gg;
+      float v = red[(0 * 16 + g) * 64 + lane] + red[(1 * 16 + g) * 64 + lane];
+      v += red[(2 * 16 + g) * 64 + lane];
+      v += red[(3 * 16 + g) * 64 + lane];
+      store(g, v);
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) store(g, acc[g]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA GEMM (the CDNA guide's 2-buffer global_load_lds structure): operand tiles go
+// global -> LDS with global_load_lds_dwordx4 (one 1-KiB wave instruction = RPI rows of one
+// BK-wide chunk; no VGPRs), two LDS buffers, one barrier per chunk: the DMA of chunk c+1 is in
+// flight while chunk c is multiplied. LDS rows are unpadded and XOR-swizzled by 16-byte column
+// (BK 32: col ^ ((row>>1)&7), BK 64: col ^ (row&15)) so the ds_read_b128 fragment reads are
+// conflict-free; the swizzle is applied on the per-lane global SOURCE address (the DMA writes
+// lane-linearly).  WG tile (32*WM) x (32*WN), 4 waves, each one 32x32 accumulator.
+// Requires K % BK == 0 and, for convs, cin % BK == 0.
+// ---------------------------------------------------------------------------------------------
+template <int BK>
+__device__ __forceinline__ int swz(int row) {
+  return BK == 32 ? ((row >> 1) & 7) : (row & 15);
+}
+
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at
+// lds_byte + 16*l. Issued through inline asm so hipcc neither counts it in vmcnt nor fences the
+// ds_reads of the other buffer behind it (it cannot prove they do not alias); the caller drains
+// it with an explicit `s_waitcnt vmcnt(0)` before the barrier that precedes reading it
+// (cdna_hip_programming.md §5.7, M0 saved and restored inside the statement).
+__device__ __forceinline__ void glds16(const float* gsrc, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_byte)
+      : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) float*)(p);
+}
+
+// s_waitcnt with only vmcnt = n (expcnt/lgkmcnt left at "no wait"), gfx9 simm16 encoding
+#define PTTS_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
+
+template <int MODE, int WM, int WN, int BK, int NBUF>
+__global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
+  constexpr int TM = 32 * WM, TN = 32 * WN, ROWS = TM + TN;
+  constexpr int CPR = BK / 4;        // 16-byte columns per LDS row
+  constexpr int RPI = 64 / CPR;      // rows per 1-KiB wave instruction
+  constexpr int NINS = ROWS / RPI;   // DMA instructions per chunk (whole workgroup)
+  static_assert(NINS % 4 == 0, "every wave issues the same number of DMAs per chunk");
+  constexpr int IPW = NINS / 4;
+  constexpr int DIST = NBUF - 1;     // chunks in flight ahead of the one being multiplied
+  static_assert(NBUF >= 2 && NBUF <= 4, "counted waits below cover up to 3 chunks in flight");
+  __shared__ __attribute__((aligned(16))) float lds[NBUF * ROWS * BK];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int r = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM, z = blockIdx.z;
+  const int nchunks = a.K / BK;
+  int cb = 0, ce = nchunks, phase = 0;
+  if (MODE == 0) {
+    cb = (int)((long)nchunks * z / a.S);
+    ce = (int)((long)nchunks * (z + 1) / a.S);
+  } else {
+    phase = z;
+  }
+  const float* Wp = a.W + (long)phase * a.w_phase_stride;
+  const unsigned lds_base = lds_addr(lds);
+  // this lane's DMA sources: instruction j = wave + 4*ins covers rows j*RPI .. +RPI-1
+  const float* src_base[IPW];
+  int src_row[IPW], src_bq[IPW], src_qq[IPW], src_col[IPW];
+  bool src_is_a[IPW];
+#pragma unroll
+  for (int ins = 0; ins < IPW; ++ins) {
+    const int j = wave + 4 * ins;
+    const int row = (j < NINS ? j : 0) * RPI + lane / CPR;
+    const int lcol = (lane % CPR) ^ swz<BK>(row);
+    src_col[ins] = 4 * lcol;
+    src_row[ins] = row;
+    src_is_a[ins] = row < TM;
+    if (row < TM) {
+      const int m = min(m0 + row, a.M - 1);  // rows >= M only feed output rows that are never stored
+      if (MODE == 0) {
+        src_base[ins] = a.X + (long)m * a.ldx;
+      } else {
+        src_bq[ins] = m / a.Tq;
+        src_qq[ins] = m - src_bq[ins] * a.Tq;
+        src_base[ins] = nullptr;
+      }
+    } else {
+      const int n = min(n0 + row - TM, a.Nw - 1);
+      src_base[ins] = Wp + (long)n * a.K;
+    }
+  }
+  auto issue = [&](int c, int buf) {
+    const int k0 = c * BK;
+#pragma unroll
+    for (int ins = 0; ins < IPW; ++ins) {
+      const int j = wave + 4 * ins;
+      if (j >= NINS) break;  // wave-uniform
+      const float* src;
+      if (MODE == 1 && src_is_a[ins]) {
+        const int tap = k0 / a.cin;
+        const int ci = k0 - tap * a.cin + src_col[ins];
+        const int t = src_qq[ins] * a.stride_in + tap - a.P;
+        src = t >= 0 ? a.X + ((long)src_bq[ins] * a.T_in + t) * a.ldx + ci
+                     : a.H + ((long)src_bq[ins] * a.P + (a.P + t)) * a.cin + ci;
+      } else {
+        src = src_base[ins] + k0 + src_col[ins];
+      }
+      // wave-uniform LDS base of this instruction; lane l -> + 16*l bytes
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)((buf * ROWS * BK + j * RPI * BK) * 4));
+      glds16(src, dst);
+    }
+  };
+  const bool elu = MODE == 1 && a.elu_in;
+  floatx16 acc;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+  const int arow = 32 * wm + r, brow = TM + 32 * wn + r;
+  for (int d = 0; d < DIST; ++d)
+    if (cb + d < ce) issue(cb + d, d);
+  for (int c = cb; c < ce; ++c) {
+    {  // chunk c landed for this wave once only the younger chunks' DMAs remain outstanding
+      const int younger = min(DIST - 1, ce - 1 - c);
+      if (younger >= 2) PTTS_WAIT_VM(2 * IPW);
+      else if (younger == 1) PTTS_WAIT_VM(IPW);
+      else PTTS_WAIT_VM(0);
+    }
+    // every wave's DMAs of chunk c have landed, and every wave is done with chunk c-1's buffer,
+    // which the DMA issued next (chunk c+DIST) overwrites
+    __syncthreads();
+    if (c + DIST < ce) issue(c + DIST, (c + DIST - cb) % NBUF);
+    {
+      const int buf = (c - cb) % NBUF;
+      const float* la = lds + buf * ROWS * BK + arow * BK;
+      const float* lb = lds + buf * ROWS * BK + brow * BK;
+#pragma unroll
+      for (int half = 0; half < BK / 32; ++half) {
+        float af[16], bf[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int lc = 8 * half + 4 * h + i;
+          const float4 x = *reinterpret_cast<const float4*>(la + 4 * (lc ^ swz<BK>(arow)));
+          const float4 y = *reinterpret_cast<const float4*>(lb + 4 * (lc ^ swz<BK>(brow)));
+          af[4 * i + 0] = x.x; af[4 * i + 1] = x.y; af[4 * i + 2] = x.z; af[4 * i + 3] = x.w;
+          bf[4 * i + 0] = y.x; bf[4 * i + 1] = y.y; bf[4 * i + 2] = y.z; bf[4 * i + 3] = y.w;
+        }
+        if (elu) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) af[j] = elu1(af[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
+      }
+    }
+  }
+  const int tm0 = m0 + 32 * wm, tn0 = n0 + 32 * wn;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int row = tm0 + (g & 3) + 8 * (g >> 2) + 4 * h;
+    const int col = tn0 + r;
     if (row >= a.M || col >= a.N) continue;
+    float v = acc[g];
     if (a.partial) {
       a.partial[((long)z * a.M + row) * a.N + col] = v;
       continue;
@@ -154,10 +523,54 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
   }
 }
 
+template <int MODE>
+static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
+  switch (a.layout) {
+#define PTTS_GLDS(L, WM_, WN_, BK_, NB_)                                                               \
+  case L:                                                                                               \
+    hipLaunchKernelGGL((k_gemm_glds<MODE, WM_, WN_, BK_, NB_>),                                         \
+                       dim3((a.N + 32 * WN_ - 1) / (32 * WN_), (a.M + 32 * WM_ - 1) / (32 * WM_), grid_z), \
+                       dim3(256), 0, s, a);                                                            \
+    return;
+    PTTS_GLDS(6, 2, 2, 32, 2)
+    PTTS_GLDS(7, 1, 4, 32, 2)
+    PTTS_GLDS(8, 2, 2, 64, 2)
+    PTTS_GLDS(11, 2, 2, 32, 3)
+    PTTS_GLDS(12, 2, 2, 32, 4)
+    PTTS_GLDS(13, 1, 4, 32, 4)
+    PTTS_GLDS(14, 4, 1, 32, 4)
+    PTTS_GLDS(15, 2, 2, 64, 3)
+    PTTS_GLDS(16, 1, 4, 64, 3)
+#undef PTTS_GLDS
+    default:
+      break;
+  }
+  switch (a.layout) {
+    case 4:
+      hipLaunchKernelGGL((k_gemm_lds<MODE, 0>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s,
+                         a);
+      break;
+    case 5:
+      hipLaunchKernelGGL((k_gemm_lds<MODE, 1>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), dim3(256), 0, s,
+                         a);
+      break;
+    case 1:
+      hipLaunchKernelGGL((k_gemm<MODE, 1>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), dim3(256), 0, s, a);
+      break;
+    case 2:
+      hipLaunchKernelGGL((k_gemm<MODE, 2>), dim3((a.N + 127) / 128, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+      break;
+    case 3:
+      hipLaunchKernelGGL((k_gemm<MODE, 3>), dim3((a.N + 31) / 32, (a.M + 127) / 128, grid_z), dim3(256), 0, s, a);
+      break;
+    default:
+      hipLaunchKernelGGL((k_gemm<MODE, 0>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+  }
+}
+
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s) {
-  dim3 grid((a.N + 31) / 32, (a.M + 31) / 32, grid_z);
-  if (a.mode == 0) hipLaunchKernelGGL(k_gemm<0>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_gemm<1>, grid, dim3(256), 0, s, a);
+  if (a.mode == 0) gemm_launch<0>(a, grid_z, s);
+  else gemm_launch<1>(a, grid_z, s);
 }
 
 // =============================================================================================
@@ -172,57 +585,70 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
-template <int NPT>
+// One workgroup per (row, 1024-column block); each thread owns 4 consecutive columns (float4).
+// The S partial slabs are summed in z order (deterministic) with 4 independent loads in flight.
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4mul(float4 a, float4 b) {
+  return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+}
+__device__ __forceinline__ float act1(float x, int act) {
+  return act == ACT_GELU ? gelu_tanh(x) : (act == ACT_SILU ? silu(x) : x);
+}
+
 __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   __shared__ float sh[4];
   const int m = blockIdx.x;
-  const int tid = threadIdx.x;
-  float v[NPT];
-#pragma unroll
-  for (int i = 0; i < NPT; ++i) {
-    const int n = tid + i * 256;
-    float x = 0.f;
-    if (n < a.N) {
-      for (int z = 0; z < a.S; ++z) x += a.P[((long)z * a.M + m) * a.N + n];
-      if (a.bias) x += a.bias[n];
-      if (a.act == ACT_GELU) x = gelu_tanh(x);
-      else if (a.act == ACT_SILU) x = silu(x);
-      if (a.gate) x *= a.gate[(long)m * a.ldg + n];
-      if (a.R) x += a.R[(long)m * a.ldr + n];
-      if (a.Y) a.Y[(long)m * a.ldy + n] = x;
-      if (a.euler) a.euler[(long)m * 32 + n] += x * a.euler_scale;
+  const int n = blockIdx.y * 1024 + 4 * threadIdx.x;
+  const bool ok = n < a.N;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    const float* p = a.P + (long)m * a.N + n;
+    const long zs = (long)a.M * a.N;
+    int z = 0;
+    for (; z + 4 <= a.S; z += 4) {
+      const float4 p0 = *reinterpret_cast<const float4*>(p + (z + 0) * zs);
+      const float4 p1 = *reinterpret_cast<const float4*>(p + (z + 1) * zs);
+      const float4 p2 = *reinterpret_cast<const float4*>(p + (z + 2) * zs);
+      const float4 p3 = *reinterpret_cast<const float4*>(p + (z + 3) * zs);
+      v = f4add(f4add(f4add(f4add(v, p0), p1), p2), p3);
     }
-    v[i] = x;
+    for (; z < a.S; ++z) v = f4add(v, *reinterpret_cast<const float4*>(p + z * zs));
+    if (a.bias) v = f4add(v, *reinterpret_cast<const float4*>(a.bias + n));
+    if (a.act != ACT_NONE) v = make_float4(act1(v.x, a.act), act1(v.y, a.act), act1(v.z, a.act), act1(v.w, a.act));
+    if (a.gate) v = f4mul(v, *reinterpret_cast<const float4*>(a.gate + (long)m * a.ldg + n));
+    if (a.R) v = f4add(v, *reinterpret_cast<const float4*>(a.R + (long)m * a.ldr + n));
+    if (a.Y) *reinterpret_cast<float4*>(a.Y + (long)m * a.ldy + n) = v;
+    if (a.euler) {
+      float4* e = reinterpret_cast<float4*>(a.euler + (long)m * 32 + n);
+      const float sc = a.euler_scale;
+      float4 c = *e;
+      *e = make_float4(c.x + v.x * sc, c.y + v.y * sc, c.z + v.z * sc, c.w + v.w * sc);
+    }
   }
-  if (!a.ln) return;
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < NPT; ++i) s += (tid + i * 256 < a.N) ? v[i] : 0.f;
+  if (!a.ln) return;  // LN rows are <= 1024 wide: gridDim.y == 1 (host-checked)
+  const float s = ok ? (v.x + v.y) + (v.z + v.w) : 0.f;
   const float mean = block_sum(s, sh) / (float)a.N;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < NPT; ++i) {
-    const float d = v[i] - mean;
-    q += (tid + i * 256 < a.N) ? d * d : 0.f;
+  const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+  const float q = ok ? (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w) : 0.f;
+  const float den = sqrtf(block_sum(q, sh) / (float)a.N + a.eps);
+  if (!ok) return;
+  float4 hh = make_float4(d.x / den, d.y / den, d.z / den, d.w / den);
+  if (a.ln_w)
+    hh = f4add(f4mul(hh, *reinterpret_cast<const float4*>(a.ln_w + n)), *reinterpret_cast<const float4*>(a.ln_b + n));
+  if (a.mshift) {
+    const float4 sc = *reinterpret_cast<const float4*>(a.mscale + (long)m * a.ldm + n);
+    const float4 sf = *reinterpret_cast<const float4*>(a.mshift + (long)m * a.ldm + n);
+    hh = make_float4(hh.x * (1.0f + sc.x) + sf.x, hh.y * (1.0f + sc.y) + sf.y, hh.z * (1.0f + sc.z) + sf.z,
+                     hh.w * (1.0f + sc.w) + sf.w);
   }
-  const float var = block_sum(q, sh) / (float)a.N;
-  const float den = sqrtf(var + a.eps);
-#pragma unroll
-  for (int i = 0; i < NPT; ++i) {
-    const int n = tid + i * 256;
-    if (n >= a.N) continue;
-    float hh = (v[i] - mean) / den;
-    if (a.ln_w) hh = hh * a.ln_w[n] + a.ln_b[n];
-    if (a.mshift) hh = hh * (1.0f + a.mscale[(long)m * a.ldm + n]) + a.mshift[(long)m * a.ldm + n];
-    a.Hout[(long)m * a.ldh + n] = hh;
-  }
+  *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = hh;
 }
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s) {
-  dim3 grid(a.M);
-  if (a.N <= 1024) hipLaunchKernelGGL(k_row_reduce<4>, grid, dim3(256), 0, s, a);
-  else if (a.N <= 4096) hipLaunchKernelGGL(k_row_reduce<16>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_row_reduce<40>, grid, dim3(256), 0, s, a);
+  dim3 grid(a.M, (a.N + 1023) / 1024);
+  hipLaunchKernelGGL(k_row_reduce, grid, dim3(256), 0, s, a);
 }
 
 // LayerNorm, one wave per row (N <= 1024, multiple of 64).
