@@ -23,15 +23,32 @@ rc=$?
 echo "smoke rc=$rc"; tail -n 5 "$OUT/smoke.log"
 if [ $rc -ne 0 ]; then exit $rc; fi
 
-timeout -k 10 600 python bench.py > "$OUT/bench.log" 2>&1
+timeout -k 10 600 python bench.py --ops-out "$OUT/bench_ops.json" > "$OUT/bench.log" 2>&1
 rc=$?
 echo "bench rc=$rc"; tail -n 3 "$OUT/bench.log"
 if [ $rc -ne 0 ]; then exit $rc; fi
 
 if [ "${PROFILE:-1}" = "1" ]; then
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-      -- python "$ROOT/bench.py" --steps 30 --warmup 5 --no-cpu-baseline --no-latency > "$OUT/prof.log" 2>&1)
+      -- python "$ROOT/bench.py" --steps 30 --warmup 5 --no-cpu-baseline --no-latency \
+      --ops-out "$OUT/prof_ops.json" > "$OUT/prof.log" 2>&1)
   rc=$?
-  echo "rocprof rc=$rc"; tail -n 3 "$OUT/prof.log"
+  echo "rocprof rc=$rc"; tail -n 2 "$OUT/prof.log"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+  python tools/prof_ops.py trace "$OUT/prof/run_kernel_trace.csv" "$OUT/prof_ops.json" "$OUT/op_stats.csv"
+fi
+
+if [ "${PMC:-0}" = "1" ]; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -d "$OUT/pmc_$C" -o run --output-format csv \
+        -- python "$ROOT/bench.py" --steps 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times \
+        > "$OUT/pmc_$C.log" 2>&1)
+    rc=$?
+    echo "pmc $C rc=$rc"; tail -n 2 "$OUT/pmc_$C.log"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+    python tools/prof_ops.py counters "$OUT/pmc_$C/run_counter_collection.csv" "$OUT/bench_ops.json" $C \
+        "$OUT/pmc_$C.json"
+  done
+  python tools/prof_ops.py traffic "$OUT/pmc_FETCH_SIZE.json" "$OUT/pmc_WRITE_SIZE.json" "$OUT/traffic.json"
 fi
 exit 0
