@@ -51,6 +51,26 @@ def measured_traffic(op):
     return t["ops"][op]["hbm_bytes_per_launch"], t.get("source")
 
 
+def slot_seed(round_id, rank, row):
+    """Noise-stream seed of one utterance: distinct across jobs, ranks and rows."""
+    return 100000 * round_id + 1000 * rank + row + 1
+
+
+def broadcast_weights(dist, blob):
+    """The one collective of the replicas design: rank 0's packed weight blob to every rank
+    (RCCL over xGMI on GPUs; gloo in the CPU tests)."""
+    dist.broadcast(blob, src=0)
+
+
+def max_over_ranks(dist, values, device):
+    """Max over ranks of per-rank wall times (the slowest replica bounds the job)."""
+    import torch
+
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
+
+
 def synth_prompt(n=PROMPT_FRAMES):
     return (0.11 * np.random.default_rng(1).standard_normal((n, 1024))).astype(np.float32)
 
@@ -97,7 +117,7 @@ def main():
         eng = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                         weight_blob=blob.data_ptr(), defer_weights=(rank != 0))
         torch.cuda.synchronize()
-        dist.broadcast(blob, src=0)
+        broadcast_weights(dist, blob)
         torch.cuda.synchronize()
         if rank != 0:
             eng.finalize()
@@ -108,7 +128,7 @@ def main():
         for b in range(B):
             eng.open(b, voice, text_ids(b), pt.GenerationParams(
                 temp=0.7, eos_threshold=float("inf"), frames_after_eos=3, max_frames=K,
-                seed=100000 * round_id + 1000 * rank + b + 1))
+                seed=slot_seed(round_id, rank, b)))
 
     # warmup: a short job on the same rows (graph capture, caches), then the rows are re-admitted
     admit(0)
@@ -139,11 +159,7 @@ def main():
     elapsed = t1 - t0
     admit_s = ta - t0
     if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed, admit_s], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, admit_s = float(t[0].item()), float(t[1].item())
+        elapsed, admit_s = max_over_ranks(dist, [elapsed, admit_s], f"cuda:{local_rank}")
     r = eng.fetch(B)
     assert r.valid.all() and r.last.all() and np.isfinite(r.pcm).all(), "bench produced invalid frames"
 

@@ -64,6 +64,13 @@ typedef struct ptts_gen_params {
 
 /* Size of the packed device weight blob (all tensors, engine layout). */
 size_t ptts_weight_blob_bytes(void);
+/* Pack the weights (synthetic from synth_seed when weights_path is NULL/empty, else a local
+ * safetensors file with TTSModel state-dict names) into a host buffer of at least
+ * ptts_weight_blob_bytes(), in the engine's device layout. Host only: no GPU needed. A
+ * multi-GPU launcher packs once, broadcasts the blob (RCCL) into every rank's engine buffer
+ * (cfg.weight_blob + defer_weights) and calls ptts_engine_finalize(). Replaces the per-process
+ * VarBuilder load of TTSModel::load_with_params_device (tts_model.rs:86-106). */
+int ptts_pack_weights(uint64_t synth_seed, const char* weights_path, float* host_out, size_t n_bytes);
 
 /* TTSModel::load / load_with_params_device (tts_model.rs:59-106,182-236). */
 int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out);

@@ -39,6 +39,19 @@ extern "C" {
 
 size_t ptts_weight_blob_bytes(void) { return ptts::pack_weights(nullptr, nullptr).total * sizeof(float); }
 
+int ptts_pack_weights(uint64_t synth_seed, const char* weights_path, float* host_out, size_t n_bytes) {
+  return guard([&] {
+    if (!host_out) throw ptts::Error(PTTS_ERR_INVALID, "null output buffer");
+    const size_t need = ptts::pack_weights(nullptr, nullptr).total * sizeof(float);
+    if (n_bytes < need) throw ptts::Error(PTTS_ERR_INVALID, "output buffer smaller than ptts_weight_blob_bytes()");
+    std::unique_ptr<ptts::TensorSource> src = weights_path && weights_path[0]
+                                                  ? ptts::make_safetensors_source(weights_path)
+                                                  : ptts::make_synth_source(synth_seed);
+    std::memset(host_out, 0, need);
+    ptts::pack_weights(src.get(), host_out);
+  });
+}
+
 int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out) {
   return guard([&] {
     if (!cfg || !out) throw ptts::Error(PTTS_ERR_INVALID, "null argument");

@@ -49,6 +49,7 @@ class GenParams(C.Structure):
 # (name, restype, argtypes) for every symbol include/pocket_tts.h declares
 SIGNATURES = [
     ("ptts_weight_blob_bytes", C.c_size_t, []),
+    ("ptts_pack_weights", C.c_int, [C.c_uint64, C.c_char_p, F32P, C.c_size_t]),
     ("ptts_engine_create", C.c_int, [C.POINTER(EngineConfig), C.POINTER(C.c_void_p)]),
     ("ptts_engine_finalize", C.c_int, [C.c_void_p]),
     ("ptts_engine_destroy", None, [C.c_void_p]),

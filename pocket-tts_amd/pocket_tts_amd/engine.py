@@ -7,7 +7,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (DIM, FRAME, LDIM, EngineConfig, GenParams, check, fptr, lib, u8ptr)
+from ._lib import (DIM, F32P, FRAME, LDIM, EngineConfig, GenParams, check, fptr, lib, u8ptr)
 
 
 @dataclass
@@ -81,6 +81,14 @@ class Engine:
     @staticmethod
     def weight_blob_bytes() -> int:
         return int(lib().ptts_weight_blob_bytes())
+
+    @staticmethod
+    def pack_weights(seed: int = 0x5EED, weights_path: str | None = None) -> np.ndarray:
+        """Packed weight blob (engine device layout) built on the host; no GPU needed."""
+        out = np.empty(Engine.weight_blob_bytes() // 4, np.float32)
+        check(lib().ptts_pack_weights(seed, weights_path.encode() if weights_path else None,
+                                      out.ctypes.data_as(F32P), out.nbytes))
+        return out
 
     def weight_blob(self) -> int:
         return int(lib().ptts_engine_weight_blob(self.handle) or 0)
