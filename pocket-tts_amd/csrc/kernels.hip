@@ -836,9 +836,225 @@ __global__ __launch_bounds__(256) void k_attention(const float* Q, int M, int nh
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Decode attention, one query per (row, head) (FlowLM step, attention.rs:104-283 with the
+// single-query mask skip of sdpa.rs:3-18): one 256-thread workgroup per (row, head), the keys
+// dealt to the 4 waves 64 at a time. Lane j owns key j of its 64-key block: the whole K row
+// (16 float4) and, for P.V, lane d owns output dim d and reads V[j][d] for the block's 64 keys
+// (coalesced 256-B rows) - all loads of a block are issued before any arithmetic, so each wave
+// pays one memory round trip per block. p_j is broadcast with v_readlane. Waves combine their
+// (max, sum, o) through LDS. Positions never wrap (max_ctx covers voice + text + frames).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_attn_decode(const float* __restrict__ Q, int nh, RowMap mp, KvStore kv,
+                                                     float* __restrict__ O) {
+  __shared__ float s_m[4], s_l[4], s_o[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row = blockIdx.x, head = blockIdx.y;
+  int slot, qp;
+  row_slot_pos(mp, row, slot, qp);
+  const int d = nh * 64;
+  const float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
+  const float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
+  const float4* q4 = reinterpret_cast<const float4*>(Q + (long)row * d + head * 64);
+  float4 q[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) q[i] = q4[i];
+  float m = -INFINITY, l = 0.f, o = 0.f;
+  for (int base = 64 * wave; base <= qp; base += 256) {
+    const int j = base + lane;
+    const bool valid = j <= qp;
+    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)(valid ? j : qp) * 64);
+    float4 k[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) k[i] = kr[i];
+    float v[64];
+#pragma unroll
+    for (int jj = 0; jj < 64; ++jj) v[jj] = vbase[(long)min(base + jj, qp) * 64 + lane];
+    float sc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sc += q[i].x * k[i].x + q[i].y * k[i].y + q[i].z * k[i].z + q[i].w * k[i].w;
+    sc = valid ? sc * 0.125f : -INFINITY;  // 1/sqrt(64) (attention.rs:191,229)
+    const float mn = fmaxf(m, wave_max(sc));  // finite: key `base` <= qp is valid
+    const float alpha = expf(m - mn);         // m = -inf -> 0
+    const float p = valid ? expf(sc - mn) : 0.f;
+    l = l * alpha + wave_sum(p);
+    o *= alpha;
+    const int pb = __builtin_bit_cast(int, p);
+#pragma unroll
+    for (int jj = 0; jj < 64; ++jj) o += __builtin_bit_cast(float, __builtin_amdgcn_readlane(pb, jj)) * v[jj];
+    m = mn;
+  }
+  if (lane == 0) {
+    s_m[wave] = m;
+    s_l[wave] = l;
+  }
+  s_o[wave][lane] = o;
+  __syncthreads();
+  if (wave == 0) {
+    const float M = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float e = s_m[w] == -INFINITY ? 0.f : expf(s_m[w] - M);
+      num += s_o[w][lane] * e;
+      den += s_l[w] * e;
+    }
+    O[(long)row * d + head * 64 + lane] = num / den;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 16-query attention on MFMA (Mimi decoder ring window: 16 upsampled positions per row, and the
+// prefill / encoder groups): one workgroup per (16 consecutive rows of one slot, head), 16-key
+// tiles dealt to 8 waves, online softmax per wave, waves merged through LDS.
+// v_mfma_f32_16x16x4_f32 fragments (lane l, c = l & 15, G = l >> 4):
+//   A[i][k] lane i + 16k, B[k][j] lane j + 16k, D reg g -> row 4G + g, col c.
+// S^T = K Q^T: A = K (key c, dims 16G+s at step s), B = Q^T (query c, same dims) -> lane holds
+// S[query c][key 4G+g]. O += P V: A = P (query c, key 4G+s at step s: the lane's own S^T regs,
+// no transpose), B = V (key 4G+s, dim 4c+dt for output tile dt: one float4 per key) -> lane holds
+// O[query 4G+g][dim 4c+dt]. The dot-product / key order permutations only reorder sums.
+// ---------------------------------------------------------------------------------------------
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+constexpr int A16_WAVES = 8;
+
+template <bool RING>
+__global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restrict__ Q, int M, int nh, RowMap mp,
+                                                          KvStore kv, int window, float* __restrict__ O) {
+  __shared__ float s_m[A16_WAVES][16], s_l[A16_WAVES][16];
+  __shared__ float s_o[A16_WAVES][16][65];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, G = lane >> 4;
+  const int row0 = blockIdx.x * 16, head = blockIdx.y;
+  const int nrows = min(16, M - row0);
+  int slot, qpos0;
+  row_slot_pos(mp, row0, slot, qpos0);
+  const int kmax = qpos0 + nrows - 1;
+  const int kmin = window > 0 ? max(0, qpos0 - window + 1) : 0;
+  const int d = nh * 64;
+  const float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
+  const float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
+  const int cmask = kv.cap - 1;
+  auto kidx = [&](int kp) { return RING ? (kp & cmask) : kp; };
+  // Q^T fragment: query c (rows past nrows reuse the last row; never stored), dims 16G..16G+15
+  float qf[16];
+  {
+    const float4* q4 = reinterpret_cast<const float4*>(Q + (long)(row0 + min(c, nrows - 1)) * d + head * 64 + 16 * G);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 t = q4[i];
+      qf[4 * i] = t.x; qf[4 * i + 1] = t.y; qf[4 * i + 2] = t.z; qf[4 * i + 3] = t.w;
+    }
+  }
+  const int qp = qpos0 + c;  // this lane's query position (softmax side)
+  float m = -INFINITY, l = 0.f;
+  floatx4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int ntiles = (kmax - kmin + 16) / 16;
+  float4 kf[4], vf[4];
+  auto load = [&](int t) {
+    const int kt = kmin + 16 * t;
+    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)kidx(min(kt + c, kmax)) * 64 + 16 * G);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kf[i] = kr[i];
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx)
+      vf[sidx] = *reinterpret_cast<const float4*>(vbase + (long)kidx(min(kt + 4 * G + sidx, kmax)) * 64 + 4 * c);
+  };
+  if (wave < ntiles) load(wave);
+  for (int t = wave; t < ntiles; t += A16_WAVES) {
+    const int kt = kmin + 16 * t;
+    float ka[16];
+    float4 vc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ka[4 * i] = kf[i].x; ka[4 * i + 1] = kf[i].y; ka[4 * i + 2] = kf[i].z; ka[4 * i + 3] = kf[i].w;
+      vc[i] = vf[i];
+    }
+    if (t + A16_WAVES < ntiles) load(t + A16_WAVES);  // next tile in flight during this one
+    floatx4 st = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sidx = 0; sidx < 16; ++sidx) st = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[sidx], qf[sidx], st, 0, 0, 0);
+    float sc[4];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int kp = kt + 4 * G + g;
+      const bool ok = kp <= kmax && kp <= qp && (window <= 0 || qp - kp < window);
+      sc[g] = ok ? st[g] * 0.125f : -INFINITY;  // 1/sqrt(64) (attention.rs:191,229)
+      mt = fmaxf(mt, sc[g]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = mn == -INFINITY ? 1.f : expf(m - mn);
+    float p[4], ps = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      p[g] = sc[g] == -INFINITY ? 0.f : expf(sc[g] - mn);
+      ps += p[g];
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = mn;
+    // O rows are queries 4G+g: their rescale factors live in lanes 4G+g
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float a = __shfl(alpha, 4 * G + g, 64);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt][g] *= a;
+    }
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx) {
+      o[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(p[sidx], vc[sidx].x, o[0], 0, 0, 0);
+      o[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(p[sidx], vc[sidx].y, o[1], 0, 0, 0);
+      o[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(p[sidx], vc[sidx].z, o[2], 0, 0, 0);
+      o[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(p[sidx], vc[sidx].w, o[3], 0, 0, 0);
+    }
+  }
+  if (G == 0) {
+    s_m[wave][c] = m;
+    s_l[wave][c] = l;
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) s_o[wave][4 * G + g][4 * c + dt] = o[dt][g];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 16 * 64; e += 64 * A16_WAVES) {
+    const int qi = e >> 6, dd = e & 63;
+    if (qi >= nrows) continue;
+    float M_ = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < A16_WAVES; ++w) M_ = fmaxf(M_, s_m[w][qi]);
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int w = 0; w < A16_WAVES; ++w) {
+      const float ew = s_m[w][qi] == -INFINITY ? 0.f : expf(s_m[w][qi] - M_);
+      num += s_o[w][qi][dd] * ew;
+      den += s_l[w][qi] * ew;
+    }
+    O[(long)(row0 + qi) * d + head * 64 + dd] = num / den;
+  }
+}
+
 void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O, hipStream_t s) {
-  dim3 grid((M + qg - 1) / qg, nh);
-  hipLaunchKernelGGL(k_attention, grid, dim3(256), 0, s, Q, M, nh, map, kv, window, qg, O);
+  if (qg == 1 && window <= 0) {
+    hipLaunchKernelGGL(k_attn_decode, dim3(M, nh), dim3(256), 0, s, Q, nh, map, kv, O);
+  } else if (qg == 16) {
+    // 16-row groups never straddle slots (rows-per-slot is 16 or the whole group)
+    const dim3 grid((M + 15) / 16, nh);
+    if ((kv.cap & (kv.cap - 1)) == 0)
+      hipLaunchKernelGGL(k_attn16<true>, grid, dim3(64 * A16_WAVES), 0, s, Q, M, nh, map, kv, window, O);
+    else
+      hipLaunchKernelGGL(k_attn16<false>, grid, dim3(64 * A16_WAVES), 0, s, Q, M, nh, map, kv, window, O);
+  } else {
+    dim3 grid((M + qg - 1) / qg, nh);
+    hipLaunchKernelGGL(k_attention, grid, dim3(256), 0, s, Q, M, nh, map, kv, window, qg, O);
+  }
 }
 
 // =============================================================================================
