@@ -124,11 +124,10 @@ def main():
 
     voice = eng.voice_from_prompt(synth_prompt())  # voice state precomputed (shared by all rows)
 
-    def admit(round_id):
-        for b in range(B):
-            eng.open(b, voice, text_ids(b), pt.GenerationParams(
-                temp=0.7, eos_threshold=float("inf"), frames_after_eos=3, max_frames=K,
-                seed=slot_seed(round_id, rank, b)))
+    def admit(round_id):  # batched admission (ptts_slots_open): one shared text-prefill pass
+        eng.open_many(list(range(B)), [voice] * B, [text_ids(b) for b in range(B)],
+                      [pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), frames_after_eos=3, max_frames=K,
+                                           seed=slot_seed(round_id, rank, b)) for b in range(B)])
 
     # warmup: a short job on the same rows (graph capture, caches), then the rows are re-admitted
     admit(0)

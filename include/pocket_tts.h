@@ -98,6 +98,12 @@ void ptts_voice_destroy(ptts_voice* v);
  * prefill `n_ids` text tokens (text.rs:289-303), reset the Mimi state, backbone = bos_emb. */
 int ptts_slot_open(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* ids, int n_ids,
                    const ptts_gen_params* p);
+/* Batched admission of n utterances (distinct slots) in one call: voices[i], params[i] and
+ * n_ids[i] tokens taken in order from the concatenated `ids`. Same per-row result as n
+ * ptts_slot_open calls; the text prefills of all rows share one pass (the server admitting a
+ * burst of requests, or a batch job starting). */
+int ptts_slots_open(ptts_engine* e, int n, const int* slots, const ptts_voice* const* voices, const int32_t* ids,
+                    const int* n_ids, const ptts_gen_params* params);
 int ptts_slot_close(ptts_engine* e, int slot);
 
 /* THE batched hot path: one iteration of the loop body of generate_stream_segment

@@ -116,6 +116,11 @@ int ptts_slot_open(ptts_engine* e, int slot, const ptts_voice* v, const int32_t*
   });
 }
 
+int ptts_slots_open(ptts_engine* e, int n, const int* slots, const ptts_voice* const* voices, const int32_t* ids,
+                    const int* n_ids, const ptts_gen_params* params) {
+  return guard([&] { eng(e).slots_open(n, slots, voices, ids, n_ids, params); });
+}
+
 int ptts_slot_close(ptts_engine* e, int slot) { return guard([&] { eng(e).slot_close(slot); }); }
 
 int ptts_slot_set_latent(ptts_engine* e, int slot, const float* latent32) {

@@ -87,9 +87,13 @@ Engine::Engine(const ptts_engine_config& cfg) {
   o_ = dalloc((size_t)R * D);
   u_ = dalloc((size_t)R * FF);
   // split-K slabs: skinny FlowLM/head GEMMs, and the 2-way split Mimi QKV (B*16 rows x 1536)
-  pcap_ = std::max((size_t)4 << 20, (size_t)2 * B * UP * 3 * MD);
+  pcap_ = std::max({(size_t)4 << 20, (size_t)2 * B * UP * 3 * MD, (size_t)PREFILL * FF});
   partial_ = dalloc(pcap_);
   ids_dev_ = (int*)dalloc(PREFILL);
+  rowtab_dev_ = (int*)dalloc(PREFILL);
+  admit_slots_ = (int*)dalloc(B);
+  admit_st_ = (SlotState*)dalloc((sizeof(SlotState) * B + 3) / 4);
+  admit_fpos_ = (int*)dalloc(B);
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
   mods_ = dalloc((size_t)lsd_ * B * NADA);
   xf_ = dalloc((size_t)B * FD);
@@ -182,6 +186,9 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   if (M <= 64 && N >= 3072) {
     layout = 13;
     S = std::max(1, std::min(8, K / 64));
+  } else if (M >= 256) {  // prefill passes: MFMA-bound, 64x64 LDS-DMA tiles, no split
+    layout = 12;
+    S = 1;
   }
   while (S > 1 && (size_t)S * M * N > pcap_) --S;
   PTTS_REQUIRE((size_t)S * M * N <= pcap_, "split-K partial buffer too small");
@@ -787,60 +794,127 @@ ptts_voice* Engine::voice_from_pcm(const float* pcm, int n) {
 }
 
 void Engine::slot_open(int slot, const ptts_voice* v, const int32_t* ids, int n, const ptts_gen_params& p) {
+  slots_open(1, &slot, &v, ids, &n, &p);
+}
+
+// Batched admission: the per-segment prologue of generate_stream_segment (tts_model.rs:938-1004)
+// for n utterances at once. Voice KV prefixes are copied in (copy-on-admit, tts_model.rs:940),
+// Mimi/conv state reset, and all utterances' text tokens are prefilled together: rows are laid out
+// per slot, padded to 16-row groups (the 16-query attention tiles), and mapped to (slot, position)
+// through a row table.
+void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices, const int32_t* ids,
+                        const int* n_ids, const ptts_gen_params* params) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
-  PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
-  PTTS_REQUIRE(v != nullptr && v->owner == this, "voice belongs to another engine");
-  PTTS_REQUIRE(n >= 0 && (n == 0 || ids != nullptr), "bad token ids");
-  PTTS_REQUIRE(p.max_frames >= 1, "max_frames must be >= 1");
-  PTTS_REQUIRE(p.frames_after_eos >= 0, "frames_after_eos must be >= 0");
-  PTTS_REQUIRE((long)v->F + n + p.max_frames <= max_ctx_, "voice + text + max_frames exceeds max_ctx");
-  for (int i = 0; i < n; ++i) PTTS_REQUIRE(ids[i] >= 0 && ids[i] < VOCAB, "token id out of range");
+  PTTS_REQUIRE(n >= 1 && n <= max_slots_, "number of admissions out of range");
+  PTTS_REQUIRE(slots && voices && n_ids && params, "null argument");
+  std::vector<char> seen(max_slots_, 0);
+  long total_ids = 0;
+  for (int i = 0; i < n; ++i) {
+    const int slot = slots[i];
+    PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
+    PTTS_REQUIRE(!seen[slot], "slot admitted twice in one call");
+    seen[slot] = 1;
+    const ptts_voice* v = voices[i];
+    PTTS_REQUIRE(v != nullptr && v->owner == this, "voice belongs to another engine");
+    const ptts_gen_params& p = params[i];
+    PTTS_REQUIRE(n_ids[i] >= 0 && (n_ids[i] == 0 || ids != nullptr), "bad token ids");
+    PTTS_REQUIRE(p.max_frames >= 1, "max_frames must be >= 1");
+    PTTS_REQUIRE(p.frames_after_eos >= 0, "frames_after_eos must be >= 0");
+    PTTS_REQUIRE((long)v->F + n_ids[i] + p.max_frames <= max_ctx_, "voice + text + max_frames exceeds max_ctx");
+    for (int j = 0; j < n_ids[i]; ++j)
+      PTTS_REQUIRE(ids[total_ids + j] >= 0 && ids[total_ids + j] < VOCAB, "token id out of range");
+    total_ids += n_ids[i];
+  }
   PTTS_HIP(hipSetDevice(dev_));
   PTTS_HIP(hipStreamSynchronize(stream_));
-  // copy-on-admit of the immutable voice prefix
-  PTTS_HIP(hipMemcpy2DAsync(kv_ + (size_t)slot * kv_slot_, sizeof(float) * max_ctx_ * 64, v->kv,
-                            sizeof(float) * v->F * 64, sizeof(float) * v->F * 64, NL * 2 * NH,
-                            hipMemcpyDeviceToDevice, stream_));
-  // fresh Mimi decoder state (init_states(1, 1000) per segment, tts_model.rs:941)
-  for (int i = 0; i < 8; ++i)
-    PTTS_HIP(hipMemsetAsync(hist_[i] + (size_t)slot * hist_P_[i] * hist_C_[i], 0,
-                            sizeof(float) * hist_P_[i] * hist_C_[i], stream_));
-  PTTS_HIP(hipMemsetAsync(qprev_ + (size_t)slot * MD, 0, sizeof(float) * MD, stream_));
-  PTTS_HIP(hipMemcpyAsync(lat_in_ + (size_t)slot * LDIM, W(L_.bos), sizeof(float) * LDIM, hipMemcpyDeviceToDevice,
-                          stream_));
-  // text prefill (tts_model.rs:947-964)
-  int pos = v->F;
-  for (int c0 = 0; c0 < n; c0 += PREFILL) {
-    const int T = std::min(PREFILL, n - c0);
-    PTTS_HIP(hipMemcpyAsync(ids_dev_, ids + c0, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+  // copy-on-admit of the immutable voice prefixes
+  for (int i = 0; i < n; ++i) {
+    const ptts_voice* v = voices[i];
+    PTTS_HIP(hipMemcpy2DAsync(kv_ + (size_t)slots[i] * kv_slot_, sizeof(float) * max_ctx_ * 64, v->kv,
+                              sizeof(float) * v->F * 64, sizeof(float) * v->F * 64, NL * 2 * NH,
+                              hipMemcpyDeviceToDevice, stream_));
+  }
+  // fresh Mimi decoder state (init_states(1, 1000) per segment, tts_model.rs:941) + slot states
+  std::vector<SlotState> st(n);
+  std::vector<int> fp(n);
+  for (int i = 0; i < n; ++i) {
+    const ptts_gen_params& p = params[i];
+    SlotState& s = st[i];
+    s = SlotState{};
+    s.active = 1;
+    s.step = 0;
+    s.eos_step = -1;
+    s.last = 0;
+    s.frames_after_eos = p.frames_after_eos;
+    s.max_frames = p.max_frames;
+    s.temp = p.temp;
+    s.eos_threshold = p.eos_threshold;
+    s.noise_clamp = p.noise_clamp;
+    s.valid = 0;
+    s.seed = p.seed;
+    fp[i] = voices[i]->F + n_ids[i];
+  }
+  PTTS_HIP(hipMemcpyAsync(admit_slots_, slots, sizeof(int) * n, hipMemcpyHostToDevice, stream_));
+  PTTS_HIP(hipMemcpyAsync(admit_st_, st.data(), sizeof(SlotState) * n, hipMemcpyHostToDevice, stream_));
+  PTTS_HIP(hipMemcpyAsync(admit_fpos_, fp.data(), sizeof(int) * n, hipMemcpyHostToDevice, stream_));
+  {
+    ResetArgs r{};
+    for (int i = 0; i < 8; ++i) {
+      r.buf[i] = hist_[i];
+      r.per_slot[i] = (long)hist_P_[i] * hist_C_[i];
+    }
+    r.buf[8] = qprev_;
+    r.per_slot[8] = MD;
+    r.nb = 9;
+    r.slots = admit_slots_;
+    r.n = n;
+    r.lat_in = lat_in_;
+    r.bos = W(L_.bos);
+    r.st_src = admit_st_;
+    r.fpos_src = admit_fpos_;
+    r.st = st_;
+    r.fpos = fpos_;
+    r.mpos = mpos_;
+    slot_reset(r, stream_);
+    PTTS_HIP(hipGetLastError());
+  }
+  // text prefill (tts_model.rs:947-964) of every admitted utterance in shared passes
+  std::vector<int> tab, rid;
+  long off = 0;
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < n_ids[i]; ++j) {
+      tab.push_back(slots[i] << 16 | (voices[i]->F + j));
+      rid.push_back(ids[off + j]);
+    }
+    while (tab.size() % 16) {
+      tab.push_back(-1);
+      rid.push_back(0);
+    }
+    off += n_ids[i];
+  }
+  for (size_t c0 = 0; c0 < tab.size(); c0 += PREFILL) {
+    const int T = (int)std::min<size_t>(PREFILL, tab.size() - c0);  // PREFILL % 16 == 0
+    PTTS_HIP(hipMemcpyAsync(ids_dev_, rid.data() + c0, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(rowtab_dev_, tab.data() + c0, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
     std::vector<Op> ops;
     {
       const int* idp = ids_dev_;
-      const float* tab = W(L_.embed);
+      const float* tb = W(L_.embed);
       float* x = x_;
-      ops.push_back({"prefill.embed", [=](hipStream_t s) { embed_gather(idp, T, tab, D, x, s); }});
+      ops.push_back({"prefill.embed", [=](hipStream_t s) { embed_gather(idp, T, tb, D, x, s); }});
     }
-    prefill_rows(ops, slot, T, pos);
+    {
+      float* x = x_;
+      float* h = h_;
+      const float* w = W(L_.fl[0].n1w);
+      const float* b = W(L_.fl[0].n1b);
+      ops.push_back({"prefill.ln1", [=](hipStream_t s) { layernorm(x, D, h, D, T, D, w, b, 1e-5f, s); }});
+    }
+    RowMap map{0, 1, 0, nullptr, rowtab_dev_};
+    flow_layers(ops, T, map, 16, false, "prefill");
     run_ops(ops);
-    PTTS_HIP(hipStreamSynchronize(stream_));  // ids_dev_ is reused by the next chunk
-    pos += T;
+    PTTS_HIP(hipStreamSynchronize(stream_));  // ids / row table are reused by the next pass
   }
-  SlotState s{};
-  s.active = 1;
-  s.step = 0;
-  s.eos_step = -1;
-  s.last = 0;
-  s.frames_after_eos = p.frames_after_eos;
-  s.max_frames = p.max_frames;
-  s.temp = p.temp;
-  s.eos_threshold = p.eos_threshold;
-  s.noise_clamp = p.noise_clamp;
-  s.valid = 0;
-  s.seed = p.seed;
-  const int zero = 0;
-  PTTS_HIP(hipMemcpy(st_ + slot, &s, sizeof s, hipMemcpyHostToDevice));
-  PTTS_HIP(hipMemcpy(fpos_ + slot, &pos, sizeof(int), hipMemcpyHostToDevice));
-  PTTS_HIP(hipMemcpy(mpos_ + slot, &zero, sizeof(int), hipMemcpyHostToDevice));
   PTTS_HIP(hipStreamSynchronize(stream_));
 }
 

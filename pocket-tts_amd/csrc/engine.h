@@ -40,6 +40,8 @@ class Engine {
   ptts_voice* voice_from_prompt(const float* prompt, int F);
   ptts_voice* voice_from_pcm(const float* pcm, int n);
   void slot_open(int slot, const ptts_voice* v, const int32_t* ids, int n, const ptts_gen_params& p);
+  void slots_open(int n, const int* slots, const ptts_voice* const* voices, const int32_t* ids, const int* n_ids,
+                  const ptts_gen_params* params);
   void slot_close(int slot);
   void set_latent(int slot, const float* lat);
 
@@ -90,10 +92,14 @@ class Engine {
   int hist_T_[8] = {}, hist_C_[8] = {}, hist_P_[8] = {};
 
   // activations
-  static constexpr int PREFILL = 256;
+  static constexpr int PREFILL = 2048;  // rows per prefill pass (batched admission: all slots' text)
   size_t pcap_ = 0;
   float *x_ = nullptr, *h_ = nullptr, *q_ = nullptr, *o_ = nullptr, *u_ = nullptr, *partial_ = nullptr;
   int* ids_dev_ = nullptr;
+  int* rowtab_dev_ = nullptr;   // [PREFILL] slot << 16 | pos, -1 = padding row
+  int* admit_slots_ = nullptr;  // [max_slots] staged admission list
+  SlotState* admit_st_ = nullptr;
+  int* admit_fpos_ = nullptr;
   float *ysilu_ = nullptr, *mods_ = nullptr, *xf_ = nullptr, *hf_ = nullptr, *uf_ = nullptr;
   float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;
   float* a0_ = nullptr;

@@ -84,9 +84,13 @@ void layernorm(const float* x, long ldx, float* y, long ldy, int M, int N, const
 // Packed QKV (sum of S partials, or dense) -> RoPE(q,k) -> q to Q[M][d], k/v into the KV store.
 // Row r belongs to slot = slot0 + r / rps at position pos = (pos_arr ? pos_arr[slot] : p0) + r % rps.
 // KV layout per slot: base + slot*slot_stride + (kv*nh + h)*cap*64 + (pos % cap)*64.
+// Row -> (slot, position). Uniform form: slot = slot0 + row / rps, position = (pos_arr ?
+// pos_arr[slot] : p0) + row % rps. Table form (tab != nullptr, batched admission): tab[row] =
+// slot << 16 | position, or -1 for a padding row (no KV write, output unused).
 struct RowMap {
   int slot0, rps, p0;
   const int* pos_arr;
+  const int* tab;
 };
 struct KvStore {
   float* base;
@@ -142,6 +146,25 @@ struct CommitArgs {
   int* mpos;            // Mimi decoder positions, += 16
 };
 void step_commit(const CommitArgs& a, hipStream_t s);
+
+// Admission reset of n slots (tts_model.rs:941 init_states per segment): zero the per-slot
+// regions of up to 10 state buffers, backbone input = bos, SlotState / FlowLM / Mimi positions
+// from the staged per-admission arrays (index i -> slots[i]).
+struct ResetArgs {
+  float* buf[10];
+  long per_slot[10];
+  int nb;
+  const int* slots;
+  int n;
+  float* lat_in;
+  const float* bos;
+  const SlotState* st_src;
+  const int* fpos_src;
+  SlotState* st;
+  int* fpos;
+  int* mpos;
+};
+void slot_reset(const ResetArgs& a, hipStream_t s);
 
 // TimestepEmbedder pair + RMSNorm + average (mlp.rs:76-133,296-319): out [n][512].
 // tmp: scratch [2][n][512].

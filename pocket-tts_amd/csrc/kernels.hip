@@ -689,6 +689,12 @@ void layernorm(const float* x, long ldx, float* y, long ldy, int M, int N, const
 // QKV (+ split-K reduce) -> RoPE -> KV append. One thread per (row, head, rotation pair).
 // =============================================================================================
 __device__ __forceinline__ void row_slot_pos(const RowMap& mp, int row, int& slot, int& pos) {
+  if (mp.tab) {
+    const int v = mp.tab[row];
+    slot = v < 0 ? -1 : v >> 16;
+    pos = v < 0 ? 0 : v & 0xFFFF;
+    return;
+  }
   slot = mp.slot0 + row / mp.rps;
   pos = (mp.pos_arr ? mp.pos_arr[slot] : mp.p0) + row % mp.rps;
 }
@@ -722,6 +728,7 @@ __global__ __launch_bounds__(256) void k_qkv_rope(const float* P, int S, const f
   const float cs = cosf(ang), sn = sinf(ang);
   Q[(long)row * d + c] = q0 * cs - q1 * sn;
   Q[(long)row * d + c + 1] = q0 * sn + q1 * cs;
+  if (slot < 0) return;  // padding row of a batched admission
   float* kb = kv.base + (long)slot * kv.slot_stride + ((long)hh * kv.cap + (pos % kv.cap)) * 64 + 2 * i;
   float* vb = kv.base + (long)slot * kv.slot_stride + ((long)(nh + hh) * kv.cap + (pos % kv.cap)) * 64 + 2 * i;
   kb[0] = k0 * cs - k1 * sn;
@@ -927,7 +934,13 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, G = lane >> 4;
   const int row0 = blockIdx.x * 16, head = blockIdx.y;
-  const int nrows = min(16, M - row0);
+  int nrows = min(16, M - row0);
+  if (mp.tab) {  // a slot's rows come first in its 16-row groups, padding rows after them
+    int n = 0;
+    for (int i = 0; i < nrows; ++i) n += mp.tab[row0 + i] >= 0;
+    nrows = n;
+  }
+  if (nrows <= 0) return;  // whole group of padding (uniform over the workgroup)
   int slot, qpos0;
   row_slot_pos(mp, row0, slot, qpos0);
   const int kmax = qpos0 + nrows - 1;
@@ -1201,6 +1214,26 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
 
 void step_commit(const CommitArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_commit, dim3(a.nh + 1, a.B), dim3(256), 0, s, a);
+}
+
+__global__ __launch_bounds__(256) void k_slot_reset(ResetArgs a) {
+  const int i = blockIdx.x, b = blockIdx.y;
+  const int slot = a.slots[i];
+  if (b < a.nb) {
+    float* p = a.buf[b] + (long)slot * a.per_slot[b];
+    for (long e = threadIdx.x; e < a.per_slot[b]; e += 256) p[e] = 0.f;
+    return;
+  }
+  if (threadIdx.x < 32) a.lat_in[slot * 32 + threadIdx.x] = a.bos[threadIdx.x];
+  if (threadIdx.x == 0) {
+    a.st[slot] = a.st_src[i];
+    a.fpos[slot] = a.fpos_src[i];
+    a.mpos[slot] = 0;
+  }
+}
+
+void slot_reset(const ResetArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_slot_reset, dim3(a.n, a.nb + 1), dim3(256), 0, s, a);
 }
 
 // =============================================================================================

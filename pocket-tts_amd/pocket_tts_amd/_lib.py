@@ -60,6 +60,8 @@ SIGNATURES = [
     ("ptts_voice_conditioning", C.c_int, [C.c_void_p, F32P, C.c_int]),
     ("ptts_voice_destroy", None, [C.c_void_p]),
     ("ptts_slot_open", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, I32P, C.c_int, C.POINTER(GenParams)]),
+    ("ptts_slots_open", C.c_int, [C.c_void_p, C.c_int, I32P, C.POINTER(C.c_void_p), I32P, I32P,
+                                  C.POINTER(GenParams)]),
     ("ptts_slot_close", C.c_int, [C.c_void_p, C.c_int]),
     ("ptts_step", C.c_int, [C.c_void_p, C.c_int, F32P, U8P, U8P, F32P, F32P]),
     ("ptts_step_async", C.c_int, [C.c_void_p, C.c_int]),

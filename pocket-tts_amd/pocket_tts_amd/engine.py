@@ -127,6 +127,19 @@ class Engine:
         check(lib().ptts_slot_open(self.handle, slot, voice.handle, a.ctypes.data_as(C.POINTER(C.c_int32)), a.size,
                                    C.byref(cp)))
 
+    def open_many(self, slots, voices, ids_list, params_list):
+        """Batched admission (ptts_slots_open): row slots[i] <- (voices[i], ids_list[i], params_list[i])."""
+        n = len(slots)
+        sl = np.ascontiguousarray(np.asarray(slots, np.int32))
+        arrs = [np.asarray(x, np.int32).reshape(-1) for x in ids_list]
+        nid = np.ascontiguousarray(np.array([a.size for a in arrs], np.int32))
+        cat = np.ascontiguousarray(np.concatenate(arrs) if arrs else np.zeros(0, np.int32))
+        vh = (C.c_void_p * n)(*[v.handle for v in voices])
+        ps = (GenParams * n)(*[p.to_c() for p in params_list])
+        i32 = C.POINTER(C.c_int32)
+        check(lib().ptts_slots_open(self.handle, n, sl.ctypes.data_as(i32), vh, cat.ctypes.data_as(i32),
+                                    nid.ctypes.data_as(i32), ps))
+
     def close_slot(self, slot: int):
         check(lib().ptts_slot_close(self.handle, slot))
 

@@ -96,6 +96,40 @@ def test_ragged_batch_matches_oracle(gpu_engine, oracle):
             assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
 
 
+def test_batched_admission_matches_oracle(gpu_engine, oracle):
+    """ptts_slots_open: 8 utterances admitted in one call, out of slot order, with ragged text
+    (0..37 tokens: padding rows inside 16-row groups, groups of one slot spanning several tiles)
+    and different voices; every row must equal its own oracle run."""
+    d = load_golden("e2e_lsd1.safetensors")
+    rng = np.random.default_rng(11)
+    B, steps = 8, 3
+    slots = [5, 0, 7, 2, 1, 6, 3, 4]
+    n_tok = [0, 1, 15, 16, 17, 37, 5, 32]
+    voices, ids_list, orc = [], [], {}
+    for i, b in enumerate(slots):
+        F = 3 + 2 * i
+        prompt = (d["prompt"][:F] * (1.0 - 0.05 * i)).astype(np.float32)
+        ids = rng.integers(0, 4000, size=n_tok[i]).astype(np.int32)
+        voices.append(gpu_engine.voice_from_prompt(prompt))
+        ids_list.append(ids)
+        s = oracle.new_state(128)
+        s.prefill(prompt)
+        if ids.size:
+            s.prefill_tokens(ids)
+        orc[b] = s
+    gpu_engine.open_many(slots, voices, ids_list, [params(max_frames=steps)] * B)
+    lat = {b: None for b in slots}
+    for _ in range(steps):
+        r = gpu_engine.step(B)
+        for b in slots:
+            o = orc[b].step(lat[b])
+            lat[b] = o["latent"]
+            assert r.valid[b]
+            assert abs(r.eos_logits[b] - o["eos_logit"]) <= 1e-4
+            np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
+            assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+
+
 def test_eos_termination_rule(gpu_engine):
     """tts_model.rs:1055-1063: the step reaching eos_step + frames_after_eos is yielded and is
     the last; without EOS the segment ends after max_gen_len frames."""
