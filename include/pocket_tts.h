@@ -48,6 +48,12 @@ typedef struct ptts_engine_config {
   void* weight_blob;        /* optional caller-owned device buffer of ptts_weight_blob_bytes() */
   int defer_weights;        /* 1: leave the blob unfilled; caller fills it (e.g. RCCL broadcast)
                                and then calls ptts_engine_finalize() */
+  int pipeline;             /* 0: each ptts_step returns the frame it computed.
+                               1: overlapped stepping - the Mimi decode of frame k runs on a
+                               second stream concurrently with the FlowLM step of frame k+1, so a
+                               call returns the frame computed by the PREVIOUS call (one extra
+                               call drains the last frame; the first call after admission
+                               returns no frame for the admitted rows). */
 } ptts_engine_config;
 
 /* Per-utterance generation parameters: TTSModel's public fields temp / eos_threshold /
@@ -134,6 +140,11 @@ int ptts_time_kernel(ptts_engine* e, int n_rows, const char* name, int reps, dou
 /* The step plan for n_rows: one line per op, "name<TAB>flops<TAB>bytes" (algorithmic cost of one
  * launch; 0 where not modelled). */
 int ptts_plan_ops(ptts_engine* e, int n_rows, char* buf, int buflen);
+
+/* Measurement: the step plan split at the FlowLM/flow-head -> Mimi boundary, timed as two
+ * graphs alone and launched together on two streams; us4 = {front, back, both, both with the
+ * front on a high-priority stream} microseconds per step. Clobbers engine state (timing only). */
+int ptts_probe_overlap(ptts_engine* e, int n_rows, int reps, double* us4);
 
 const char* ptts_last_error(void);
 

@@ -121,6 +121,13 @@ int ptts_slots_open(ptts_engine* e, int n, const int* slots, const ptts_voice* c
   return guard([&] { eng(e).slots_open(n, slots, voices, ids, n_ids, params); });
 }
 
+int ptts_probe_overlap(ptts_engine* e, int n_rows, int reps, double* us4) {
+  return guard([&] {
+    if (!us4) throw ptts::Error(PTTS_ERR_INVALID, "null output");
+    eng(e).overlap_probe(n_rows, reps, us4);
+  });
+}
+
 int ptts_slot_close(ptts_engine* e, int slot) { return guard([&] { eng(e).slot_close(slot); }); }
 
 int ptts_slot_set_latent(ptts_engine* e, int slot, const float* latent32) {
@@ -155,10 +162,14 @@ int ptts_generate(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* 
     std::vector<float> pcm((size_t)B * ptts::FRAME);
     std::vector<uint8_t> valid(B), last(B);
     int total = 0;
-    for (int it = 0; it < p->max_frames; ++it) {
+    // pipelined engines return each frame one call later: one extra call drains the last one
+    for (int it = 0; it < p->max_frames + 1; ++it) {
       E.step_async(B);
       E.fetch(B, pcm.data(), valid.data(), last.data(), nullptr, nullptr);
-      if (!valid[slot]) break;
+      if (!valid[slot]) {
+        if (it == 0 && E.pipelined()) continue;
+        break;
+      }
       const int take = std::max(0, std::min(ptts::FRAME, max_samples - total));
       if (pcm_out && take > 0) memcpy(pcm_out + total, pcm.data() + (size_t)slot * ptts::FRAME, sizeof(float) * take);
       total += ptts::FRAME;

@@ -68,6 +68,13 @@ Engine::Engine(const ptts_engine_config& cfg) {
   cur_ = dalloc((size_t)B * LDIM);
   qprev_ = dalloc((size_t)B * MD);
   eos_ = dalloc(B);
+  for (int q = 0; q < 2; ++q) {  // front -> back hand-off, one set per step parity
+    lat_out_[q] = dalloc((size_t)B * LDIM);
+    eos_out_[q] = dalloc(B);
+    flags_[q] = (FrameFlags*)dalloc((size_t)2 * B);
+    pcm_[q] = dalloc((size_t)B * FRAME);
+  }
+  mpartial_ = dalloc((size_t)2 * B * UP * 3 * MD);  // back part's own split-K slabs (Mimi QKV)
 
   // streaming conv histories (SEANetDecoder, seanet.rs:307-402): source T, channels, rows kept
   const int hT[8] = {16, 16, 96, 96, 480, 480, 1920, 1920};
@@ -114,14 +121,21 @@ Engine::Engine(const ptts_engine_config& cfg) {
     cv_[i] = dalloc((size_t)B * T * (ch / 2));
     ca_[i] = dalloc((size_t)B * T * ch);
   }
-  pcm_ = dalloc((size_t)B * FRAME);
   temb_ = dalloc((size_t)lsd_ * FD);
   temb_tmp_ = dalloc((size_t)2 * lsd_ * FD);
 
   PTTS_HIP(hipHostMalloc((void**)&h_pcm_, sizeof(float) * B * FRAME, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_eos_, sizeof(float) * B, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_lat_, sizeof(float) * B * LDIM, hipHostMallocDefault));
-  PTTS_HIP(hipHostMalloc((void**)&h_st_, sizeof(SlotState) * B, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_fl_, sizeof(FrameFlags) * B, hipHostMallocDefault));
+  PTTS_HIP(hipStreamCreateWithFlags(&stream_be_, hipStreamNonBlocking));
+  for (int q = 0; q < 2; ++q) {
+    PTTS_HIP(hipEventCreateWithFlags(&ev_front_[q], hipEventDisableTiming));
+    PTTS_HIP(hipEventCreateWithFlags(&ev_back_[q], hipEventDisableTiming));
+    PTTS_HIP(hipEventRecord(ev_front_[q], stream_));
+    PTTS_HIP(hipEventRecord(ev_back_[q], stream_));
+  }
+  pipeline_ = cfg.pipeline != 0;
 
   if (!cfg.defer_weights) {
     std::unique_ptr<TensorSource> src = cfg.weights_path && cfg.weights_path[0]
@@ -135,13 +149,19 @@ Engine::Engine(const ptts_engine_config& cfg) {
 Engine::~Engine() {
   (void)hipSetDevice(dev_);
   if (stream_) (void)hipStreamSynchronize(stream_);
+  if (stream_be_) (void)hipStreamSynchronize(stream_be_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
+  for (int q = 0; q < 2; ++q) {
+    if (ev_front_[q]) (void)hipEventDestroy(ev_front_[q]);
+    if (ev_back_[q]) (void)hipEventDestroy(ev_back_[q]);
+  }
+  if (stream_be_) (void)hipStreamDestroy(stream_be_);
   for (void* p : allocs_) (void)hipFree(p);
   if (h_pcm_) (void)hipHostFree(h_pcm_);
   if (h_eos_) (void)hipHostFree(h_eos_);
   if (h_lat_) (void)hipHostFree(h_lat_);
-  if (h_st_) (void)hipHostFree(h_st_);
+  if (h_fl_) (void)hipHostFree(h_fl_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -336,8 +356,8 @@ void Engine::prefill_rows(std::vector<Op>& ops, int slot, int T, int p0) {
   flow_layers(ops, T, map, 16, false, "prefill");
 }
 
-std::vector<Op> Engine::build_step(int B) {
-  std::vector<Op> ops;
+// FRONT part of a step (FlowLM + flow head) for rows [0, B), handing its frame to parity `par`.
+void Engine::build_front(std::vector<Op>& ops, int B, int par) {
   int S = 1;
   // ---- FlowLM step (flow_lm.rs:98-164): input_linear -> transformer -> out_norm
   linear_split(ops, "flow.input_gemm", lat_in_, LDIM, B, W(L_.input_linear), D, LDIM, &S);
@@ -466,14 +486,33 @@ std::vector<Op> Engine::build_step(int B) {
       ops.push_back({p + ".euler", [a](hipStream_t s) { row_reduce(a, s); }});
     }
   }
+  // ---- EOS rule, frame flags, hand-off of the frame to the back part, next backbone input
+  {
+    FrontCommitArgs c{};
+    c.B = B;
+    c.st = st_;
+    c.eos = eos_;
+    c.cur = cur_;
+    c.lat_in = lat_in_;
+    c.lat_out = lat_out_[par];
+    c.eos_out = eos_out_[par];
+    c.flags = flags_[par];
+    c.fpos = fpos_;
+    ops.push_back({"front_commit", [c](hipStream_t s) { front_commit(c, s); }});
+  }
+}
+
+// BACK part of a step: Mimi decode of the frames the front part left in parity `par`.
+void Engine::build_back(std::vector<Op>& ops, int B, int par) {
   // ---- Mimi decode (mimi.rs:143-157): quantize + upsample, decoder transformer, SEANet decoder
   {
-    const float *lat = cur_, *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w), *wu = W(L_.up_w);
+    const float *lat = lat_out_[par], *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w),
+                *wu = W(L_.up_w);
     const float *lw = W(L_.mdec[0].n1w), *lb = W(L_.mdec[0].n1b);
     float *qp = qprev_, *x = mx_, *h = mh_;
-    const SlotState* st = st_;
+    const FrameFlags* fl = flags_[par];
     ops.push_back({"mimi.quant_upsample",
-                   [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qp, st, x, h, lw, lb, s); }});
+                   [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qp, fl, x, h, lw, lb, s); }});
   }
   const int MR = B * UP;
   RowMap mmap{0, UP, 0, mpos_};
@@ -497,11 +536,10 @@ std::vector<Op> Engine::build_step(int B) {
       a.ldx = MD;
       a.W = W(t.in_proj);
       a.S = S;
-      a.partial = partial_;
-      PTTS_REQUIRE((size_t)S * MR * 3 * MD <= pcap_, "split-K partial buffer too small");
+      a.partial = mpartial_;
       ops.push_back({p + ".qkv_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * 3 * MD * MD,
                      4.0 * (3.0 * MD * MD + (double)MR * MD + (double)S * MR * 3 * MD)});
-      const float* P = partial_;
+      const float* P = mpartial_;
       float* Q = mq_;
       ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(P, S, nullptr, MR, MNH, mmap, kv, Q, s); }});
     } else {
@@ -556,23 +594,27 @@ std::vector<Op> Engine::build_step(int B) {
   }
   {
     const float *X = ca_[2], *H = hist_[7], *w = W(L_.dfin_w), *b = W(L_.dfin_b);
-    float* Y = pcm_;
+    float* Y = pcm_[par];
     ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, FRAME, 64, 3, w, b, Y, s); }});
   }
-  // ---- commit: conv histories, positions, next backbone input
+  // ---- commit of the back part: conv histories and Mimi positions of rows with a frame
   {
     CommitArgs c{};
     const float* srcs[8] = {mx_, a0_, cb_[0], ca_[0], cb_[1], ca_[1], cb_[2], ca_[2]};
     for (int i = 0; i < 8; ++i) c.h[i] = HistDesc{srcs[i], hist_[i], hist_T_[i], hist_C_[i], hist_P_[i]};
     c.nh = 8;
     c.B = B;
-    c.st = st_;
-    c.latent_next = lat_in_;
-    c.latent = cur_;
-    c.fpos = fpos_;
+    c.flags = flags_[par];
     c.mpos = mpos_;
     ops.push_back({"commit", [c](hipStream_t s) { step_commit(c, s); }});
   }
+}
+
+// The whole step in plan order (front then back, parity 0): plan listing and per-op timing.
+std::vector<Op> Engine::build_step(int B) {
+  std::vector<Op> ops;
+  build_front(ops, B, 0);
+  build_back(ops, B, 0);
   return ops;
 }
 
@@ -587,49 +629,95 @@ std::vector<std::string> Engine::plan_names(int B) {
   return v;
 }
 
+hipGraphExec_t Engine::part_graph(int part, int B, int par) {
+  const int key = (B * 2 + part) * 2 + par;
+  auto it = graphs_.find(key);
+  if (it != graphs_.end()) return it->second;
+  std::vector<Op> ops;
+  if (part == 0) build_front(ops, B, par);
+  else build_back(ops, B, par);
+  hipGraph_t g = nullptr;
+  PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+  try {
+    for (const Op& op : ops) op.fn(stream_);
+  } catch (...) {
+    (void)hipStreamEndCapture(stream_, &g);
+    throw;
+  }
+  PTTS_HIP(hipStreamEndCapture(stream_, &g));
+  hipGraphExec_t ge = nullptr;
+  PTTS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  graph_defs_[key] = g;
+  graphs_[key] = ge;
+  return ge;
+}
+
+// One call = one step of the generation loop for rows [0, B).
+//   sequential: front(k) then back(k) on one stream; the call's frame is frame k.
+//   pipelined:  front(k) on stream_ || back(k-1) on stream_be_ (the back part decodes the frame
+//               the previous call's front part produced); the call's frame is frame k-1. The
+//               parity buffers make the two independent: front(k) only waits for back(k-2)
+//               (last reader of its parity), back(k-1) for front(k-1).
 void Engine::step_async(int B) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
   PTTS_HIP(hipSetDevice(dev_));
-  auto it = graphs_.find(B);
-  if (it == graphs_.end()) {
-    std::vector<Op> ops = build_step(B);
-    hipGraph_t g = nullptr;
-    PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-    try {
-      for (const Op& op : ops) op.fn(stream_);
-    } catch (...) {
-      (void)hipStreamEndCapture(stream_, &g);
-      throw;
-    }
-    PTTS_HIP(hipStreamEndCapture(stream_, &g));
-    hipGraphExec_t ge = nullptr;
-    PTTS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-    graph_defs_[B] = g;
-    it = graphs_.emplace(B, ge).first;
+  const int par = (int)(k_ & 1);
+  hipGraphExec_t front = part_graph(0, B, par);
+  if (!pipeline_) {
+    hipGraphExec_t back = part_graph(1, B, par);
+    PTTS_HIP(hipGraphLaunch(front, stream_));
+    PTTS_HIP(hipGraphLaunch(back, stream_));
+    out_par_ = par;
+    out_rows_ = B;
+  } else {
+    const int prev_rows = k_ > 0 ? front_rows_ : B;
+    hipGraphExec_t back = part_graph(1, prev_rows, par ^ 1);
+    PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[par], 0));
+    PTTS_HIP(hipGraphLaunch(front, stream_));
+    PTTS_HIP(hipEventRecord(ev_front_[par], stream_));
+    PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[par ^ 1], 0));
+    PTTS_HIP(hipGraphLaunch(back, stream_be_));
+    PTTS_HIP(hipEventRecord(ev_back_[par ^ 1], stream_be_));
+    out_par_ = par ^ 1;
+    out_rows_ = prev_rows;
   }
-  PTTS_HIP(hipGraphLaunch(it->second, stream_));
+  front_rows_ = B;
+  ++k_;
 }
 
 void Engine::sync() {
   PTTS_HIP(hipSetDevice(dev_));
   PTTS_HIP(hipStreamSynchronize(stream_));
+  PTTS_HIP(hipStreamSynchronize(stream_be_));
 }
 
+// Outputs of the last call's frame (see step_async); rows past the rows that frame covered
+// report no frame.
 void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat) {
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
-  PTTS_HIP(hipSetDevice(dev_));
-  if (pcm) PTTS_HIP(hipMemcpyAsync(h_pcm_, pcm_, sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, stream_));
-  if (eos) PTTS_HIP(hipMemcpyAsync(h_eos_, eos_, sizeof(float) * B, hipMemcpyDeviceToHost, stream_));
-  if (lat) PTTS_HIP(hipMemcpyAsync(h_lat_, cur_, sizeof(float) * B * LDIM, hipMemcpyDeviceToHost, stream_));
-  PTTS_HIP(hipMemcpyAsync(h_st_, st_, sizeof(SlotState) * B, hipMemcpyDeviceToHost, stream_));
-  PTTS_HIP(hipStreamSynchronize(stream_));
-  if (pcm) memcpy(pcm, h_pcm_, sizeof(float) * B * FRAME);
-  if (eos) memcpy(eos, h_eos_, sizeof(float) * B);
-  if (lat) memcpy(lat, h_lat_, sizeof(float) * B * LDIM);
+  sync();
+  const int q = out_par_;
+  const int n = std::min(B, out_rows_);
+  if (n > 0) {
+    if (pcm) PTTS_HIP(hipMemcpy(h_pcm_, pcm_[q], sizeof(float) * n * FRAME, hipMemcpyDeviceToHost));
+    if (eos) PTTS_HIP(hipMemcpy(h_eos_, eos_out_[q], sizeof(float) * n, hipMemcpyDeviceToHost));
+    if (lat) PTTS_HIP(hipMemcpy(h_lat_, lat_out_[q], sizeof(float) * n * LDIM, hipMemcpyDeviceToHost));
+    PTTS_HIP(hipMemcpy(h_fl_, flags_[q], sizeof(FrameFlags) * n, hipMemcpyDeviceToHost));
+  }
   for (int b = 0; b < B; ++b) {
-    if (valid) valid[b] = (uint8_t)(h_st_[b].valid != 0);
-    if (last) last[b] = (uint8_t)(h_st_[b].valid && h_st_[b].last);
+    const bool ok = b < n && h_fl_[b].valid;
+    if (valid) valid[b] = ok;
+    if (last) last[b] = ok && h_fl_[b].last;
+    if (pcm) {
+      if (b < n) memcpy(pcm + (size_t)b * FRAME, h_pcm_ + (size_t)b * FRAME, sizeof(float) * FRAME);
+      else memset(pcm + (size_t)b * FRAME, 0, sizeof(float) * FRAME);
+    }
+    if (eos) eos[b] = b < n ? h_eos_[b] : 0.f;
+    if (lat) {
+      if (b < n) memcpy(lat + (size_t)b * LDIM, h_lat_ + (size_t)b * LDIM, sizeof(float) * LDIM);
+      else memset(lat + (size_t)b * LDIM, 0, sizeof(float) * LDIM);
+    }
   }
 }
 
@@ -658,13 +746,79 @@ double Engine::time_op(int B, const std::string& name, int reps) {
   return 1000.0 * ms / reps;
 }
 
+// Measurement hook: the step plan split at the FlowLM/flow-head -> Mimi boundary into two graphs;
+// times each alone and both launched together on two streams (no dependency, data races are
+// irrelevant for timing). us[0] = front alone, us[1] = back alone, us[2] = both concurrently.
+void Engine::overlap_probe(int B, int reps, double* us) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
+  PTTS_REQUIRE(B >= 1 && B <= max_slots_ && reps >= 1, "bad probe arguments");
+  PTTS_HIP(hipSetDevice(dev_));
+  std::vector<Op> ops = build_step(B);
+  size_t cut = 0;
+  while (cut < ops.size() && ops[cut].name != "mimi.quant_upsample") ++cut;
+  PTTS_REQUIRE(cut < ops.size(), "step plan has no Mimi stage");
+  hipStream_t s2 = nullptr, s_hi = nullptr, s_lo = nullptr;
+  PTTS_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  int prio_lo = 0, prio_hi = 0;
+  PTTS_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  PTTS_HIP(hipStreamCreateWithPriority(&s_hi, hipStreamNonBlocking, prio_hi));
+  PTTS_HIP(hipStreamCreateWithPriority(&s_lo, hipStreamNonBlocking, prio_lo));
+  hipGraphExec_t ge[2] = {};
+  hipGraph_t g[2] = {};
+  for (int part = 0; part < 2; ++part) {
+    PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    for (size_t i = part ? cut : 0; i < (part ? ops.size() : cut); ++i) ops[i].fn(stream_);
+    PTTS_HIP(hipStreamEndCapture(stream_, &g[part]));
+    PTTS_HIP(hipGraphInstantiate(&ge[part], g[part], nullptr, nullptr, 0));
+  }
+  hipEvent_t e0, e1, e2;
+  PTTS_HIP(hipEventCreate(&e0));
+  PTTS_HIP(hipEventCreate(&e1));
+  PTTS_HIP(hipEventCreate(&e2));
+  auto timed = [&](int mode) {
+    hipStream_t sa = mode == 3 ? s_hi : stream_, sb = mode == 3 ? s_lo : s2;
+    for (int w = 0; w < 2; ++w) {
+      if (mode != 1) PTTS_HIP(hipGraphLaunch(ge[0], sa));
+      if (mode != 0) PTTS_HIP(hipGraphLaunch(ge[1], sb));
+    }
+    PTTS_HIP(hipStreamSynchronize(sa));
+    PTTS_HIP(hipStreamSynchronize(sb));
+    PTTS_HIP(hipEventRecord(e0, sa));
+    PTTS_HIP(hipStreamWaitEvent(sb, e0, 0));
+    for (int r = 0; r < reps; ++r) {
+      if (mode != 1) PTTS_HIP(hipGraphLaunch(ge[0], sa));
+      if (mode != 0) PTTS_HIP(hipGraphLaunch(ge[1], sb));
+    }
+    PTTS_HIP(hipEventRecord(e2, sb));
+    PTTS_HIP(hipStreamWaitEvent(sa, e2, 0));
+    PTTS_HIP(hipEventRecord(e1, sa));
+    PTTS_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    PTTS_HIP(hipEventElapsedTime(&ms, e0, e1));
+    return 1000.0 * ms / reps;
+  };
+  us[0] = timed(0);
+  us[1] = timed(1);
+  us[2] = timed(2);
+  us[3] = timed(3);
+  for (int part = 0; part < 2; ++part) {
+    (void)hipGraphExecDestroy(ge[part]);
+    (void)hipGraphDestroy(g[part]);
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipEventDestroy(e2);
+  (void)hipStreamDestroy(s2);
+  (void)hipStreamDestroy(s_hi);
+  (void)hipStreamDestroy(s_lo);
+}
+
 // ------------------------------------------------------------------ voices and slots
 ptts_voice* Engine::voice_from_prompt(const float* prompt, int F) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(prompt != nullptr && F >= 1, "empty prompt");
   PTTS_REQUIRE(F < max_ctx_, "prompt longer than max_ctx");
-  PTTS_HIP(hipSetDevice(dev_));
-  PTTS_HIP(hipStreamSynchronize(stream_));
+  sync();
   const int scratch = max_slots_;
   for (int c0 = 0; c0 < F; c0 += PREFILL) {
     const int T = std::min(PREFILL, F - c0);
@@ -721,7 +875,7 @@ void Engine::encoder_transformer(std::vector<Op>& ops, float* x, int T, float* h
 ptts_voice* Engine::voice_from_pcm(const float* pcm, int n) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(pcm != nullptr && n >= 1, "empty PCM");
-  PTTS_HIP(hipSetDevice(dev_));
+  sync();
   const int Np = (n + FRAME - 1) / FRAME * FRAME;  // zero-pad to whole frames (mimi.py:103)
   const int F = Np / FRAME, Te = Np / 120;
   PTTS_REQUIRE(F < max_ctx_, "voice prompt longer than max_ctx");
@@ -825,8 +979,7 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
       PTTS_REQUIRE(ids[total_ids + j] >= 0 && ids[total_ids + j] < VOCAB, "token id out of range");
     total_ids += n_ids[i];
   }
-  PTTS_HIP(hipSetDevice(dev_));
-  PTTS_HIP(hipStreamSynchronize(stream_));
+  sync();
   // copy-on-admit of the immutable voice prefixes
   for (int i = 0; i < n; ++i) {
     const ptts_voice* v = voices[i];
@@ -844,13 +997,11 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     s.active = 1;
     s.step = 0;
     s.eos_step = -1;
-    s.last = 0;
     s.frames_after_eos = p.frames_after_eos;
     s.max_frames = p.max_frames;
     s.temp = p.temp;
     s.eos_threshold = p.eos_threshold;
     s.noise_clamp = p.noise_clamp;
-    s.valid = 0;
     s.seed = p.seed;
     fp[i] = voices[i]->F + n_ids[i];
   }
@@ -875,6 +1026,8 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     r.st = st_;
     r.fpos = fpos_;
     r.mpos = mpos_;
+    r.flags0 = flags_[0];
+    r.flags1 = flags_[1];
     slot_reset(r, stream_);
     PTTS_HIP(hipGetLastError());
   }
@@ -920,17 +1073,16 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
 
 void Engine::slot_close(int slot) {
   PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
-  PTTS_HIP(hipSetDevice(dev_));
-  PTTS_HIP(hipStreamSynchronize(stream_));
+  sync();
   SlotState s{};
   s.eos_step = -1;
   PTTS_HIP(hipMemcpy(st_ + slot, &s, sizeof s, hipMemcpyHostToDevice));
+  for (int q = 0; q < 2; ++q) PTTS_HIP(hipMemset(flags_[q] + slot, 0, sizeof(FrameFlags)));  // drop pending frame
 }
 
 void Engine::set_latent(int slot, const float* lat) {
   PTTS_REQUIRE(slot >= 0 && slot < max_slots_ && lat != nullptr, "bad slot / latent");
-  PTTS_HIP(hipSetDevice(dev_));
-  PTTS_HIP(hipStreamSynchronize(stream_));
+  sync();
   PTTS_HIP(hipMemcpy(lat_in_ + (size_t)slot * LDIM, lat, sizeof(float) * LDIM, hipMemcpyHostToDevice));
 }
 

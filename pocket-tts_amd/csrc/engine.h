@@ -36,6 +36,7 @@ class Engine {
   void finalize();
   float* blob() { return blob_; }
   int max_slots() const { return max_slots_; }
+  bool pipelined() const { return pipeline_; }
 
   ptts_voice* voice_from_prompt(const float* prompt, int F);
   ptts_voice* voice_from_pcm(const float* pcm, int n);
@@ -50,6 +51,7 @@ class Engine {
   void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat);
 
   double time_op(int B, const std::string& name, int reps);
+  void overlap_probe(int B, int reps, double* us);
   std::vector<std::string> plan_names(int B);
 
  private:
@@ -59,6 +61,9 @@ class Engine {
   void prefill_rows(std::vector<Op>& ops, int slot, int T, int p0);
   void run_ops(const std::vector<Op>& ops);
   std::vector<Op> build_step(int B);
+  void build_front(std::vector<Op>& ops, int B, int par);
+  void build_back(std::vector<Op>& ops, int B, int par);
+  hipGraphExec_t part_graph(int part, int B, int par);
   void flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag);
   void linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M, const float* Wt,
                     int N, int K, int* S_out);
@@ -104,14 +109,27 @@ class Engine {
   float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;
   float* a0_ = nullptr;
   float *cb_[3] = {}, *cv_[3] = {}, *ca_[3] = {};
-  float* pcm_ = nullptr;
+  // front -> back hand-off per step parity, and the back part's own split-K slabs
+  float* lat_out_[2] = {};
+  float* eos_out_[2] = {};
+  FrameFlags* flags_[2] = {};
+  float* pcm_[2] = {};
+  float* mpartial_ = nullptr;
+  // pipelined stepping (cfg.pipeline): back part on its own stream, parity events
+  bool pipeline_ = false;
+  hipStream_t stream_be_ = nullptr;
+  hipEvent_t ev_front_[2] = {}, ev_back_[2] = {};
+  long long k_ = 0;          // steps issued
+  int out_par_ = 0;          // parity of the frame the last call produced
+  int out_rows_ = 0;         // rows that frame covers
+  int front_rows_ = 0;       // rows of the last front part
   float *temb_ = nullptr, *temb_tmp_ = nullptr;
 
   // pinned host staging
   float* h_pcm_ = nullptr;
   float* h_eos_ = nullptr;
   float* h_lat_ = nullptr;
-  SlotState* h_st_ = nullptr;
+  FrameFlags* h_fl_ = nullptr;
 
   std::map<int, hipGraphExec_t> graphs_;
   std::map<int, hipGraph_t> graph_defs_;

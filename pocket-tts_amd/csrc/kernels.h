@@ -107,29 +107,53 @@ void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window
 
 // ---------------------------------------------------------------------------------------------
 // Per-slot generation bookkeeping (device resident so the step can be replayed as a graph).
+// The step is split into a FRONT part (FlowLM + flow head: produces this step's latent and
+// frame flags, owns SlotState / FlowLM KV / positions) and a BACK part (Mimi decode of a frame
+// produced by the front, owns the Mimi ring, conv histories and Mimi positions). They exchange
+// frames through per-parity buffers, so the back part of frame k can run concurrently with the
+// front part of frame k+1.
 struct SlotState {
-  int active;  // row takes part in this step
+  int active;  // row still generating
   int step;    // generation step index within the segment
   int eos_step;
-  int last;  // set by the step that yields the final frame
   int frames_after_eos, max_frames;
   float temp, eos_threshold, noise_clamp;
-  int valid;  // this step produced a frame for the row
   unsigned long long seed;
 };
+struct FrameFlags {
+  int valid;  // the front produced a frame for this row at this step
+  int last;   // ... and it is the row's final frame (EOS tail reached or max_frames)
+};
 
-// After the cond_embed|out_eos split-K GEMM: c = sum + b, eos logit, EOS state machine,
-// y_s = silu(temb[s] + c) for each lsd step, x0 noise -> cur.
+// After the cond_embed|out_eos split-K GEMM: c = sum + b, eos logit -> eos_out,
+// y_s = silu(temb[s] + c) for each lsd step, x0 noise -> cur (reads SlotState only).
 void flow_cond(const float* P, int S, int B, const float* bias, const float* temb, int lsd_steps,
-               SlotState* st, float* ysilu, float* cur, float* eos_out, hipStream_t s);
+               const SlotState* st, float* ysilu, float* cur, float* eos_out, hipStream_t s);
+
+// End of the front part: EOS state machine (tts_model.rs:1055-1063), frame flags, the frame's
+// latent / eos logit into the parity buffers, next backbone input, step / FlowLM position.
+struct FrontCommitArgs {
+  int B;
+  SlotState* st;
+  const float* eos;  // [B] this step's logits
+  const float* cur;  // [B][32] this step's latent
+  float* lat_in;     // [B][32] backbone input of the next step
+  float* lat_out;    // [B][32] frame latent (parity buffer)
+  float* eos_out;    // [B] frame eos logit (parity buffer)
+  FrameFlags* flags; // [B] (parity buffer)
+  int* fpos;         // FlowLM positions, += 1
+};
+void front_commit(const FrontCommitArgs& a, hipStream_t s);
 
 // Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0.
-// latent [B][32] -> x [B*16][512], h = LN(x); qprev [B][512] carries the overlap-add history.
+// latent [B][32] -> x [B*16][512], h = LN(x); qprev [B][512] carries the overlap-add history
+// (advanced only for rows whose frame is valid).
 void quant_upsample(const float* latent, int B, const float* emb_std, const float* emb_mean,
-                    const float* wq, const float* wup, float* qprev, const SlotState* st, float* x, float* h,
+                    const float* wq, const float* wup, float* qprev, const FrameFlags* fl, float* x, float* h,
                     const float* ln_w, const float* ln_b, hipStream_t s);
 
-// Copy the last P rows of each conv input into its history, and advance per-slot counters.
+// End of the back part, for rows with a valid frame: copy the last P rows of each conv input
+// into its history, advance the Mimi position.
 struct HistDesc {
   const float* src;  // [B][T][C]
   float* dst;        // [B][P][C]
@@ -139,11 +163,8 @@ struct CommitArgs {
   HistDesc h[10];
   int nh;
   int B;
-  SlotState* st;
-  float* latent_next;   // [B][32] backbone input for the next step
-  const float* latent;  // [B][32] this step's latent
-  int* fpos;            // FlowLM positions in cache, += 1
-  int* mpos;            // Mimi decoder positions, += 16
+  const FrameFlags* flags;
+  int* mpos;  // Mimi decoder positions, += 16
 };
 void step_commit(const CommitArgs& a, hipStream_t s);
 
@@ -160,6 +181,8 @@ struct ResetArgs {
   const float* bos;
   const SlotState* st_src;
   const int* fpos_src;
+  FrameFlags* flags0;  // both parity buffers: an undrained frame of the slot's previous
+  FrameFlags* flags1;  // utterance is discarded
   SlotState* st;
   int* fpos;
   int* mpos;

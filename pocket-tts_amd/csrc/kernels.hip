@@ -49,22 +49,29 @@ __device__ __forceinline__ float wave_max(float v) {
 //             partial tiles summed through LDS (skinny M <= 32 GEMMs: more waves per tile)
 //   LAYOUT 1  2x2 waves = WG tile 64x64     LAYOUT 2  1x4 = 32x128     LAYOUT 3  4x1 = 128x32
 //   (each wave runs the whole K chain of its z-slice; neighbours share A rows / W rows in L1/L2)
+//   K-split variants of LAYOUT 0: LAYOUT 9 = 8 waves (2 per SIMD at one workgroup per CU),
+//   LAYOUT 10 = 4 waves with two chunks in flight, LAYOUT 17 = 8 waves, two chunks in flight.
 template <int LAYOUT>
 struct Lay {
+  static constexpr bool KSPLIT = LAYOUT == 0 || LAYOUT == 9 || LAYOUT == 10 || LAYOUT == 17;
+  static constexpr int NW = (LAYOUT == 9 || LAYOUT == 17) ? 8 : 4;  // waves per workgroup
+  static constexpr int PF = (LAYOUT == 10 || LAYOUT == 17) ? 2 : 1;  // chunks in flight per wave
   static constexpr int WM = LAYOUT == 1 ? 2 : (LAYOUT == 3 ? 4 : 1);
   static constexpr int WN = LAYOUT == 1 ? 2 : (LAYOUT == 2 ? 4 : 1);
 };
 
 template <int MODE, int LAYOUT>
-__global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
-  __shared__ float red[LAYOUT == 0 ? 4 * 16 * 64 : 1];
+__global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
+  constexpr bool KS = Lay<LAYOUT>::KSPLIT;
+  constexpr int NW = Lay<LAYOUT>::NW;
+  __shared__ float red[KS ? NW * 16 * 64 : 1];
   const int lane = threadIdx.x & 63;
   // wave-uniform (SGPR) so that the chunk loop is a scalar loop: no exec-masked joins, and
   // the compiler can keep the next chunk's loads in flight across the MFMAs (counted vmcnt)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
   constexpr int WM = Lay<LAYOUT>::WM, WN = Lay<LAYOUT>::WN;
-  const int wm = LAYOUT == 0 ? 0 : wave / WN, wn = LAYOUT == 0 ? 0 : wave % WN;
+  const int wm = KS ? 0 : wave / WN, wn = KS ? 0 : wave % WN;
   const int n0 = (blockIdx.x * WN + wn) * 32, m0 = (blockIdx.y * WM + wm) * 32, z = blockIdx.z;
   const int nchunks = a.K >> 5;
   int cb = 0, ce = nchunks, phase = 0;
@@ -128,25 +135,46 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
   };
-  // ping-pong register sets: chunk c is multiplied while chunk c+CSTEP is in flight
+  // rotating register sets: chunk c is multiplied while the next PF chunks are in flight
   float4 a0[4], b0[4], a1[4], b1[4];
-  constexpr int CSTEP = LAYOUT == 0 ? 4 : 1;
-  int c = LAYOUT == 0 ? cb + wave : cb;
+  constexpr int CSTEP = KS ? NW : 1;
+  int c = KS ? cb + wave : cb;
   if (!wave_live) c = ce;
-  // The prefetch is unconditional (past the end it re-reads the last chunk, never used), so no
+  // The prefetch is unconditional (past the end it re-reads a valid chunk, never used), so no
   // control-flow join sits between a load and the MFMAs that must not wait for it.
-  if (c < ce) {
-    load(c, a0, b0);
-    for (;;) {
-      const int c1 = c + CSTEP;
-      load(c1 < ce ? c1 : c, a1, b1);
-      mma(a0, b0);
-      if (c1 >= ce) break;
-      const int c2 = c1 + CSTEP;
-      load(c2 < ce ? c2 : c1, a0, b0);
-      mma(a1, b1);
-      if (c2 >= ce) break;
-      c = c2;
+  if (Lay<LAYOUT>::PF == 1) {
+    if (c < ce) {
+      load(c, a0, b0);
+      for (;;) {
+        const int c1 = c + CSTEP;
+        load(c1 < ce ? c1 : c, a1, b1);
+        mma(a0, b0);
+        if (c1 >= ce) break;
+        const int c2 = c1 + CSTEP;
+        load(c2 < ce ? c2 : c1, a0, b0);
+        mma(a1, b1);
+        if (c2 >= ce) break;
+        c = c2;
+      }
+    }
+  } else {
+    float4 a2[4], b2[4];
+    if (c < ce) {
+      load(c, a0, b0);
+      load(c + CSTEP < ce ? c + CSTEP : c, a1, b1);
+      for (;;) {  // invariant: a0 = chunk c, a1 = chunk c+CSTEP (if any), a2 free
+        const int c1 = c + CSTEP, c2 = c + 2 * CSTEP, c3 = c + 3 * CSTEP, c4 = c + 4 * CSTEP;
+        load(c2 < ce ? c2 : c, a2, b2);
+        mma(a0, b0);
+        if (c1 >= ce) break;
+        load(c3 < ce ? c3 : c, a0, b0);
+        mma(a1, b1);
+        if (c2 >= ce) break;
+        load(c4 < ce ? c4 : c, a1, b1);
+        mma(a2, b2);
+        if (c3 >= ce) break;
+        c = c3;
+      }
     }
   }
 
@@ -171,16 +199,17 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
     if (a.R) v += a.R[yrow * a.ldr + col];
     a.Y[yrow * a.ldy + col] = v;
   };
-  if (LAYOUT == 0) {
+  if (KS) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[g];
     __syncthreads();
+    constexpr int GPW = 16 / NW;  // output registers finished per wave
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      const int g = wave * 4 + gg;
-      float v = red[(0 * 16 + g) * 64 + lane] + red[(1 * 16 + g) * 64 + lane];
-      v += red[(2 * 16 + g) * 64 + lane];
-      v += red[(3 * 16 + g) * 64 + lane];
+    for (int gg = 0; gg < GPW; ++gg) {
+      const int g = wave * GPW + gg;
+      float v = red[(0 * 16 + g) * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v += red[(w * 16 + g) * 64 + lane];
       store(g, v);
     }
   } else if (wave_live) {
@@ -562,6 +591,15 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
       break;
     case 3:
       hipLaunchKernelGGL((k_gemm<MODE, 3>), dim3((a.N + 31) / 32, (a.M + 127) / 128, grid_z), dim3(256), 0, s, a);
+      break;
+    case 9:
+      hipLaunchKernelGGL((k_gemm<MODE, 9>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(512), 0, s, a);
+      break;
+    case 10:
+      hipLaunchKernelGGL((k_gemm<MODE, 10>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+      break;
+    case 17:
+      hipLaunchKernelGGL((k_gemm<MODE, 17>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(512), 0, s, a);
       break;
     default:
       hipLaunchKernelGGL((k_gemm<MODE, 0>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
@@ -1089,7 +1127,8 @@ __device__ float normal_at(unsigned long long seed, int step, int k, int attempt
 }
 
 __global__ __launch_bounds__(256) void k_flow_cond(const float* P, int S, int B, const float* bias, const float* temb,
-                                                   int lsd, SlotState* st, float* ysilu, float* cur, float* eos_out) {
+                                                   int lsd, const SlotState* st, float* ysilu, float* cur,
+                                                   float* eos_out) {
   const int b = blockIdx.x, tid = threadIdx.x;
   const int NC = 513;  // cond_embed (512) | out_eos (1)
   for (int n = tid; n < 512; n += 256) {
@@ -1098,19 +1137,11 @@ __global__ __launch_bounds__(256) void k_flow_cond(const float* P, int S, int B,
     c += bias[n];
     for (int s = 0; s < lsd; ++s) ysilu[((long)s * B + b) * 512 + n] = silu(temb[s * 512 + n] + c);
   }
-  SlotState& ss = st[b];
-  if (tid == 0) {
+  const SlotState& ss = st[b];
+  if (tid == 0) {  // out_eos logit (flow_lm.rs:139-145); the EOS rule runs in front_commit
     float e = 0.f;
     for (int z = 0; z < S; ++z) e += P[((long)z * B + b) * NC + 512];
-    e += bias[512];
-    eos_out[b] = e;
-    ss.valid = ss.active;
-    ss.last = 0;
-    if (ss.active) {  // tts_model.rs:1055-1063 + map_while over 0..max_gen_len
-      if (e > ss.eos_threshold && ss.eos_step < 0) ss.eos_step = ss.step;
-      const bool tail = ss.eos_step >= 0 && ss.step >= ss.eos_step + ss.frames_after_eos;
-      ss.last = (tail || ss.step + 1 >= ss.max_frames) ? 1 : 0;
-    }
+    eos_out[b] = e + bias[512];
   }
   if (tid < 32) {
     float x0 = 0.f;
@@ -1128,8 +1159,8 @@ __global__ __launch_bounds__(256) void k_flow_cond(const float* P, int S, int B,
   }
 }
 
-void flow_cond(const float* P, int S, int B, const float* bias, const float* temb, int lsd_steps, SlotState* st,
-               float* ysilu, float* cur, float* eos_out, hipStream_t s) {
+void flow_cond(const float* P, int S, int B, const float* bias, const float* temb, int lsd_steps,
+               const SlotState* st, float* ysilu, float* cur, float* eos_out, hipStream_t s) {
   hipLaunchKernelGGL(k_flow_cond, dim3(B), dim3(256), 0, s, P, S, B, bias, temb, lsd_steps, st, ysilu, cur, eos_out);
 }
 
@@ -1140,14 +1171,14 @@ void flow_cond(const float* P, int S, int B, const float* bias, const float* tem
 // =============================================================================================
 __global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, const float* emb_std,
                                                         const float* emb_mean, const float* wq, const float* wup,
-                                                        float* qprev, const SlotState* st, float* x, float* h,
+                                                        float* qprev, const FrameFlags* fl, float* x, float* h,
                                                         const float* ln_w, const float* ln_b) {
   __shared__ float sz[32];
   __shared__ float sx[16 * 512];
   const int b = blockIdx.x, tid = threadIdx.x;
   if (tid < 32) sz[tid] = latent[b * 32 + tid] * emb_std[tid] + emb_mean[tid];
   __syncthreads();
-  const bool upd = st[b].valid != 0;
+  const bool upd = fl[b].valid != 0;
   for (int c = tid; c < 512; c += 256) {
     float q = 0.f;
     for (int k = 0; k < 32; ++k) q += wq[c * 32 + k] * sz[k];
@@ -1182,9 +1213,9 @@ __global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, con
 }
 
 void quant_upsample(const float* latent, int B, const float* emb_std, const float* emb_mean, const float* wq,
-                    const float* wup, float* qprev, const SlotState* st, float* x, float* h, const float* ln_w,
+                    const float* wup, float* qprev, const FrameFlags* fl, float* x, float* h, const float* ln_w,
                     const float* ln_b, hipStream_t s) {
-  hipLaunchKernelGGL(k_quant_upsample, dim3(B), dim3(256), 0, s, latent, emb_std, emb_mean, wq, wup, qprev, st, x,
+  hipLaunchKernelGGL(k_quant_upsample, dim3(B), dim3(256), 0, s, latent, emb_std, emb_mean, wq, wup, qprev, fl, x,
                      h, ln_w, ln_b);
 }
 
@@ -1193,8 +1224,7 @@ void quant_upsample(const float* latent, int B, const float* emb_std, const floa
 // =============================================================================================
 __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
   const int b = blockIdx.y;
-  SlotState& ss = a.st[b];
-  if (!ss.valid) return;
+  if (!a.flags[b].valid) return;
   if ((int)blockIdx.x < a.nh) {
     const HistDesc& hd = a.h[blockIdx.x];
     const long n = (long)hd.P * hd.C;
@@ -1203,13 +1233,39 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
     for (long e = threadIdx.x; e < n; e += 256) dst[e] = src[e];
     return;
   }
-  if (threadIdx.x < 32) a.latent_next[b * 32 + threadIdx.x] = a.latent[b * 32 + threadIdx.x];
-  if (threadIdx.x == 0) {
-    ss.step += 1;
-    a.fpos[b] += 1;
-    a.mpos[b] += 16;
-    if (ss.last) ss.active = 0;
+  if (threadIdx.x == 0) a.mpos[b] += 16;
+}
+
+// one 64-thread block per row
+__global__ __launch_bounds__(64) void k_front_commit(FrontCommitArgs a) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  SlotState& ss = a.st[b];
+  const int valid = ss.active;
+  __syncthreads();  // every lane has read `active` before lane 0 updates the state
+  if (t == 0) {
+    FrameFlags f{0, 0};
+    const float e = a.eos[b];
+    if (valid) {  // tts_model.rs:1055-1063 + map_while over 0..max_gen_len
+      if (e > ss.eos_threshold && ss.eos_step < 0) ss.eos_step = ss.step;
+      const bool tail = ss.eos_step >= 0 && ss.step >= ss.eos_step + ss.frames_after_eos;
+      f.valid = 1;
+      f.last = (tail || ss.step + 1 >= ss.max_frames) ? 1 : 0;
+      ss.step += 1;
+      a.fpos[b] += 1;
+      if (f.last) ss.active = 0;
+    }
+    a.flags[b] = f;
+    a.eos_out[b] = e;
   }
+  if (t < 32) {
+    const float v = a.cur[b * 32 + t];
+    a.lat_out[b * 32 + t] = v;
+    if (valid) a.lat_in[b * 32 + t] = v;
+  }
+}
+
+void front_commit(const FrontCommitArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_front_commit, dim3(a.B), dim3(64), 0, s, a);
 }
 
 void step_commit(const CommitArgs& a, hipStream_t s) {
@@ -1229,6 +1285,8 @@ __global__ __launch_bounds__(256) void k_slot_reset(ResetArgs a) {
     a.st[slot] = a.st_src[i];
     a.fpos[slot] = a.fpos_src[i];
     a.mpos[slot] = 0;
+    a.flags0[slot] = FrameFlags{0, 0};
+    a.flags1[slot] = FrameFlags{0, 0};
   }
 }
 

@@ -32,6 +32,7 @@ class EngineConfig(C.Structure):
         ("weights_path", C.c_char_p),
         ("weight_blob", C.c_void_p),
         ("defer_weights", C.c_int),
+        ("pipeline", C.c_int),
     ]
 
 
@@ -62,6 +63,7 @@ SIGNATURES = [
     ("ptts_slot_open", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, I32P, C.c_int, C.POINTER(GenParams)]),
     ("ptts_slots_open", C.c_int, [C.c_void_p, C.c_int, I32P, C.POINTER(C.c_void_p), I32P, I32P,
                                   C.POINTER(GenParams)]),
+    ("ptts_probe_overlap", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]),
     ("ptts_slot_close", C.c_int, [C.c_void_p, C.c_int]),
     ("ptts_step", C.c_int, [C.c_void_p, C.c_int, F32P, U8P, U8P, F32P, F32P]),
     ("ptts_step_async", C.c_int, [C.c_void_p, C.c_int]),

@@ -67,16 +67,19 @@ class StepResult:
 class Engine:
     def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
                  seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
-                 defer_weights: bool = False):
+                 defer_weights: bool = False, pipeline: bool = False):
+        """pipeline=True: overlapped stepping, each step() returns the frame produced by the
+        previous call (see ptts_engine_config.pipeline)."""
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
-                           weight_blob or None, int(defer_weights))
+                           weight_blob or None, int(defer_weights), int(pipeline))
         h = C.c_void_p()
         check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
         self.handle = h
         self.max_slots = max_slots
         self.max_ctx = max_ctx
         self.lsd_decode_steps = lsd_decode_steps
+        self.pipeline = bool(pipeline)
 
     @staticmethod
     def weight_blob_bytes() -> int:

@@ -120,10 +120,15 @@ class TTSModel:
         ids, mgl, fae = self._ids(text_or_ids)
         p = self._params(max_frames or mgl, fae)
         self.engine.open(0, voice_state, ids, p)
+        first = True
         while True:
             r = self.engine.step(1)
             if not r.valid[0]:
+                if first and self.engine.pipeline:  # overlapped stepping: frames arrive one call late
+                    first = False
+                    continue
                 return
+            first = False
             yield r.pcm[0].reshape(1, 1, FRAME).copy()
             if r.last[0]:
                 return

@@ -229,3 +229,58 @@ def test_plan_and_kernel_timer(gpu_engine):
     names = gpu_engine.plan_ops(8)
     assert "flow.l0.qkv_gemm" in names and "seanet.conv0" in names and names[-1] == "commit"
     assert gpu_engine.time_kernel(8, "flow.l0.ff1_gemm", reps=5) > 0
+
+
+def test_pipelined_stepping_matches_oracle(oracle):
+    """pipeline=1: the Mimi decode of frame k overlaps the FlowLM step of frame k+1, and a call
+    returns the previous call's frame. Rows admitted at different times (continuous batching)
+    and a row re-admitted after it finished must still equal their oracle runs frame for frame."""
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    rng = np.random.default_rng(5)
+    eng = pt.Engine(device=0, max_slots=4, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True)
+    try:
+        voices, orc, lat, got = {}, {}, {}, {}
+
+        def admit(slots, n_frames):
+            ids_l, vs = [], []
+            for b in slots:
+                F = 5 + 3 * b
+                prompt = (d["prompt"][:F] * (1.0 + 0.07 * b)).astype(np.float32)
+                ids = rng.integers(0, 4000, size=3 + 4 * b).astype(np.int32)
+                voices[b] = eng.voice_from_prompt(prompt)
+                vs.append(voices[b])
+                ids_l.append(ids)
+                s = oracle.new_state(256)
+                s.prefill(prompt)
+                s.prefill_tokens(ids)
+                orc[b], lat[b], got[b] = s, None, 0
+            eng.open_many(slots, vs, ids_l, [params(max_frames=n_frames)] * len(slots))
+
+        def check_frames(r):
+            for b in list(orc):
+                if not r.valid[b]:
+                    continue
+                o = orc[b].step(lat[b])
+                lat[b] = o["latent"]
+                got[b] += 1
+                assert abs(r.eos_logits[b] - o["eos_logit"]) <= 1e-4
+                np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
+                assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+
+        admit([0, 1], 4)
+        r = eng.step(4)
+        assert not r.valid.any()  # first call: nothing decoded yet
+        check_frames(eng.step(4))
+        admit([2, 3], 3)  # joins while rows 0/1 have a frame in flight
+        for _ in range(3):
+            check_frames(eng.step(4))
+        assert got[0] == 4 and got[1] == 4
+        admit([0], 2)  # re-admission of a finished row
+        for _ in range(4):
+            check_frames(eng.step(4))
+        assert got[0] == 2 and got[2] == 3 and got[3] == 3
+        assert not eng.step(4).valid.any()
+    finally:
+        eng.close()

@@ -70,7 +70,11 @@ struct Case {
   std::vector<std::pair<int, int>> variants;  // (layout, S)
 };
 
-int main() {
+int main(int argc, char** argv) {
+  // optional filter: gemm_bench <case substring> <layout> [S]  (PMC runs)
+  const char* only_case = argc > 1 ? argv[1] : nullptr;
+  const int only_layout = argc > 2 ? atoi(argv[2]) : -1;
+  const int only_s = argc > 3 ? atoi(argv[3]) : -1;
   hipStream_t st;
   CK(hipStreamCreate(&st));
   const int B = 32;
@@ -111,8 +115,8 @@ int main() {
     a.T_out = T_in * tstride; a.out_tstride = tstride;
     cases.push_back({nm, a, phases, v});
   };
-  std::vector<std::pair<int, int>> skinny = {{0, 8}, {7, 8}, {13, 4}, {13, 8}, {13, 16}, {16, 4}, {16, 8}};
-  std::vector<std::pair<int, int>> fat = {{0, 1}, {6, 1}, {11, 1}, {12, 1}, {12, 2}, {12, 4}, {15, 1}, {15, 2},
+  std::vector<std::pair<int, int>> skinny = {{0, 8}, {9, 8}, {10, 8}, {17, 8}, {0, 4}, {9, 4}, {10, 4}, {13, 8}};
+  std::vector<std::pair<int, int>> fat = {{0, 1}, {9, 1}, {10, 1}, {17, 1}, {6, 1}, {12, 1}, {12, 2}, {15, 1},
                                           {13, 1}, {14, 1}};
   dense("flow.qkv M32 N3072 K1024", B, 3072, 1024, skinny);
   dense("flow.out M32 N1024 K1024", B, 1024, 1024, skinny);
@@ -137,6 +141,7 @@ int main() {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   for (auto& c : cases) {
+    if (only_case && c.name.find(only_case) == std::string::npos) continue;
     GemmArgs a = c.a;
     const long out_n = (long)c.phases * a.M * a.N;
     for (int ph = 0; ph < c.phases; ++ph)
@@ -148,6 +153,7 @@ int main() {
     const double wbytes = 4.0 * c.phases * a.N * a.K;
     printf("== %s  (%.1f MFLOP, W %.2f MB)\n", c.name.c_str(), flops / 1e6, wbytes / 1e6);
     for (auto [layout, S] : c.variants) {
+      if (only_layout >= 0 && (layout != only_layout || (only_s >= 0 && S != only_s))) continue;
       GemmArgs v = a;
       v.layout = layout;
       const int bk = (layout == 8 || layout == 15 || layout == 16) ? 64 : 32;

@@ -27,6 +27,13 @@ timeout -k 10 600 python bench.py --ops-out "$OUT/bench_ops.json" > "$OUT/bench.
 rc=$?
 echo "bench rc=$rc"; tail -n 3 "$OUT/bench.log"
 if [ $rc -ne 0 ]; then exit $rc; fi
+if [ "${SEQ:-0}" = "1" ]; then
+  timeout -k 10 300 python bench.py --no-pipeline --no-cpu-baseline --no-latency --no-op-times \
+      > "$OUT/bench_seq.log" 2>&1
+  rc=$?
+  echo "bench sequential rc=$rc"; tail -n 1 "$OUT/bench_seq.log" | cut -c1-400
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
 
 if [ "${PROFILE:-1}" = "1" ]; then
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
