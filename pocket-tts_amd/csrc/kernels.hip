@@ -88,21 +88,27 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
   const int m = m0 + r;
   const bool mvalid = m < a.M;
   const float* xrow = nullptr;
-  int bq = 0, qq = 0;
+  const float *xb = nullptr, *hb = nullptr;  // conv: this row's batch base in X and in H (t = 0)
+  int qs = 0;                                // conv: q * stride - P
   if (MODE == 0) {
     xrow = a.X + (long)(mvalid ? m : 0) * a.ldx + 16 * h;
-  } else if (mvalid) {
-    bq = m / a.Tq;
-    qq = m - bq * a.Tq;
+  } else {
+    const int mm = mvalid ? m : 0;
+    const int bq = mm / a.Tq;
+    qs = (mm - bq * a.Tq) * a.stride_in - a.P;
+    xb = a.X + (long)bq * a.T_in * a.ldx + 16 * h;
+    hb = a.H + ((long)bq * a.P + a.P) * a.cin + 16 * h;
   }
 
+  // select, not branch: both candidate addresses are formed and one is picked per lane
   auto a_ptr = [&](int k0) -> const float* {
     if (MODE == 0) return xrow + k0;
-    const int j = k0 / a.cin;
-    const int ci = k0 - j * a.cin + 16 * h;
-    const int t = qq * a.stride_in + j - a.P;
-    if (t >= 0) return a.X + ((long)bq * a.T_in + t) * a.ldx + ci;
-    return a.H + ((long)bq * a.P + (a.P + t)) * a.cin + ci;
+    const int j = k0 / a.cin;  // wave-uniform (scalar)
+    const int ci = k0 - j * a.cin;
+    const int t = qs + j;
+    const float* px = xb + t * a.ldx + ci;
+    const float* ph = hb + t * a.cin + ci;
+    return t >= 0 ? px : ph;
   };
 
   floatx16 acc;
@@ -143,19 +149,21 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
   // The prefetch is unconditional (past the end it re-reads a valid chunk, never used), so no
   // control-flow join sits between a load and the MFMAs that must not wait for it.
   if (Lay<LAYOUT>::PF == 1) {
-    if (c < ce) {
+    // n chunks for this wave; loop body = two chunks with fixed register roles and no exits,
+    // odd tail peeled (keeps the accumulator in place and the loads one chunk ahead)
+    const int n = c < ce ? (ce - c + CSTEP - 1) / CSTEP : 0;
+    const int clast = c + (n - 1) * CSTEP;
+    auto chunk = [&](int i) { return i < n ? c + i * CSTEP : clast; };
+    if (n > 0) {
       load(c, a0, b0);
-      for (;;) {
-        const int c1 = c + CSTEP;
-        load(c1 < ce ? c1 : c, a1, b1);
+      int i = 0;
+      for (; i + 2 <= n; i += 2) {
+        load(chunk(i + 1), a1, b1);
         mma(a0, b0);
-        if (c1 >= ce) break;
-        const int c2 = c1 + CSTEP;
-        load(c2 < ce ? c2 : c1, a0, b0);
+        load(chunk(i + 2), a0, b0);
         mma(a1, b1);
-        if (c2 >= ce) break;
-        c = c2;
       }
+      if (i < n) mma(a0, b0);
     }
   } else {
     float4 a2[4], b2[4];
