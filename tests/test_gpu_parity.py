@@ -284,3 +284,28 @@ def test_pipelined_stepping_matches_oracle(oracle):
         assert not eng.step(4).valid.any()
     finally:
         eng.close()
+
+
+def test_long_utterance_wraps_mimi_ring(gpu_engine, oracle):
+    """70 frames: the Mimi decoder ring (512 positions = 32 frames) wraps twice and the 250-key
+    window slides across the wrap; the FlowLM cache grows to voice + text + 70 positions. Every
+    frame must match the oracle (temp 0; the backbone input is teacher-forced to the oracle's
+    latent so that per-step differences do not compound through the autoregression)."""
+    d = load_golden("e2e_lsd1.safetensors")
+    v = gpu_engine.voice_from_prompt(d["prompt"])
+    n = 70
+    gpu_engine.open(0, v, d["text_ids"], params(max_frames=n))
+    s = oracle.new_state(256)
+    s.prefill(d["prompt"])
+    s.prefill_tokens(d["text_ids"])
+    lat = None
+    worst = 0.0
+    for i in range(n):
+        r = gpu_engine.step(1)
+        o = s.step(lat)
+        lat = o["latent"]
+        assert r.valid[0] and r.last[0] == (i == n - 1)
+        np.testing.assert_allclose(r.latents[0], o["latent"], atol=1e-4)
+        worst = max(worst, rms(r.pcm[0] - o["pcm"]))
+        gpu_engine.set_latent(0, o["latent"])  # teacher forcing: no drift over 70 AR steps
+    assert worst <= 1e-4, worst
