@@ -20,7 +20,7 @@ int pick_splits(int M, int N, int K) {
   const int chunks = K / 32;
   int s = std::max(1, 768 / std::max(1, tiles));
   s = std::min(s, std::max(1, chunks / 4));
-  return s;
+  return std::min(s, 16);  // k_row_reduce sums at most 16 slabs
 }
 }  // namespace
 
@@ -299,12 +299,16 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
     KvStore kv{kv_ + (long)l * kv_layer_, kv_slot_, max_ctx_};
     int S = 1;
     linear_split(ops, p + ".qkv_gemm", h_, D, M, W(t.in_proj), 3 * D, D, &S);
-    {
+    if (qg == 1) {  // step: slab sum + RoPE + KV append fused into the attention kernel
       const float* P = partial_;
-      float* Q = q_;
-      ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(P, S, nullptr, M, NH, map, kv, Q, s); }});
-    }
-    {
+      float* O = o_;
+      ops.push_back({p + ".attention", [=](hipStream_t s) { attention_step_qkv(P, S, M, NH, map, kv, O, s); }});
+    } else {
+      {
+        const float* P = partial_;
+        float* Q = q_;
+        ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(P, S, nullptr, M, NH, map, kv, Q, s); }});
+      }
       const float* Q = q_;
       float* O = o_;
       ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, M, NH, map, kv, 0, qg, O, s); }});

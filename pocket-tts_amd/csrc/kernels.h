@@ -104,6 +104,9 @@ void qkv_rope_append(const float* P, int S, const float* dense, int M, int nh, R
 // in groups of qg (<= 16) consecutive rows of one slot. O[M][nh*64].
 void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O,
                hipStream_t s);
+// One-query-per-row step attention fused with the QKV slab sum, RoPE and KV append (positions
+// must not wrap: FlowLM cache).
+void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStore kv, float* O, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // Per-slot generation bookkeeping (device resident so the step can be replayed as a graph).

@@ -643,28 +643,33 @@ __device__ __forceinline__ float act1(float x, int act) {
   return act == ACT_GELU ? gelu_tanh(x) : (act == ACT_SILU ? silu(x) : x);
 }
 
+// Every load of a thread (its S slab float4s and the bias / gate / residual / modulation
+// operands) is issued before the first add: one memory round trip per kernel. Absent operands
+// are read from a valid stand-in address and dropped by a select (no branches around loads).
+template <int SMAX>
 __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   __shared__ float sh[4];
   const int m = blockIdx.x;
-  const int n = blockIdx.y * 1024 + 4 * threadIdx.x;
-  const bool ok = n < a.N;
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int n0 = blockIdx.y * 1024 + 4 * threadIdx.x;
+  const bool ok = n0 < a.N;
+  const int n = ok ? n0 : 0;
+  const float* p = a.P + (long)m * a.N + n;
+  const long zs = (long)a.M * a.N;
+  float4 pz[SMAX];
+#pragma unroll
+  for (int z = 0; z < SMAX; ++z) pz[z] = *reinterpret_cast<const float4*>(p + (long)min(z, a.S - 1) * zs);
+  const float4 bi = *reinterpret_cast<const float4*>((a.bias ? a.bias + n : p));
+  const float4 ga = *reinterpret_cast<const float4*>((a.gate ? a.gate + (long)m * a.ldg + n : p));
+  const float4 rr = *reinterpret_cast<const float4*>((a.R ? a.R + (long)m * a.ldr + n : p));
+  float4 v = pz[0];
+#pragma unroll
+  for (int z = 1; z < SMAX; ++z)
+    if (z < a.S) v = f4add(v, pz[z]);
+  if (a.bias) v = f4add(v, bi);
+  if (a.act != ACT_NONE) v = make_float4(act1(v.x, a.act), act1(v.y, a.act), act1(v.z, a.act), act1(v.w, a.act));
+  if (a.gate) v = f4mul(v, ga);
+  if (a.R) v = f4add(v, rr);
   if (ok) {
-    const float* p = a.P + (long)m * a.N + n;
-    const long zs = (long)a.M * a.N;
-    int z = 0;
-    for (; z + 4 <= a.S; z += 4) {
-      const float4 p0 = *reinterpret_cast<const float4*>(p + (z + 0) * zs);
-      const float4 p1 = *reinterpret_cast<const float4*>(p + (z + 1) * zs);
-      const float4 p2 = *reinterpret_cast<const float4*>(p + (z + 2) * zs);
-      const float4 p3 = *reinterpret_cast<const float4*>(p + (z + 3) * zs);
-      v = f4add(f4add(f4add(f4add(v, p0), p1), p2), p3);
-    }
-    for (; z < a.S; ++z) v = f4add(v, *reinterpret_cast<const float4*>(p + z * zs));
-    if (a.bias) v = f4add(v, *reinterpret_cast<const float4*>(a.bias + n));
-    if (a.act != ACT_NONE) v = make_float4(act1(v.x, a.act), act1(v.y, a.act), act1(v.z, a.act), act1(v.w, a.act));
-    if (a.gate) v = f4mul(v, *reinterpret_cast<const float4*>(a.gate + (long)m * a.ldg + n));
-    if (a.R) v = f4add(v, *reinterpret_cast<const float4*>(a.R + (long)m * a.ldr + n));
     if (a.Y) *reinterpret_cast<float4*>(a.Y + (long)m * a.ldy + n) = v;
     if (a.euler) {
       float4* e = reinterpret_cast<float4*>(a.euler + (long)m * 32 + n);
@@ -674,6 +679,10 @@ __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
     }
   }
   if (!a.ln) return;  // LN rows are <= 1024 wide: gridDim.y == 1 (host-checked)
+  const float4 lw = *reinterpret_cast<const float4*>(a.ln_w ? a.ln_w + n : p);
+  const float4 lb = *reinterpret_cast<const float4*>(a.ln_w ? a.ln_b + n : p);
+  const float4 msc = *reinterpret_cast<const float4*>(a.mshift ? a.mscale + (long)m * a.ldm + n : p);
+  const float4 msf = *reinterpret_cast<const float4*>(a.mshift ? a.mshift + (long)m * a.ldm + n : p);
   const float s = ok ? (v.x + v.y) + (v.z + v.w) : 0.f;
   const float mean = block_sum(s, sh) / (float)a.N;
   const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
@@ -681,20 +690,20 @@ __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   const float den = sqrtf(block_sum(q, sh) / (float)a.N + a.eps);
   if (!ok) return;
   float4 hh = make_float4(d.x / den, d.y / den, d.z / den, d.w / den);
-  if (a.ln_w)
-    hh = f4add(f4mul(hh, *reinterpret_cast<const float4*>(a.ln_w + n)), *reinterpret_cast<const float4*>(a.ln_b + n));
-  if (a.mshift) {
-    const float4 sc = *reinterpret_cast<const float4*>(a.mscale + (long)m * a.ldm + n);
-    const float4 sf = *reinterpret_cast<const float4*>(a.mshift + (long)m * a.ldm + n);
-    hh = make_float4(hh.x * (1.0f + sc.x) + sf.x, hh.y * (1.0f + sc.y) + sf.y, hh.z * (1.0f + sc.z) + sf.z,
-                     hh.w * (1.0f + sc.w) + sf.w);
-  }
+  if (a.ln_w) hh = f4add(f4mul(hh, lw), lb);
+  if (a.mshift)
+    hh = make_float4(hh.x * (1.0f + msc.x) + msf.x, hh.y * (1.0f + msc.y) + msf.y, hh.z * (1.0f + msc.z) + msf.z,
+                     hh.w * (1.0f + msc.w) + msf.w);
   *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = hh;
 }
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s) {
   dim3 grid(a.M, (a.N + 1023) / 1024);
-  hipLaunchKernelGGL(k_row_reduce, grid, dim3(256), 0, s, a);
+  if (a.S <= 1) hipLaunchKernelGGL(k_row_reduce<1>, grid, dim3(256), 0, s, a);
+  else if (a.S <= 2) hipLaunchKernelGGL(k_row_reduce<2>, grid, dim3(256), 0, s, a);
+  else if (a.S <= 4) hipLaunchKernelGGL(k_row_reduce<4>, grid, dim3(256), 0, s, a);
+  else if (a.S <= 8) hipLaunchKernelGGL(k_row_reduce<8>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_row_reduce<16>, grid, dim3(256), 0, s, a);
 }
 
 // LayerNorm, one wave per row (N <= 1024, multiple of 64).
@@ -1098,6 +1107,110 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
     }
     O[(long)(row0 + qi) * d + head * 64 + dd] = num / den;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// FlowLM step attention with the QKV split-K sum, RoPE and KV append fused in front (replaces
+// qkv_rope_append + k_attn_decode for the one-query-per-row step): the workgroup of (row, head)
+// sums its 192 q|k|v columns over the S slabs, rotates q and k (rope.rs:18-60), appends k, v at
+// the row's position and attends over the cached keys 0..pos-1 plus the new key from LDS.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict__ P, int S, int M, int nh, RowMap mp,
+                                                         KvStore kv, float* __restrict__ O) {
+  __shared__ float s_m[4], s_l[4], s_o[4][64];
+  __shared__ float s_qkv[3][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row = blockIdx.x, head = blockIdx.y;
+  int slot, qp;
+  row_slot_pos(mp, row, slot, qp);
+  const int d = nh * 64, ld = 3 * d;
+  if (tid < 192) {  // q | k | v column of this head, summed over the slabs in z order
+    const int part = tid >> 6;
+    const float* pr = P + (long)row * ld + part * d + head * 64 + lane;
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += pr[(long)z * M * ld];
+    s_qkv[part][lane] = v;
+  }
+  __syncthreads();
+  float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
+  float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
+  if (tid < 64) {  // rotate the (2i, 2i+1) pairs of q (tid < 32) and k (tid >= 32)
+    const int i = tid & 31, part = tid >> 5;
+    const float freq = expf((float)i * (-logf(10000.0f) * 2.0f / 64.0f));
+    const float ang = (float)qp * freq;
+    const float cs = cosf(ang), sn = sinf(ang);
+    const float x0 = s_qkv[part][2 * i], x1 = s_qkv[part][2 * i + 1];
+    const float y0 = x0 * cs - x1 * sn, y1 = x0 * sn + x1 * cs;  // one wave: all reads precede the writes
+    s_qkv[part][2 * i] = y0;
+    s_qkv[part][2 * i + 1] = y1;
+    if (part == 1) {
+      kbase[(long)qp * 64 + 2 * i] = y0;
+      kbase[(long)qp * 64 + 2 * i + 1] = y1;
+    }
+  } else if (tid < 128) {
+    vbase[(long)qp * 64 + lane] = s_qkv[2][lane];
+  }
+  __syncthreads();
+  float4 q[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) q[i] = reinterpret_cast<const float4*>(s_qkv[0])[i];
+  float m = -INFINITY, l = 0.f, o = 0.f;
+  for (int base = 64 * wave; base < qp; base += 256) {  // cached keys 0 .. qp-1
+    const int j = base + lane;
+    const int last = qp - 1;
+    const bool valid = j <= last;
+    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)(valid ? j : last) * 64);
+    float4 k[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) k[i] = kr[i];
+    float v[64];
+#pragma unroll
+    for (int jj = 0; jj < 64; ++jj) v[jj] = vbase[(long)min(base + jj, last) * 64 + lane];
+    float sc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sc += q[i].x * k[i].x + q[i].y * k[i].y + q[i].z * k[i].z + q[i].w * k[i].w;
+    sc = valid ? sc * 0.125f : -INFINITY;  // 1/sqrt(64) (attention.rs:191,229)
+    const float mn = fmaxf(m, wave_max(sc));
+    const float alpha = expf(m - mn);
+    const float p = valid ? expf(sc - mn) : 0.f;
+    l = l * alpha + wave_sum(p);
+    o *= alpha;
+    const int pb = __builtin_bit_cast(int, p);
+#pragma unroll
+    for (int jj = 0; jj < 64; ++jj) o += __builtin_bit_cast(float, __builtin_amdgcn_readlane(pb, jj)) * v[jj];
+    m = mn;
+  }
+  if (wave == 0) {  // the new key (position qp) from LDS
+    const float sc = wave_sum(s_qkv[0][lane] * s_qkv[1][lane]) * 0.125f;
+    const float mn = fmaxf(m, sc);
+    const float alpha = expf(m - mn);
+    const float p = expf(sc - mn);
+    l = l * alpha + p;
+    o = o * alpha + p * s_qkv[2][lane];
+    m = mn;
+  }
+  if (lane == 0) {
+    s_m[wave] = m;
+    s_l[wave] = l;
+  }
+  s_o[wave][lane] = o;
+  __syncthreads();
+  if (wave == 0) {
+    const float Mx = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float e = s_m[w] == -INFINITY ? 0.f : expf(s_m[w] - Mx);
+      num += s_o[w][lane] * e;
+      den += s_l[w] * e;
+    }
+    O[(long)row * d + head * 64 + lane] = num / den;
+  }
+}
+
+void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStore kv, float* O, hipStream_t s) {
+  hipLaunchKernelGGL(k_attn_decode_qkv, dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, O);
 }
 
 void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O, hipStream_t s) {
