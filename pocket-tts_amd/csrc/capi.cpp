@@ -121,10 +121,11 @@ int ptts_slots_open(ptts_engine* e, int n, const int* slots, const ptts_voice* c
   return guard([&] { eng(e).slots_open(n, slots, voices, ids, n_ids, params); });
 }
 
-int ptts_probe_overlap(ptts_engine* e, int n_rows, int reps, double* us4) {
+int ptts_probe_overlap(ptts_engine* e, int n_rows, int reps, double* us8) {
   return guard([&] {
-    if (!us4) throw ptts::Error(PTTS_ERR_INVALID, "null output");
-    eng(e).overlap_probe(n_rows, reps, us4);
+    if (!us8) throw ptts::Error(PTTS_ERR_INVALID, "null output");
+    for (int i = 0; i < 8; ++i) us8[i] = 0.0;
+    eng(e).overlap_probe(n_rows, reps, us8);
   });
 }
 

@@ -9,6 +9,7 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -101,6 +102,11 @@ Engine::Engine(const ptts_engine_config& cfg) {
   admit_slots_ = (int*)dalloc(B);
   admit_st_ = (SlotState*)dalloc((sizeof(SlotState) * B + 3) / 4);
   admit_fpos_ = (int*)dalloc(B);
+  tickets_ = (int*)dalloc(TICKETS);
+  row_tickets_ = (int*)dalloc(ROW_TICKETS);
+  // measured slower than a separate row_reduce launch on every front GEMM (ff2 43 vs 13 us with
+  // the LayerNorm row finisher, ff1 15.6 vs 11.4 us tile-local): opt-in only
+  fuse_splitk_ = getenv("PTTS_FUSED_SPLITK") != nullptr;
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
   mods_ = dalloc((size_t)lsd_ * B * NADA);
   xf_ = dalloc((size_t)B * FD);
@@ -226,7 +232,34 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   a.partial = partial_;
   ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
                  4.0 * ((double)N * K + (double)M * K + (double)S * M * N)});
+  last_split_ = a;
+  last_split_op_ = ops.size() - 1;
   *S_out = S;
+}
+
+// The row-reduce epilogue of the split GEMM just emitted: run inside that GEMM's launch (in-launch
+// split-K combine, layouts 0 and 13) when possible, else as its own row_reduce launch.
+void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r) {
+  GemmArgs g = last_split_;
+  const bool prev_is_gemm = !ops.empty() && last_split_op_ == ops.size() - 1;
+  const bool tiles_ok = g.layout == 0 || g.layout == 13;
+  const bool ln_ok = !r.ln || (r.N % 256 == 0 && r.N <= 1024);
+  const bool same = prev_is_gemm && r.P == g.partial && r.S == g.S && r.M == g.M && r.N == g.N;
+  if (fuse_splitk_ && same && tiles_ok && ln_ok) {
+    const int gx = g.layout == 13 ? (g.N + 127) / 128 : (g.N + 31) / 32;
+    const int gy = (g.M + 31) / 32;
+    PTTS_REQUIRE(gx * gy <= TICKETS && gy <= ROW_TICKETS, "split-K ticket arrays too small");
+    g.fuse = r.ln ? 2 : 1;
+    g.tickets = tickets_;
+    g.row_tickets = row_tickets_;
+    g.rr = r;
+    const int S = g.S;
+    Op& op = ops.back();
+    op.fn = [g, S](hipStream_t s) { gemm(g, S, s); };
+    last_split_op_ = (size_t)-1;
+    return;
+  }
+  ops.push_back({name, [r](hipStream_t s) { row_reduce(r, s); }});
 }
 
 void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,
@@ -333,7 +366,7 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       a.eps = 1e-5f;
       a.Hout = Hout;
       a.ldh = N;
-      ops.push_back({name, [a](hipStream_t s) { row_reduce(a, s); }});
+      push_rr(ops, name, a);
     };
     linear_split(ops, p + ".out_gemm", o_, D, M, W(t.out_proj), D, D, &S);
     rr(p + ".out_reduce_ln2", S, D, ACT_NONE, true, x_, W(t.n2w), W(t.n2b), true, h_);
@@ -379,7 +412,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
     a.eps = 1e-5f;
     a.Hout = h_;
     a.ldh = D;
-    ops.push_back({"flow.input_reduce_ln1", [a](hipStream_t s) { row_reduce(a, s); }});
+    push_rr(ops, "flow.input_reduce_ln1", a);
   }
   flow_layers(ops, B, RowMap{0, 1, 0, fpos_}, 1, true, "flow");
   // ---- flow head (mlp.rs:215-383): cond_embed | out_eos, EOS bookkeeping, noise
@@ -404,7 +437,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
     a.bias = W(L_.ada_b);
     a.Y = mods_;
     a.ldy = NADA;
-    ops.push_back({"head.ada_reduce", [a](hipStream_t s) { row_reduce(a, s); }});
+    push_rr(ops, "head.ada_reduce", a);
   }
   // lsd_decode Euler steps (flow_lm.rs:7-22) over ResBlocks (mlp.rs:146-213)
   for (int st = 0; st < lsd_; ++st) {
@@ -429,7 +462,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
       a.ldm = NADA;
       a.Hout = hf_;
       a.ldh = FD;
-      ops.push_back({p + ".inproj_reduce", [a](hipStream_t s) { row_reduce(a, s); }});
+      push_rr(ops, p + ".inproj_reduce", a);
     }
     for (int i = 0; i < FDEPTH; ++i) {
       const std::string pb = p + ".rb" + std::to_string(i);
@@ -444,7 +477,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
         a.act = ACT_SILU;
         a.Y = uf_;
         a.ldy = FD;
-        ops.push_back({pb + ".mlp0_reduce", [a](hipStream_t s) { row_reduce(a, s); }});
+        push_rr(ops, pb + ".mlp0_reduce", a);
       }
       linear_split(ops, pb + ".mlp2_gemm", uf_, FD, B, W(L_.rb_w2[i]), FD, FD, &S);
       {
@@ -474,7 +507,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
         a.ldm = NADA;
         a.Hout = hf_;
         a.ldh = FD;
-        ops.push_back({pb + ".mlp2_reduce", [a](hipStream_t s) { row_reduce(a, s); }});
+        push_rr(ops, pb + ".mlp2_reduce", a);
       }
     }
     linear_split(ops, p + ".final_gemm", hf_, FD, B, W(L_.fin_w), LDIM, FD, &S);
@@ -487,7 +520,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
       a.bias = W(L_.fin_b);
       a.euler = cur_;
       a.euler_scale = 1.0f / (float)lsd_;
-      ops.push_back({p + ".euler", [a](hipStream_t s) { row_reduce(a, s); }});
+      push_rr(ops, p + ".euler", a);
     }
   }
   // ---- EOS rule, frame flags, hand-off of the frame to the back part, next backbone input
@@ -583,8 +616,8 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
     // per-stage tile choice (tools/gemm_bench.hip at B=32): the short-K, many-row late stages
     // run the LDS-DMA kernels; the first stage keeps the K-split register kernel
     const bool big = B >= 16;
-    const int l_tr = big ? (i == 1 ? 13 : (i == 2 ? 6 : 0)) : 0;
-    const int l_r3 = big && i == 2 ? 14 : 0;
+    const int l_tr = big ? (i == 1 ? 20 : (i == 2 ? 6 : 0)) : 0;
+    const int l_r3 = big && i == 0 ? 18 : 0;
     const int l_r1 = big && i == 2 ? 6 : 0;
     conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 1, W(L_.dtr_w[i]), ch / 2, 2, r,
             W(L_.dtr_b[i]), nullptr, cb_[i], T * r, r, l_tr);
@@ -805,6 +838,29 @@ void Engine::overlap_probe(int B, int reps, double* us) {
   us[1] = timed(1);
   us[2] = timed(2);
   us[3] = timed(3);
+  // CU partitions: front on the first F CUs of every XCD-interleaved group, back on the rest
+  int ncu = 0;
+  PTTS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_));
+  const int fronts[3] = {32, 64, 128};
+  for (int v = 0; v < 3; ++v) {
+    std::vector<uint32_t> mf((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
+    for (int cu = 0; cu < ncu; ++cu) {
+      // spread the front's CUs evenly over the chip (every ncu/F-th CU)
+      const bool front = (cu % (ncu / fronts[v])) == 0;
+      (front ? mf : mb)[cu / 32] |= 1u << (cu % 32);
+    }
+    hipStream_t sf = nullptr, sbk = nullptr;
+    PTTS_HIP(hipExtStreamCreateWithCUMask(&sf, (uint32_t)mf.size(), mf.data()));
+    PTTS_HIP(hipExtStreamCreateWithCUMask(&sbk, (uint32_t)mb.size(), mb.data()));
+    hipStream_t keep_hi = s_hi, keep_lo = s_lo;
+    s_hi = sf;
+    s_lo = sbk;
+    us[4 + v] = timed(3);
+    s_hi = keep_hi;
+    s_lo = keep_lo;
+    (void)hipStreamDestroy(sf);
+    (void)hipStreamDestroy(sbk);
+  }
   for (int part = 0; part < 2; ++part) {
     (void)hipGraphExecDestroy(ge[part]);
     (void)hipGraphDestroy(g[part]);

@@ -64,6 +64,7 @@ class Engine {
   void build_front(std::vector<Op>& ops, int B, int par);
   void build_back(std::vector<Op>& ops, int B, int par);
   hipGraphExec_t part_graph(int part, int B, int par);
+  void push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r);
   void flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag);
   void linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M, const float* Wt,
                     int N, int K, int* S_out);
@@ -115,6 +116,13 @@ class Engine {
   FrameFlags* flags_[2] = {};
   float* pcm_[2] = {};
   float* mpartial_ = nullptr;
+  // in-launch split-K combine (front part only; the back part never uses it)
+  static constexpr int TICKETS = 4096, ROW_TICKETS = 256;
+  int* tickets_ = nullptr;
+  int* row_tickets_ = nullptr;
+  bool fuse_splitk_ = false;
+  GemmArgs last_split_{};
+  size_t last_split_op_ = (size_t)-1;
   // pipelined stepping (cfg.pipeline): back part on its own stream, parity events
   bool pipeline_ = false;
   hipStream_t stream_be_ = nullptr;

@@ -17,34 +17,6 @@ namespace ptts {
 // or the transposed-conv phase index (mode 1).
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2 };
 
-struct GemmArgs {
-  int mode;    // 0 dense, 1 conv
-  int layout;  // workgroup layout, see kernels.hip (0 ksplit 32x32, 1: 64x64, 2: 32x128, 3: 128x32)
-  int M, N, K;
-  int Nw;  // rows present in W (N rounded up to 32)
-  // A operand
-  const float* X;
-  long ldx;
-  const float* H;  // conv history [B][P][cin]
-  int P, T_in, Tq, stride_in, cin, elu_in;
-  // B operand
-  const float* W;
-  long w_phase_stride;  // floats between polyphase weight blocks (mode 1)
-  // split-K
-  int S;
-  float* partial;  // [S][M][N] when S > 1
-  // epilogue (S == 1)
-  const float* bias;
-  int act;
-  const float* R;  // residual (same row mapping as Y), may alias Y
-  long ldr;
-  const float* rscale;  // per-column scale of the update (LayerScale) or nullptr
-  float* Y;
-  long ldy;
-  int T_out, out_tstride;  // mode 1 output row = b*T_out + q*out_tstride + phase
-};
-void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
-
 // ---------------------------------------------------------------------------------------------
 // Row reduce / epilogue of a split-K GEMM, fused with residual, gate, LayerNorm and modulate:
 //   v = sum_z P[z][m][n] (+bias[n]) ; v = act(v) ; v *= gate[m][n] ; v += R[m][n] ;
@@ -74,6 +46,42 @@ struct RowReduceArgs {
   float* Hout;
   long ldh;
 };
+struct GemmArgs {
+  int mode;    // 0 dense, 1 conv
+  int layout;  // workgroup layout, see kernels.hip (0 ksplit 32x32, 1: 64x64, 2: 32x128, 3: 128x32)
+  int M, N, K;
+  int Nw;  // rows present in W (N rounded up to 32)
+  // A operand
+  const float* X;
+  long ldx;
+  const float* H;  // conv history [B][P][cin]
+  int P, T_in, Tq, stride_in, cin, elu_in;
+  // B operand
+  const float* W;
+  long w_phase_stride;  // floats between polyphase weight blocks (mode 1)
+  // split-K
+  int S;
+  float* partial;  // [S][M][N] when S > 1
+  // epilogue (S == 1)
+  const float* bias;
+  int act;
+  const float* R;  // residual (same row mapping as Y), may alias Y
+  long ldr;
+  const float* rscale;  // per-column scale of the update (LayerScale) or nullptr
+  float* Y;
+  long ldy;
+  int T_out, out_tstride;  // mode 1 output row = b*T_out + q*out_tstride + phase
+  // In-launch split-K combine (layouts 0 and 13, mode 0): every workgroup stores its slab into
+  // `partial`, then draws a ticket on its output tile; the last arriver sums the S slabs and runs
+  // the row-reduce epilogue `rr` on the tile (fuse 1). With fuse 2 the tile finishers also draw a
+  // ticket on their 32-row block and the last one applies rr's LayerNorm / modulate to the rows.
+  int fuse;
+  int* tickets;      // one counter per output tile, zero between launches
+  int* row_tickets;  // one counter per 32-row block
+  RowReduceArgs rr;  // rr.P == partial, rr.S == S
+};
+void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
+
 void row_reduce(const RowReduceArgs& a, hipStream_t s);
 
 // LayerNorm over rows of width N (<= 1024), biased variance (candle_nn::LayerNorm).

@@ -33,6 +33,8 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+__device__ void splitk_combine(const GemmArgs& g, int m0, int n0, int ncols, float* flag);
+
 // =============================================================================================
 // GEMM (see kernels.h). One 256-thread workgroup = 4 waves owns a 32x32 output tile; the
 // tile's K chunks (32 wide) are dealt round-robin to the 4 waves, each wave accumulates with
@@ -220,6 +222,7 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
       for (int w = 1; w < NW; ++w) v += red[(w * 16 + g) * 64 + lane];
       store(g, v);
     }
+    if (MODE == 0 && a.fuse) splitk_combine(a, m0, n0, 32, red);
   } else if (wave_live) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) store(g, acc[g]);
@@ -558,6 +561,162 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
     if (a.R) v += a.R[yrow * a.ldr + col];
     a.Y[yrow * a.ldy + col] = v;
   }
+  if (MODE == 0 && WM == 1 && a.fuse) splitk_combine(a, m0, n0, TN, lds);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Register-blocked K-split GEMM: each wave accumulates a (32*TM) x (32*TN) block (TM*TN
+// 32x32 accumulators); one A fragment feeds TN MFMAs and one B fragment TM, so operand bytes per
+// flop fall to (TM+TN)/(2*TM*TN) of the 32x32 tile's. The 4 waves split the K chunks of the
+// workgroup tile and are summed through LDS; loads run one chunk ahead in an exit-free loop.
+// LAYOUT 18: 32x64 per workgroup (TM 1, TN 2), 19: 64x32 (2, 1), 20: 64x64 (2, 2).
+// ---------------------------------------------------------------------------------------------
+template <int MODE, int TM, int TN>
+__global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
+  __shared__ float red[4 * 16 * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.x * 32 * TN, m0 = blockIdx.y * 32 * TM, z = blockIdx.z;
+  const int nchunks = a.K >> 5;
+  int cb = 0, ce = nchunks, phase = 0;
+  if (MODE == 0) {
+    cb = (int)((long)nchunks * z / a.S);
+    ce = (int)((long)nchunks * (z + 1) / a.S);
+  } else {
+    phase = z;
+  }
+  const float* wrow[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = min(n0 + 32 * j + r, a.Nw - 1);
+    wrow[j] = a.W + (long)phase * a.w_phase_stride + (long)n * a.K + 16 * h;
+  }
+  const float* xrow[TM];
+  const float *xb[TM], *hb[TM];
+  int qs[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mm = min(m0 + 32 * i + r, a.M - 1);  // rows past M only feed unstored outputs
+    if (MODE == 0) {
+      xrow[i] = a.X + (long)mm * a.ldx + 16 * h;
+    } else {
+      const int bq = mm / a.Tq;
+      qs[i] = (mm - bq * a.Tq) * a.stride_in - a.P;
+      xb[i] = a.X + (long)bq * a.T_in * a.ldx + 16 * h;
+      hb[i] = a.H + ((long)bq * a.P + a.P) * a.cin + 16 * h;
+    }
+  }
+  auto a_ptr = [&](int i, int k0) -> const float* {
+    if (MODE == 0) return xrow[i] + k0;
+    const int j = k0 / a.cin;
+    const int ci = k0 - j * a.cin;
+    const int t = qs[i] + j;
+    const float* px = xb[i] + t * a.ldx + ci;
+    const float* ph = hb[i] + t * a.cin + ci;
+    return t >= 0 ? px : ph;
+  };
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.f;
+  const bool elu = MODE == 1 && a.elu_in;
+  auto load = [&](int cc, float4 (&A)[TM][4], float4 (&Bv)[TN][4]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* ap = a_ptr(i, cc << 5);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) A[i][q] = *reinterpret_cast<const float4*>(ap + 4 * q);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Bv[j][q] = *reinterpret_cast<const float4*>(wrow[j] + (cc << 5) + 4 * q);
+  };
+  auto mma = [&](float4 (&A)[TM][4], float4 (&Bv)[TN][4]) {
+    float af[TM][16], bf[TN][16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        af[i][4 * q] = A[i][q].x; af[i][4 * q + 1] = A[i][q].y; af[i][4 * q + 2] = A[i][q].z; af[i][4 * q + 3] = A[i][q].w;
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bf[j][4 * q] = Bv[j][q].x; bf[j][4 * q + 1] = Bv[j][q].y; bf[j][4 * q + 2] = Bv[j][q].z; bf[j][4 * q + 3] = Bv[j][q].w;
+      }
+    }
+    if (elu) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) af[i][k] = elu1(af[i][k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][k], bf[j][k], acc[i][j], 0, 0, 0);
+  };
+  float4 a0[TM][4], b0[TN][4], a1[TM][4], b1[TN][4];
+  {
+    const int c = cb + wave;
+    const int n = c < ce ? (ce - c + 3) / 4 : 0;
+    const int clast = c + (n - 1) * 4;
+    auto chunk = [&](int i) { return i < n ? c + i * 4 : clast; };
+    if (n > 0) {
+      load(c, a0, b0);
+      int i = 0;
+      for (; i + 2 <= n; i += 2) {
+        load(chunk(i + 1), a1, b1);
+        mma(a0, b0);
+        load(chunk(i + 2), a0, b0);
+        mma(a1, b1);
+      }
+      if (i < n) mma(a0, b0);
+    }
+  }
+  // K-split sum over the 4 waves, one 32x32 accumulator at a time through LDS
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (i + j > 0) __syncthreads();
+#pragma unroll
+      for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[i][j][g];
+      __syncthreads();
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int g = wave * 4 + gg;
+        float v = red[(0 * 16 + g) * 64 + lane] + red[(1 * 16 + g) * 64 + lane];
+        v += red[(2 * 16 + g) * 64 + lane];
+        v += red[(3 * 16 + g) * 64 + lane];
+        const int row = m0 + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+        const int col = n0 + 32 * j + r;
+        if (row >= a.M || col >= a.N) continue;
+        if (a.partial) {
+          a.partial[((long)z * a.M + row) * a.N + col] = v;
+          continue;
+        }
+        if (a.bias) v += a.bias[col];
+        if (a.act == ACT_GELU) v = gelu_tanh(v);
+        else if (a.act == ACT_SILU) v = silu(v);
+        long yrow = row;
+        if (MODE == 1) {
+          const int b2 = row / a.Tq;
+          const int q2 = row - b2 * a.Tq;
+          yrow = (long)b2 * a.T_out + (long)q2 * a.out_tstride + phase;
+        }
+        if (a.rscale) v *= a.rscale[col];
+        if (a.R) v += a.R[yrow * a.ldr + col];
+        a.Y[yrow * a.ldy + col] = v;
+      }
+    }
 }
 
 template <int MODE>
@@ -603,6 +762,15 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     case 9:
       hipLaunchKernelGGL((k_gemm<MODE, 9>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(512), 0, s, a);
       break;
+    case 18:
+      hipLaunchKernelGGL((k_gemm_rb<MODE, 1, 2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+      break;
+    case 19:
+      hipLaunchKernelGGL((k_gemm_rb<MODE, 2, 1>), dim3((a.N + 31) / 32, (a.M + 63) / 64, grid_z), dim3(256), 0, s, a);
+      break;
+    case 20:
+      hipLaunchKernelGGL((k_gemm_rb<MODE, 2, 2>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), dim3(256), 0, s, a);
+      break;
     case 10:
       hipLaunchKernelGGL((k_gemm<MODE, 10>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
       break;
@@ -643,16 +811,12 @@ __device__ __forceinline__ float act1(float x, int act) {
   return act == ACT_GELU ? gelu_tanh(x) : (act == ACT_SILU ? silu(x) : x);
 }
 
-// Every load of a thread (its S slab float4s and the bias / gate / residual / modulation
-// operands) is issued before the first add: one memory round trip per kernel. Absent operands
-// are read from a valid stand-in address and dropped by a select (no branches around loads).
+// Every load of a thread (its S slab float4s and the bias / gate / residual operands) is issued
+// before the first add: one memory round trip. Absent operands are read from a valid stand-in
+// address and dropped by a select (no branches around loads). Shared by the row-reduce kernel
+// and the in-launch split-K combine of the GEMM kernels (identical summation order).
 template <int SMAX>
-__global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
-  __shared__ float sh[4];
-  const int m = blockIdx.x;
-  const int n0 = blockIdx.y * 1024 + 4 * threadIdx.x;
-  const bool ok = n0 < a.N;
-  const int n = ok ? n0 : 0;
+__device__ __forceinline__ float4 rr_value(const RowReduceArgs& a, int m, int n) {
   const float* p = a.P + (long)m * a.N + n;
   const long zs = (long)a.M * a.N;
   float4 pz[SMAX];
@@ -669,32 +833,139 @@ __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   if (a.act != ACT_NONE) v = make_float4(act1(v.x, a.act), act1(v.y, a.act), act1(v.z, a.act), act1(v.w, a.act));
   if (a.gate) v = f4mul(v, ga);
   if (a.R) v = f4add(v, rr);
-  if (ok) {
-    if (a.Y) *reinterpret_cast<float4*>(a.Y + (long)m * a.ldy + n) = v;
-    if (a.euler) {
-      float4* e = reinterpret_cast<float4*>(a.euler + (long)m * 32 + n);
-      const float sc = a.euler_scale;
-      float4 c = *e;
-      *e = make_float4(c.x + v.x * sc, c.y + v.y * sc, c.z + v.z * sc, c.w + v.w * sc);
-    }
+  return v;
+}
+__device__ __forceinline__ void rr_store(const RowReduceArgs& a, int m, int n, float4 v) {
+  if (a.Y) *reinterpret_cast<float4*>(a.Y + (long)m * a.ldy + n) = v;
+  if (a.euler) {
+    float4* e = reinterpret_cast<float4*>(a.euler + (long)m * 32 + n);
+    const float sc = a.euler_scale;
+    float4 c = *e;
+    *e = make_float4(c.x + v.x * sc, c.y + v.y * sc, c.z + v.z * sc, c.w + v.w * sc);
   }
+}
+// LayerNorm (+affine) (+modulate) of one row value quad, given the row mean and 1/den
+__device__ __forceinline__ float4 rr_ln(const RowReduceArgs& a, int m, int n, float4 d, float den) {
+  float4 hh = make_float4(d.x / den, d.y / den, d.z / den, d.w / den);
+  if (a.ln_w)
+    hh = f4add(f4mul(hh, *reinterpret_cast<const float4*>(a.ln_w + n)), *reinterpret_cast<const float4*>(a.ln_b + n));
+  if (a.mshift) {
+    const float4 sc = *reinterpret_cast<const float4*>(a.mscale + (long)m * a.ldm + n);
+    const float4 sf = *reinterpret_cast<const float4*>(a.mshift + (long)m * a.ldm + n);
+    hh = make_float4(hh.x * (1.0f + sc.x) + sf.x, hh.y * (1.0f + sc.y) + sf.y, hh.z * (1.0f + sc.z) + sf.z,
+                     hh.w * (1.0f + sc.w) + sf.w);
+  }
+  return hh;
+}
+
+template <int SMAX>
+__global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
+  __shared__ float sh[4];
+  const int m = blockIdx.x;
+  const int n0 = blockIdx.y * 1024 + 4 * threadIdx.x;
+  const bool ok = n0 < a.N;
+  const int n = ok ? n0 : 0;
+  const float4 v = rr_value<SMAX>(a, m, n);
+  if (ok) rr_store(a, m, n, v);
   if (!a.ln) return;  // LN rows are <= 1024 wide: gridDim.y == 1 (host-checked)
-  const float4 lw = *reinterpret_cast<const float4*>(a.ln_w ? a.ln_w + n : p);
-  const float4 lb = *reinterpret_cast<const float4*>(a.ln_w ? a.ln_b + n : p);
-  const float4 msc = *reinterpret_cast<const float4*>(a.mshift ? a.mscale + (long)m * a.ldm + n : p);
-  const float4 msf = *reinterpret_cast<const float4*>(a.mshift ? a.mshift + (long)m * a.ldm + n : p);
   const float s = ok ? (v.x + v.y) + (v.z + v.w) : 0.f;
   const float mean = block_sum(s, sh) / (float)a.N;
   const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
   const float q = ok ? (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w) : 0.f;
   const float den = sqrtf(block_sum(q, sh) / (float)a.N + a.eps);
   if (!ok) return;
-  float4 hh = make_float4(d.x / den, d.y / den, d.z / den, d.w / den);
-  if (a.ln_w) hh = f4add(f4mul(hh, lw), lb);
-  if (a.mshift)
-    hh = make_float4(hh.x * (1.0f + msc.x) + msf.x, hh.y * (1.0f + msc.y) + msf.y, hh.z * (1.0f + msc.z) + msf.z,
-                     hh.w * (1.0f + msc.w) + msf.w);
-  *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = hh;
+  *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = rr_ln(a, m, n, d, den);
+}
+
+// ---------------------------------------------------------------------------------------------
+// In-launch split-K combine (cdna_hip_programming.md, "In-launch split-K reduction"): slab
+// stores -> vmcnt(0) on every wave -> barrier -> one lane: agent-scope release fence, vmcnt(0),
+// relaxed agent-scope ticket add; the workgroup drawing target-1 is the reducer: one lane's
+// agent-scope acquire fence + vmcnt(0) before the barrier, then plain loads of the slabs.
+// The reducer re-arms the counter for the next launch. `flag` is a word of the kernel's one LDS
+// array (a second __shared__ object would de-pipeline the LDS-DMA loop).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool splitk_arrive(int* cnt, int target, float* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == target - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last ? 1.f : 0.f;
+  }
+  __syncthreads();
+  const bool last = *flag != 0.f;
+  __syncthreads();  // the flag word is reused by the caller's LDS afterwards
+  return last;
+}
+
+// rows [m0, m0+32) x cols [n0, n0+ncols) of the row-reduce epilogue (256 threads)
+template <int SMAX>
+__device__ void splitk_tile_finish(const RowReduceArgs& a, int m0, int n0, int ncols) {
+  const int per_row = ncols / 4;
+  for (int e = threadIdx.x; e < 32 * per_row; e += 256) {
+    const int m = m0 + e / per_row, n = n0 + 4 * (e % per_row);
+    if (m >= a.M || n >= a.N) continue;
+    rr_store(a, m, n, rr_value<SMAX>(a, m, n));
+  }
+}
+__device__ void splitk_finish(const RowReduceArgs& a, int m0, int n0, int ncols) {
+  if (a.S <= 1) splitk_tile_finish<1>(a, m0, n0, ncols);
+  else if (a.S <= 2) splitk_tile_finish<2>(a, m0, n0, ncols);
+  else if (a.S <= 4) splitk_tile_finish<4>(a, m0, n0, ncols);
+  else if (a.S <= 8) splitk_tile_finish<8>(a, m0, n0, ncols);
+  else splitk_tile_finish<16>(a, m0, n0, ncols);
+}
+// LayerNorm (+modulate) of rows [m0, m0+32) from Y (N <= 1024, N % 256 == 0): one wave per row
+__device__ void splitk_rows_ln(const RowReduceArgs& a, int m0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nq = a.N / 256;  // float4 per lane
+  for (int r = wave; r < 32; r += 4) {
+    const int m = m0 + r;
+    if (m >= a.M) break;
+    float4 v[4];
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i < nq) {
+        v[i] = *reinterpret_cast<const float4*>(a.Y + (long)m * a.ldy + 4 * lane + 256 * i);
+        sum += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+      }
+    }
+    const float mean = wave_sum(sum) / (float)a.N;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i < nq) {
+        v[i] = make_float4(v[i].x - mean, v[i].y - mean, v[i].z - mean, v[i].w - mean);
+        q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+      }
+    }
+    const float den = sqrtf(wave_sum(q) / (float)a.N + a.eps);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i < nq) {
+        const int n = 4 * lane + 256 * i;
+        *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = rr_ln(a, m, n, v[i], den);
+      }
+    }
+  }
+}
+// whole in-launch combine for the workgroup that stored tile (bx, by) of a 32 x ncols tiling
+__device__ void splitk_combine(const GemmArgs& g, int m0, int n0, int ncols, float* flag) {
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  if (!splitk_arrive(g.tickets + tile, g.S, flag)) return;
+  splitk_finish(g.rr, m0, n0, ncols);
+  if (g.fuse != 2) return;
+  if (!splitk_arrive(g.row_tickets + blockIdx.y, gridDim.x, flag)) return;
+  splitk_rows_ln(g.rr, m0);
 }
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s) {
