@@ -1568,15 +1568,33 @@ __global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, con
   __shared__ float sz[32];
   __shared__ float sx[16 * 512];
   const int b = blockIdx.x, tid = threadIdx.x;
+  // every operand load of the thread's two channels is issued before the arithmetic
+  float4 wqr[2][8], wur[2][8];
+  float qpv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = tid + 256 * u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      wqr[u][i] = *reinterpret_cast<const float4*>(wq + c * 32 + 4 * i);
+      wur[u][i] = *reinterpret_cast<const float4*>(wup + c * 32 + 4 * i);
+    }
+    qpv[u] = qprev[(long)b * 512 + c];
+  }
   if (tid < 32) sz[tid] = latent[b * 32 + tid] * emb_std[tid] + emb_mean[tid];
   __syncthreads();
   const bool upd = fl[b].valid != 0;
-  for (int c = tid; c < 512; c += 256) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = tid + 256 * u;
+    const float* wqf = reinterpret_cast<const float*>(wqr[u]);
+    const float* wuf = reinterpret_cast<const float*>(wur[u]);
     float q = 0.f;
-    for (int k = 0; k < 32; ++k) q += wq[c * 32 + k] * sz[k];
-    const float qp = qprev[(long)b * 512 + c];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) q += wqf[k] * sz[k];
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float v = q * wup[c * 32 + r] + qp * wup[c * 32 + 16 + r];
+      const float v = q * wuf[r] + qpv[u] * wuf[16 + r];
       sx[r * 512 + c] = v;
       x[((long)b * 16 + r) * 512 + c] = v;
     }
@@ -1755,30 +1773,50 @@ void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols
 }
 
 // Final SEANet conv (64 -> 1, k=3) with ELU'd input and 2-row history: one thread per sample.
-__global__ __launch_bounds__(256) void k_conv_cout1(const float* X, const float* H, int B, int T, int cin, int k,
+// One wave per (batch row, 64 consecutive outputs): lane c owns input channel c (cin == 64) and
+// loads its channel of the 64 + k - 1 input rows with coalesced 256-B row reads (history rows for
+// t < 0), applies ELU once per element, and the k-tap dot products are reduced across the wave.
+// One wave per (batch row, 64 consecutive outputs). The 64 + k - 1 input rows (cin == 64; history
+// rows for t < 0) are read with coalesced 256-B row loads, ELU'd once per element and transposed
+// through a padded LDS tile (row stride 65: conflict-free column reads); lane t then forms output
+// t as a plain k x cin dot product (weights broadcast from LDS).
+template <int KT>
+__global__ __launch_bounds__(256) void k_conv_cout1(const float* X, const float* H, int B, int T, int cin,
                                                     const float* w, const float* bias, float* Y) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)B * T) return;
-  const int b = (int)(idx / T), t = (int)(idx % T);
-  const int P = k - 1;
-  float acc = 0.f;
-  for (int j = 0; j < k; ++j) {
-    const int tt = t + j - P;
-    const float* src = tt >= 0 ? X + ((long)b * T + tt) * cin : H + ((long)b * P + (P + tt)) * cin;
-    const float* wr = w + j * cin;
-    for (int c = 0; c < cin; c += 4) {
-      const float4 xv = *reinterpret_cast<const float4*>(src + c);
-      const float4 wv = *reinterpret_cast<const float4*>(wr + c);
-      acc += elu1(xv.x) * wv.x + elu1(xv.y) * wv.y + elu1(xv.z) * wv.z + elu1(xv.w) * wv.w;
-    }
+  constexpr int P = KT - 1, ROWS = 64 + P;
+  __shared__ float tile[4][ROWS][65];
+  __shared__ float sw[KT * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < KT * 64; i += 256) sw[i] = w[i];
+  const int blk = blockIdx.x * 4 + wave;
+  const int nblk = (T + 63) / 64;
+  const bool live = blk < B * nblk;
+  const int b = live ? blk / nblk : 0, t0 = live ? (blk - b * nblk) * 64 : 0;
+  const float* xb = X + (long)b * T * cin + lane;
+  const float* hb = H + ((long)b * P + P) * cin + lane;
+  float e[ROWS];
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) {  // unconditional loads: rows past T re-read row T-1
+    const int tt = min(t0 + i - P, T - 1);
+    e[i] = tt >= 0 ? xb[(long)tt * cin] : hb[(long)tt * cin];
   }
-  Y[idx] = acc + bias[0];
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) tile[wave][i][lane] = elu1(e[i]);
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll 8
+  for (int c = 0; c < 64; ++c)
+#pragma unroll
+    for (int j = 0; j < KT; ++j) acc += sw[j * 64 + c] * tile[wave][lane + j][c];
+  if (live && t0 + lane < T) Y[(long)b * T + t0 + lane] = acc + bias[0];
 }
+
 void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, const float* w, const float* bias,
                 float* Y, hipStream_t s) {
-  const long total = (long)B * T;
-  hipLaunchKernelGGL(k_conv_cout1, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, X, H, B, T, cin, k, w,
-                     bias, Y);
+  const long waves = (long)B * ((T + 63) / 64);  // one lane per input channel: cin == 64, k == 3
+  (void)k;
+  hipLaunchKernelGGL(k_conv_cout1<3>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, X, H, B, T, cin, w, bias,
+                     Y);
 }
 
 // Encoder first conv (1 -> cout, k taps, zero history of k-1 samples): one thread per output.
