@@ -143,8 +143,8 @@ int ptts_plan_ops(ptts_engine* e, int n_rows, char* buf, int buflen);
 
 /* Measurement: the step plan split at the FlowLM/flow-head -> Mimi boundary, timed as two
  * graphs alone and launched together on two streams; us8 = {front, back, both, both with the
- * front on a high-priority stream, both with the front / back on disjoint CU sets of 32/224,
- * 64/192, 128/128 CUs, unused} microseconds per step. Clobbers engine state (timing only). */
+ * front on a high-priority stream, 0, 0, 0, 0} microseconds per step. Clobbers engine state
+ * (timing only). */
 int ptts_probe_overlap(ptts_engine* e, int n_rows, int reps, double* us8);
 
 const char* ptts_last_error(void);

@@ -210,7 +210,7 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   // wide skinny GEMMs (FlowLM qkv/ff1, flow-head adaLN): 32x128 LDS-DMA tiles, 8-way split-K
   // (tools/gemm_bench.hip on MI355X: qkv 6.7 -> 6.3 us, ff1 7.9 -> 6.5 us, ada 10.1 -> 8.7 us)
   if (M <= 64 && N >= 3072) {
-    layout = 13;
+    layout = getenv("PTTS_SKINNY_NBUF4") ? 13 : 7;  // 2-buffer LDS (40 KB) co-resides with the back part
     S = std::max(1, std::min(8, K / 64));
   } else if (M >= 256) {  // prefill passes: MFMA-bound, 64x64 LDS-DMA tiles, no split
     layout = 12;
@@ -242,11 +242,11 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
 void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r) {
   GemmArgs g = last_split_;
   const bool prev_is_gemm = !ops.empty() && last_split_op_ == ops.size() - 1;
-  const bool tiles_ok = g.layout == 0 || g.layout == 13;
+  const bool tiles_ok = g.layout == 0 || g.layout == 13 || g.layout == 7;
   const bool ln_ok = !r.ln || (r.N % 256 == 0 && r.N <= 1024);
   const bool same = prev_is_gemm && r.P == g.partial && r.S == g.S && r.M == g.M && r.N == g.N;
   if (fuse_splitk_ && same && tiles_ok && ln_ok) {
-    const int gx = g.layout == 13 ? (g.N + 127) / 128 : (g.N + 31) / 32;
+    const int gx = (g.layout == 13 || g.layout == 7) ? (g.N + 127) / 128 : (g.N + 31) / 32;
     const int gy = (g.M + 31) / 32;
     PTTS_REQUIRE(gx * gy <= TICKETS && gy <= ROW_TICKETS, "split-K ticket arrays too small");
     g.fuse = r.ln ? 2 : 1;
@@ -838,29 +838,6 @@ void Engine::overlap_probe(int B, int reps, double* us) {
   us[1] = timed(1);
   us[2] = timed(2);
   us[3] = timed(3);
-  // CU partitions: front on the first F CUs of every XCD-interleaved group, back on the rest
-  int ncu = 0;
-  PTTS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_));
-  const int fronts[3] = {32, 64, 128};
-  for (int v = 0; v < 3; ++v) {
-    std::vector<uint32_t> mf((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
-    for (int cu = 0; cu < ncu; ++cu) {
-      // spread the front's CUs evenly over the chip (every ncu/F-th CU)
-      const bool front = (cu % (ncu / fronts[v])) == 0;
-      (front ? mf : mb)[cu / 32] |= 1u << (cu % 32);
-    }
-    hipStream_t sf = nullptr, sbk = nullptr;
-    PTTS_HIP(hipExtStreamCreateWithCUMask(&sf, (uint32_t)mf.size(), mf.data()));
-    PTTS_HIP(hipExtStreamCreateWithCUMask(&sbk, (uint32_t)mb.size(), mb.data()));
-    hipStream_t keep_hi = s_hi, keep_lo = s_lo;
-    s_hi = sf;
-    s_lo = sbk;
-    us[4 + v] = timed(3);
-    s_hi = keep_hi;
-    s_lo = keep_lo;
-    (void)hipStreamDestroy(sf);
-    (void)hipStreamDestroy(sbk);
-  }
   for (int part = 0; part < 2; ++part) {
     (void)hipGraphExecDestroy(ge[part]);
     (void)hipGraphDestroy(g[part]);

@@ -22,4 +22,3 @@ us = (C.c_double * 8)()
 check(lib().ptts_probe_overlap(eng.handle, B, 50, us))
 print(f"front {us[0]:.1f} us, back {us[1]:.1f} us, both concurrently {us[2]:.1f} us "
       f"(sum {us[0] + us[1]:.1f}); front high-priority {us[3]:.1f} us")
-print(f"CU split front/back 32/224: {us[4]:.1f} us, 64/192: {us[5]:.1f} us, 128/128: {us[6]:.1f} us")
