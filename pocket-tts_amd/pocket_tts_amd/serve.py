@@ -1,0 +1,353 @@
+"""Batched serving front end: continuous batching of TTS requests over
+the engine's slots, and the reference server's HTTP surface on top of it.
+
+The reference server serializes every generation behind one mutex
+(pocket-tts-cli/src/server/state.rs:69) and runs one utterance at a time per process. Here a
+`BatchScheduler` owns one engine (one GPU) and a driver thread:
+
+  1. requests wait in a queue; whenever slots are free, all waiting requests that fit are
+     admitted in ONE batched admission (`ptts_slots_open`: shared text-prefill pass);
+  2. every engine step advances all admitted rows together (`ptts_step`), and each row's
+     1920-sample frame is handed to its request's stream as soon as it exists;
+  3. a row's slot is recycled when its last frame (EOS tail or max_gen_len) has been delivered.
+
+Works with both stepping modes of the engine (with `pipeline=True` a row's frames arrive one
+step after they are computed). `MultiGpuScheduler` spreads requests over one scheduler per GPU
+(replicas, no inter-GPU traffic: DESIGN.md §6).
+
+HTTP (`create_app`, FastAPI; routes of pocket-tts-cli/src/server/routes.rs:20-30):
+  GET  /health             {"status": "healthy", "version": ...}
+  POST /generate           JSON {text | token_ids, voice?, temperature?, eos_threshold?,
+                           noise_clamp?, lsd_steps?} -> audio/wav (handlers.rs:128-213)
+  POST /stream             same body -> chunked 16-bit PCM LE, one chunk per frame
+                           (handlers.rs:215-310)
+  POST /v1/audio/speech    OpenAI body {model, input, voice?, response_format?} -> wav / pcm
+                           (handlers.rs:380-398)
+Wire formats follow crates/pocket-tts/src/audio.rs:110-185 (clamp to [-1, 1], x 32767,
+truncate to i16; 16-bit mono RIFF/WAVE).
+"""
+
+from __future__ import annotations
+
+import queue
+import struct
+import threading
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Callable, Iterator, Sequence
+
+import numpy as np
+
+from ._lib import FRAME, SAMPLE_RATE
+from .engine import GenerationParams, Voice
+from .tts_model import estimate_frames_after_eos, max_gen_len, prepare_text_prompt
+
+VERSION = "0.1.0"
+
+
+# ---------------------------------------------------------------------------------------------
+# wire formats (audio.rs:110-185)
+def pcm_i16_le_bytes(samples: np.ndarray) -> bytes:
+    x = np.clip(np.asarray(samples, np.float32).reshape(-1), -1.0, 1.0) * 32767.0
+    return x.astype(np.int16).astype("<i2").tobytes()  # float -> int cast truncates toward zero
+
+
+def wav_bytes(samples: np.ndarray, sample_rate: int = SAMPLE_RATE) -> bytes:
+    data = pcm_i16_le_bytes(samples)
+    hdr = b"RIFF" + struct.pack("<I", 36 + len(data)) + b"WAVE"
+    hdr += b"fmt " + struct.pack("<IHHIIHH", 16, 1, 1, sample_rate, sample_rate * 2, 2, 16)
+    hdr += b"data" + struct.pack("<I", len(data))
+    return hdr + data
+
+
+# ---------------------------------------------------------------------------------------------
+@dataclass
+class Request:
+    ids: np.ndarray
+    voice: Voice
+    params: GenerationParams
+    out: "queue.Queue" = field(default_factory=queue.Queue)  # np.ndarray frames, then None
+    slot: int = -1
+    frames: int = 0
+
+    def stream(self, timeout: float | None = None) -> Iterator[np.ndarray]:
+        """Frames [1920] float32 as they are produced; raises the driver's error if any."""
+        while True:
+            item = self.out.get(timeout=timeout)
+            if item is None:
+                return
+            if isinstance(item, BaseException):
+                raise item
+            yield item
+
+    def audio(self, timeout: float | None = None) -> np.ndarray:
+        frames = list(self.stream(timeout))
+        return np.concatenate(frames) if frames else np.zeros(0, np.float32)
+
+
+class BatchScheduler:
+    """Continuous batching over one engine's slots (one GPU)."""
+
+    def __init__(self, engine, max_rows: int | None = None):
+        self.engine = engine
+        self.max_rows = min(max_rows or engine.max_slots, engine.max_slots)
+        self.waiting: deque[Request] = deque()
+        self.active: dict[int, Request] = {}
+        self.cv = threading.Condition()
+        self.running = True
+        self.steps = 0
+        self.thread = threading.Thread(target=self._loop, name="ptts-scheduler", daemon=True)
+        self.thread.start()
+
+    # -- client side
+    def submit(self, ids, voice: Voice, params: GenerationParams) -> Request:
+        req = Request(np.asarray(ids, np.int32).reshape(-1), voice, params)
+        if voice.n_frames + req.ids.size + params.max_frames > self.engine.max_ctx:
+            raise ValueError("voice + text + max_frames exceeds the engine's max_ctx")
+        with self.cv:
+            if not self.running:
+                raise RuntimeError("scheduler stopped")
+            self.waiting.append(req)
+            self.cv.notify()
+        return req
+
+    def load(self) -> int:
+        with self.cv:
+            return len(self.active) + len(self.waiting)
+
+    def close(self):
+        with self.cv:
+            self.running = False
+            self.cv.notify()
+        self.thread.join()
+
+    # -- driver thread
+    def _admit(self):
+        free = [s for s in range(self.max_rows) if s not in self.active]
+        batch = []
+        while self.waiting and free:
+            req = self.waiting.popleft()
+            req.slot = free.pop(0)
+            batch.append(req)
+        if batch:
+            self.engine.open_many([r.slot for r in batch], [r.voice for r in batch], [r.ids for r in batch],
+                                  [r.params for r in batch])
+            for r in batch:
+                self.active[r.slot] = r
+
+    def _loop(self):
+        try:
+            while True:
+                with self.cv:
+                    while self.running and not self.waiting and not self.active:
+                        self.cv.wait()
+                    if not self.running:
+                        break
+                    self._admit()
+                    rows = max(self.active) + 1
+                res = self.engine.step(rows)
+                self.steps += 1
+                done = []
+                for slot, req in list(self.active.items()):
+                    if slot < rows and res.valid[slot]:
+                        req.frames += 1
+                        req.out.put(res.pcm[slot].copy())
+                        if res.last[slot]:
+                            req.out.put(None)
+                            done.append(slot)
+                with self.cv:
+                    for slot in done:
+                        del self.active[slot]
+        except BaseException as e:  # deliver the failure to every waiting client
+            with self.cv:
+                self.running = False
+                for req in list(self.active.values()) + list(self.waiting):
+                    req.out.put(e)
+                    req.out.put(None)
+                self.active.clear()
+                self.waiting.clear()
+        finally:
+            with self.cv:
+                for req in list(self.active.values()) + list(self.waiting):
+                    req.out.put(None)
+
+
+class MultiGpuScheduler:
+    """Replicas: one BatchScheduler per GPU engine; a request goes to the least loaded one."""
+
+    def __init__(self, schedulers: Sequence[BatchScheduler]):
+        self.schedulers = list(schedulers)
+
+    def submit(self, ids, voices: Sequence[Voice], params: GenerationParams) -> Request:
+        i = min(range(len(self.schedulers)), key=lambda k: self.schedulers[k].load())
+        return self.schedulers[i].submit(ids, voices[i], params)
+
+    def close(self):
+        for s in self.schedulers:
+            s.close()
+
+
+# ---------------------------------------------------------------------------------------------
+def load_tokenizer(path: str) -> Callable[[str], list[int]]:
+    """SentencePiece-Unigram tokenizer.json with the native Rust settings (text.rs:71-79):
+    Metaspace with prepend "always" and no BOS post-processor."""
+    from tokenizers import Tokenizer, decoders, pre_tokenizers
+
+    tok = Tokenizer.from_file(path)
+    tok.pre_tokenizer = pre_tokenizers.Metaspace(replacement="▁", prepend_scheme="always")
+    tok.decoder = decoders.Metaspace(replacement="▁", prepend_scheme="always")
+    tok.post_processor = None
+    return lambda text: tok.encode(text, add_special_tokens=False).ids
+
+
+class TTSService:
+    """Request-level logic shared by the HTTP routes: text -> ids, voice lookup, params."""
+
+    def __init__(self, scheduler, voices: dict[str, Voice | Sequence[Voice]], default_voice: str,
+                 tokenizer: Callable[[str], Sequence[int]] | None = None, temp: float = 0.7,
+                 eos_threshold: float = -4.0, noise_clamp: float | None = None, lsd_decode_steps: int = 1):
+        self.scheduler = scheduler
+        self.voices = voices
+        self.default_voice = default_voice
+        self.tokenizer = tokenizer
+        self.temp, self.eos_threshold, self.noise_clamp = temp, eos_threshold, noise_clamp
+        self.lsd_decode_steps = lsd_decode_steps
+        self._seed = 0
+        self._lock = threading.Lock()
+
+    def request(self, text: str | None = None, token_ids=None, voice: str | None = None,
+                temperature: float | None = None, eos_threshold: float | None = None,
+                noise_clamp: float | None = None, lsd_steps: int | None = None) -> Request:
+        if lsd_steps is not None and lsd_steps != self.lsd_decode_steps:
+            raise ValueError(f"lsd_steps is fixed at engine creation ({self.lsd_decode_steps})")
+        if token_ids is not None:
+            ids = np.asarray(token_ids, np.int32).reshape(-1)
+            mgl, fae = (max(1, ids.size // 2) + 2) * 13, 3
+        elif text is not None:
+            if self.tokenizer is None:
+                raise ValueError("no tokenizer configured: send token_ids")
+            prepared = prepare_text_prompt(text)
+            ids = np.asarray(self.tokenizer(prepared), np.int32)
+            mgl, fae = max_gen_len(prepared), estimate_frames_after_eos(text)
+        else:
+            raise ValueError("text or token_ids required")
+        name = voice or self.default_voice
+        if name not in self.voices:
+            raise ValueError(f"unknown voice {name!r}")
+        with self._lock:
+            self._seed += 1
+            seed = self._seed
+        p = GenerationParams(temp=self.temp if temperature is None else temperature,
+                             eos_threshold=self.eos_threshold if eos_threshold is None else eos_threshold,
+                             noise_clamp=self.noise_clamp if noise_clamp is None else noise_clamp,
+                             frames_after_eos=fae, max_frames=mgl, seed=seed)
+        return self.scheduler.submit(ids, self.voices[name], p)  # MultiGpuScheduler: one voice per GPU
+
+
+from pydantic import BaseModel  # noqa: E402  (request bodies; module level so FastAPI resolves them)
+
+
+class GenerateRequest(BaseModel):
+    """handlers.rs:84-92 (+ token_ids when no tokenizer is configured)."""
+
+    text: str | None = None
+    token_ids: list[int] | None = None
+    voice: str | None = None
+    temperature: float | None = None
+    lsd_steps: int | None = None
+    eos_threshold: float | None = None
+    noise_clamp: float | None = None
+
+
+class OpenAIRequest(BaseModel):
+    """handlers.rs:378-385."""
+
+    model: str = "pocket-tts"
+    input: str | None = None
+    voice: str | None = None
+    response_format: str | None = None
+    token_ids: list[int] | None = None
+
+
+def create_app(service: TTSService):
+    from fastapi import FastAPI, HTTPException
+    from fastapi.responses import JSONResponse, Response, StreamingResponse
+
+    app = FastAPI(title="pocket-tts (MI355X engine)")
+
+    def submit(**kw) -> Request:
+        try:
+            return service.request(**kw)
+        except ValueError as e:
+            raise HTTPException(status_code=400, detail=str(e)) from e
+
+    @app.get("/health")
+    def health():
+        return JSONResponse({"status": "healthy", "version": VERSION})
+
+    @app.post("/generate")
+    def generate(req: GenerateRequest):
+        r = submit(**req.model_dump())
+        return Response(wav_bytes(r.audio()), media_type="audio/wav")
+
+    @app.post("/stream")
+    def stream(req: GenerateRequest):
+        r = submit(**req.model_dump())
+        return StreamingResponse((pcm_i16_le_bytes(f) for f in r.stream()), media_type="audio/pcm")
+
+    @app.post("/v1/audio/speech")
+    def openai_speech(req: OpenAIRequest):
+        r = submit(text=req.input, token_ids=req.token_ids, voice=req.voice)
+        audio = r.audio()
+        if (req.response_format or "wav") == "pcm":
+            return Response(pcm_i16_le_bytes(audio), media_type="audio/pcm")
+        return Response(wav_bytes(audio), media_type="audio/wav")
+
+    return app
+
+
+def main(argv=None):
+    """python -m pocket_tts_amd.serve --voice NAME=prompt.npy [--voice ...] [--tokenizer t.json]
+    [--gpus N] [--slots 32] [--port 8000]"""
+    import argparse
+
+    from .engine import Engine
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--voice", action="append", default=[], help="NAME=path (.npy prompt [F,1024] or .wav)")
+    ap.add_argument("--tokenizer", default=None)
+    ap.add_argument("--weights", default=None)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--slots", type=int, default=32)
+    ap.add_argument("--max-ctx", type=int, default=1024)
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8000)
+    args = ap.parse_args(argv)
+    engines = [Engine(device=d, max_slots=args.slots, max_ctx=args.max_ctx, weights_path=args.weights, pipeline=True)
+               for d in range(args.gpus)]
+    voices: dict[str, list[Voice]] = {}
+    for spec in args.voice or []:
+        name, path = spec.split("=", 1)
+        if path.endswith(".npy"):
+            prompt = np.load(path, allow_pickle=False).astype(np.float32)
+            voices[name] = [e.voice_from_prompt(prompt) for e in engines]
+        else:
+            from .tts_model import read_wav_mono
+
+            x = read_wav_mono(path)
+            voices[name] = [e.voice_from_pcm(x) for e in engines]
+    if not voices:
+        raise SystemExit("at least one --voice NAME=path is required")
+    scheds = [BatchScheduler(e) for e in engines]
+    sched = scheds[0] if len(scheds) == 1 else MultiGpuScheduler(scheds)
+    if len(scheds) == 1:
+        voices = {k: v[0] for k, v in voices.items()}
+    service = TTSService(sched, voices, default_voice=next(iter(voices)),
+                         tokenizer=load_tokenizer(args.tokenizer) if args.tokenizer else None)
+    import uvicorn
+
+    uvicorn.run(create_app(service), host=args.host, port=args.port)
+
+
+if __name__ == "__main__":
+    main()

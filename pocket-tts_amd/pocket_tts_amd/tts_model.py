@@ -49,6 +49,23 @@ def max_gen_len(prepared_text: str) -> int:
     return (len(prepared_text.split()) + 2) * 13
 
 
+def read_wav_mono(path: str) -> np.ndarray:
+    """16-bit PCM WAV -> mono float32 at 24 kHz (audio.rs:12-108: channel mean, /32768; the
+    resampler is scipy's polyphase resample_poly where the reference uses rubato)."""
+    with wave.open(str(path), "rb") as w:
+        sr, ch, sw, n = w.getframerate(), w.getnchannels(), w.getsampwidth(), w.getnframes()
+        raw = w.readframes(n)
+    if sw != 2:
+        raise ValueError("only 16-bit PCM WAV is supported")
+    x = np.frombuffer(raw, np.int16).astype(np.float32).reshape(-1, ch).mean(axis=1) / 32768.0
+    if sr != SAMPLE_RATE:
+        from scipy.signal import resample_poly
+
+        g = np.gcd(sr, SAMPLE_RATE)
+        x = resample_poly(x, SAMPLE_RATE // g, sr // g).astype(np.float32)
+    return x.astype(np.float32)
+
+
 class TTSModel:
     def __init__(self, engine: Engine, temp: float, lsd_decode_steps: int, eos_threshold: float,
                  noise_clamp: float | None, tokenizer: Callable[[str], Sequence[int]] | None = None):
@@ -84,18 +101,7 @@ class TTSModel:
         return self.engine.voice_from_pcm(np.asarray(audio, np.float32).reshape(-1))
 
     def get_voice_state(self, path: str) -> Voice:
-        with wave.open(str(path), "rb") as w:
-            sr, ch, sw, n = w.getframerate(), w.getnchannels(), w.getsampwidth(), w.getnframes()
-            raw = w.readframes(n)
-        if sw != 2:
-            raise ValueError("only 16-bit PCM WAV is supported")
-        x = np.frombuffer(raw, np.int16).astype(np.float32).reshape(-1, ch).mean(axis=1) / 32768.0
-        if sr != SAMPLE_RATE:
-            from scipy.signal import resample_poly
-
-            g = np.gcd(sr, SAMPLE_RATE)
-            x = resample_poly(x, SAMPLE_RATE // g, sr // g).astype(np.float32)
-        return self.get_voice_state_from_tensor(x)
+        return self.get_voice_state_from_tensor(read_wav_mono(path))
 
     # ---- generation
     def _ids(self, text_or_ids) -> tuple[np.ndarray, int, int]:

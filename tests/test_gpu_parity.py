@@ -309,3 +309,40 @@ def test_long_utterance_wraps_mimi_ring(gpu_engine, oracle):
         worst = max(worst, rms(r.pcm[0] - o["pcm"]))
         gpu_engine.set_latent(0, o["latent"])  # teacher forcing: no drift over 70 AR steps
     assert worst <= 1e-4, worst
+
+
+def test_batch_scheduler_matches_oracle(oracle):
+    """Serving front end (f1) on the real pipelined engine: 6 requests of different lengths through
+    3 slots (continuous admission into recycled slots); every request's audio equals its own
+    oracle run."""
+    import pocket_tts_amd as pt
+    from pocket_tts_amd.serve import BatchScheduler
+
+    d = load_golden("e2e_lsd1.safetensors")
+    eng = pt.Engine(device=0, max_slots=3, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True)
+    sch = BatchScheduler(eng)
+    try:
+        rng = np.random.default_rng(3)
+        jobs = []
+        for u in range(6):
+            F = 4 + u
+            prompt = (d["prompt"][:F] * (1.0 + 0.03 * u)).astype(np.float32)
+            ids = rng.integers(0, 4000, size=2 + 3 * u).astype(np.int32)
+            n = 2 + u % 3
+            v = eng.voice_from_prompt(prompt)
+            jobs.append((prompt, ids, n, v))
+        reqs = [sch.submit(ids, v, params(max_frames=n)) for _, ids, n, v in jobs]
+        for (prompt, ids, n, _), req in zip(jobs, reqs):
+            frames = list(req.stream(timeout=120))
+            assert len(frames) == n
+            s = oracle.new_state(128)
+            s.prefill(prompt)
+            s.prefill_tokens(ids)
+            lat = None
+            for f in frames:
+                o = s.step(lat)
+                lat = o["latent"]
+                assert rms(f - o["pcm"]) <= 1e-4
+    finally:
+        sch.close()
+        eng.close()

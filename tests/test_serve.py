@@ -1,0 +1,132 @@
+"""Serving front end on CPU: continuous-batching scheduler logic and the HTTP
+routes, driven by a stand-in engine with the ptts_slots_open / ptts_step contract (sequential and
+pipelined frame delivery). The real-engine run of the same scheduler is a GPU parity test."""
+
+import io
+import struct
+import wave
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from pocket_tts_amd import GenerationParams
+from pocket_tts_amd.serve import BatchScheduler, MultiGpuScheduler, TTSService, create_app, pcm_i16_le_bytes, wav_bytes
+
+
+class FakeEngine:
+    """Row r of step k of utterance u yields a frame filled with u*1000 + k; the last frame is
+    flagged at max_frames. pipeline=True delivers each frame one call later (ptts_engine_config)."""
+
+    def __init__(self, max_slots=4, pipeline=False):
+        self.max_slots, self.max_ctx, self.pipeline = max_slots, 10_000, pipeline
+        self.rows = {}
+        self.pending = None
+        self.calls = 0
+        self.admissions = []
+
+    def open_many(self, slots, voices, ids_list, params_list):
+        self.admissions.append(list(slots))
+        for s, ids, p in zip(slots, ids_list, params_list):
+            self.rows[s] = {"u": int(ids[0]), "k": 0, "n": p.max_frames}
+            if self.pending is not None:  # admission discards the slot's undrained frame
+                self.pending["valid"][s] = False
+
+    def _compute(self, n):
+        out = {"pcm": np.zeros((n, 1920), np.float32), "valid": np.zeros(n, bool), "last": np.zeros(n, bool)}
+        for s, st in list(self.rows.items()):
+            if s >= n:
+                continue
+            out["pcm"][s] = st["u"] * 1000 + st["k"]
+            out["valid"][s] = True
+            st["k"] += 1
+            out["last"][s] = st["k"] == st["n"]
+            if out["last"][s]:
+                del self.rows[s]
+        return out
+
+    def step(self, n):
+        self.calls += 1
+        cur = self._compute(n)
+        if not self.pipeline:
+            return SimpleNamespace(**cur)
+        prev, self.pending = self.pending, cur
+        if prev is None:
+            return SimpleNamespace(pcm=np.zeros((n, 1920), np.float32), valid=np.zeros(n, bool),
+                                   last=np.zeros(n, bool))
+        m = min(n, prev["valid"].size)
+        r = SimpleNamespace(pcm=np.zeros((n, 1920), np.float32), valid=np.zeros(n, bool), last=np.zeros(n, bool))
+        r.pcm[:m], r.valid[:m], r.last[:m] = prev["pcm"][:m], prev["valid"][:m], prev["last"][:m]
+        return r
+
+
+VOICE = SimpleNamespace(n_frames=10)
+
+
+def params(n):
+    return GenerationParams(temp=0.0, eos_threshold=float("inf"), max_frames=n, seed=1)
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_scheduler_continuous_batching(pipeline):
+    eng = FakeEngine(max_slots=4, pipeline=pipeline)
+    sch = BatchScheduler(eng)
+    try:
+        lens = [5, 1, 3, 7, 2, 4, 6, 3, 1, 8]  # 10 requests through 4 slots
+        reqs = [sch.submit([u + 1, 7, 7], VOICE, params(n)) for u, n in enumerate(lens)]
+        for u, (req, n) in enumerate(zip(reqs, lens)):
+            frames = list(req.stream(timeout=10))
+            assert len(frames) == n
+            assert [int(f[0]) for f in frames] == [(u + 1) * 1000 + k for k in range(n)]
+        assert all(len(a) <= 4 for a in eng.admissions)
+        assert sum(len(a) for a in eng.admissions) == len(lens)
+        # continuous batching: far fewer engine calls than running the requests one by one
+        assert eng.calls < sum(lens) - 10
+    finally:
+        sch.close()
+
+
+def test_multi_gpu_scheduler_spreads_requests():
+    scheds = [BatchScheduler(FakeEngine(max_slots=2)) for _ in range(3)]
+    multi = MultiGpuScheduler(scheds)
+    try:
+        reqs = [multi.submit([u + 1], [VOICE] * 3, params(4)) for u in range(9)]
+        for u, r in enumerate(reqs):
+            assert [int(f[0]) for f in r.stream(timeout=10)] == [(u + 1) * 1000 + k for k in range(4)]
+        assert all(s.engine.calls > 0 for s in scheds)
+    finally:
+        multi.close()
+
+
+def test_wire_formats_match_reference_rules():
+    x = np.array([0.0, 0.5, -0.5, 1.0, -1.0, 2.0, -3.0, 0.99999, -0.00001], np.float32)
+    got = np.frombuffer(pcm_i16_le_bytes(x), "<i2")
+    # audio.rs:139-140: clamp to [-1, 1], * 32767, truncate toward zero
+    assert got.tolist() == [0, 16383, -16383, 32767, -32767, 32767, -32767, 32766, 0]
+    w = wave.open(io.BytesIO(wav_bytes(x)), "rb")
+    assert (w.getnchannels(), w.getsampwidth(), w.getframerate(), w.getnframes()) == (1, 2, 24000, x.size)
+    assert w.readframes(x.size) == pcm_i16_le_bytes(x)
+
+
+def test_http_routes():
+    from fastapi.testclient import TestClient
+
+    sch = BatchScheduler(FakeEngine(max_slots=2, pipeline=True))
+    svc = TTSService(sch, {"alba": VOICE}, default_voice="alba", tokenizer=lambda s: [5] * len(s.split()))
+    try:
+        c = TestClient(create_app(svc))
+        assert c.get("/health").json()["status"] == "healthy"
+        r = c.post("/generate", json={"token_ids": [3, 1, 2, 2]})  # max_gen_len (4//2+2)*13 = 52 frames
+        assert r.status_code == 200 and r.headers["content-type"] == "audio/wav"
+        w = wave.open(io.BytesIO(r.content), "rb")
+        assert w.getnframes() == 52 * 1920
+        r = c.post("/stream", json={"text": "Hello world", "voice": "alba"})
+        assert r.status_code == 200 and len(r.content) % (1920 * 2) == 0 and len(r.content) > 0
+        r = c.post("/v1/audio/speech", json={"model": "pocket-tts", "input": "Hi there friend.",
+                                             "response_format": "pcm"})
+        assert r.status_code == 200 and len(r.content) % 3840 == 0
+        assert c.post("/generate", json={"token_ids": [1], "voice": "nope"}).status_code == 400
+        assert c.post("/generate", json={"token_ids": [1], "lsd_steps": 4}).status_code == 400
+        assert c.post("/generate", json={}).status_code == 400
+    finally:
+        sch.close()
