@@ -93,6 +93,24 @@ int ptts_voice_from_prompt(ptts_engine* e, const float* prompt, int n_frames, pt
  * Mimi encoder -> speaker projection -> FlowLM prefill. n_samples is zero-padded to a
  * multiple of 1920. */
 int ptts_voice_from_pcm(ptts_engine* e, const float* pcm, int n_samples, ptts_voice** out);
+/* The voice-cloning front end of TTSModel::get_voice_state / get_voice_state_from_bytes
+ * (tts_model.rs:428-463) after the WAV decode, then get_voice_state_from_tensor (:504-577):
+ * `n_samples` mono samples at `sample_rate` Hz are resampled to 24 kHz on the GPU (the
+ * resample_poly rule of the Python reference's convert_audio, audio_utils.py:8-28, which the Rust
+ * resample() of audio.rs:197-255 states it matches), zero-padded to whole frames and encoded.
+ * chunk_frames = TTSModel.voice_prompt_chunk_frames: the encoder chunk length in frames; 0 = the
+ * reference's adaptive rule (adaptive_voice_prompt_chunk_frames, tts_model.rs:562-577: whole
+ * prompt up to 120 frames, then 120/180/240), < 0 = one pass (the Python reference,
+ * tts_model.py:258-262). Each chunk re-applies the downsample conv's replicate padding, as the
+ * Rust driver's step=0 per chunk does (tts_model.rs:536-541, conv.rs:116-123).
+ * ptts_voice_from_pcm(e, pcm, n, out) == ptts_voice_from_audio(e, pcm, n, 24000, 0, out). */
+int ptts_voice_from_audio(ptts_engine* e, const float* samples, int n_samples, int sample_rate, int chunk_frames,
+                          ptts_voice** out);
+/* The GPU resampler alone (audio.rs:197-255 `resample` for one channel): y receives
+ * ptts_resample_len(n_samples, sr_from, sr_to) samples = ceil(n * up / down) with up/down the
+ * rates divided by their gcd. */
+int ptts_resample_len(int n_samples, int sr_from, int sr_to);
+int ptts_resample(ptts_engine* e, const float* x, int n_samples, int sr_from, int sr_to, float* y);
 /* Conditioning rows the voice holds (frames). */
 int ptts_voice_len(const ptts_voice* v);
 /* The [n_frames x 1024] conditioning a PCM voice was built from (host copy); for tests. */

@@ -628,6 +628,11 @@ void orc_step(const orc_model* m, orc_state* s, const float* latent_in, const fl
 /* ---------------- encoder (voice cloning) ---------------- */
 void orc_encode(const orc_model* m, const float* pcm, int n, float* cond, float* after_enc, float* after_tr,
                 float* latent_o) {
+  orc_encode_ex(m, pcm, n, -1, cond, after_enc, after_tr, latent_o);
+}
+
+void orc_encode_ex(const orc_model* m, const float* pcm, int n, int chunk_frames, float* cond, float* after_enc,
+                   float* after_tr, float* latent_o) {
   int T = n;
   float* a = (float*)malloc(sizeof(float) * (size_t)T * 64);
   float* b = (float*)malloc(sizeof(float) * (size_t)T * 64);
@@ -654,15 +659,84 @@ void orc_encode(const orc_model* m, const float* pcm, int n, float* cond, float*
   for (int l = 0; l < MNL; ++l) tlayer(&m->menc[l], b, T, MD, MNH, MFF, ring, T, 0, MCTX);
   free(ring);
   if (after_tr) memcpy(after_tr, b, sizeof(float) * (size_t)T * 512);
-  /* ConvDownsample1d, replicate padding on the first frame (conv.rs:116-123; conv.py:103-108) */
+  /* ConvDownsample1d, replicate padding on the first frame (conv.rs:116-123; conv.py:103-108).
+   * The Rust driver encodes chunk by chunk with step=0 every time (tts_model.rs:536-541), so the
+   * replicate padding is re-applied at each chunk's first frame; the streaming convs and the
+   * transformer before it carry their state across chunks, which equals the one pass above. */
   Conv dc = {m->down_w, NULL, 512, 512, 32, 16};
-  for (int t = 0; t < 16; ++t) memcpy(hist + t * 512, b, sizeof(float) * 512);
-  sconv(&dc, b, T, hist, a, 0);
   int F = T / 16;
+  const int cf = chunk_frames <= 0 ? F : chunk_frames;
+  for (int c0 = 0; c0 < F; c0 += cf) {
+    const int nf = F - c0 < cf ? F - c0 : cf;
+    const float* xc = b + (size_t)c0 * 16 * 512;
+    for (int t = 0; t < 16; ++t) memcpy(hist + t * 512, xc, sizeof(float) * 512);
+    sconv(&dc, xc, nf * 16, hist, a + (size_t)c0 * 512, 0);
+  }
   if (latent_o) memcpy(latent_o, a, sizeof(float) * (size_t)F * 512);
   /* speaker projection (tts_model.rs:543-553) */
   linear(cond, a, m->speaker_proj, NULL, F, D, MD);
   free(a); free(b); free(v);
+}
+
+/* ---------------- resampler (voice-cloning front end) ----------------
+ * scipy.signal.resample_poly(x, up, down) with its default Kaiser(5.0) FIR, as the Python reference
+ * calls it in convert_audio (python-reference/pocket_tts/data/audio_utils.py:8-28); the Rust
+ * reference's audio.rs:197-255 states it matches that function (it calls rubato 0.14.1
+ * FastFixedIn/Septic, whose source is not in the reference: that drift stays unpinned, and the
+ * reference's own test allows 0.3 for it, parity_tests.rs:379-433).
+ * Filter: firwin(2*half+1, 1/max(up,down)), half = 10*max(up,down): h[i] = fc*sinc(fc*(i-half))
+ * * kaiser(5.0)[i], normalised to unit DC gain, cast to f32 and scaled by `up` in f32 (scipy casts
+ * the taps to the f32 input dtype). Output m = sum_j x[j] * h[m*down + half - j*up]; the f32
+ * products are accumulated in double. */
+static double bessel_i0(double x) {
+  double s = 1.0, t = 1.0, q = 0.25 * x * x;
+  for (int k = 1; k < 500; ++k) {
+    t *= q / ((double)k * k);
+    s += t;
+    if (t < 1e-17 * s) break;
+  }
+  return s;
+}
+static int gcd_int(int a, int b) {
+  while (b) { int t = a % b; a = b; b = t; }
+  return a;
+}
+int orc_resample_len(int n, int sr_from, int sr_to) {
+  if (n <= 0 || sr_from <= 0 || sr_to <= 0) return 0;
+  const int g = gcd_int(sr_from, sr_to);
+  const long up = sr_to / g, down = sr_from / g, t = (long)n * up;
+  return (int)(t / down + (t % down != 0));
+}
+int orc_resample(const float* x, int n, int sr_from, int sr_to, float* y) {
+  const int n_out = orc_resample_len(n, sr_from, sr_to);
+  if (n_out <= 0) return 0;
+  const int g = gcd_int(sr_from, sr_to), up = sr_to / g, down = sr_from / g;
+  if (up == 1 && down == 1) { memcpy(y, x, sizeof(float) * (size_t)n); return n; }
+  const int mr = up > down ? up : down, half = 10 * mr, L = 2 * half + 1;
+  double* hd = (double*)malloc(sizeof(double) * (size_t)L);
+  float* h = (float*)malloc(sizeof(float) * (size_t)L);
+  const double fc = 1.0 / mr, alpha = 0.5 * (L - 1), i0b = bessel_i0(5.0);
+  double s = 0.0;
+  for (int i = 0; i < L; ++i) {
+    const double mm = i - alpha, v = fc * mm, r = (i - alpha) / alpha;
+    const double sinc = v == 0.0 ? 1.0 : sin(M_PI * v) / (M_PI * v);
+    hd[i] = fc * sinc * (bessel_i0(5.0 * sqrt(fmax(0.0, 1.0 - r * r))) / i0b);
+    s += hd[i];
+  }
+  for (int i = 0; i < L; ++i) h[i] = (float)(hd[i] / s) * (float)up;
+  for (int m = 0; m < n_out; ++m) {
+    const long a = (long)m * down + half;
+    long jhi = a / up;
+    if (jhi > n - 1) jhi = n - 1;
+    const long lo = a - (L - 1);
+    const long jlo = lo <= 0 ? 0 : (lo + up - 1) / up;
+    double acc = 0.0;
+    for (long j = jlo; j <= jhi; ++j) acc += (double)x[j] * (double)h[a - j * up];
+    y[m] = (float)acc;
+  }
+  free(hd);
+  free(h);
+  return n_out;
 }
 
 /* ---------------- CPU baseline driver ---------------- */

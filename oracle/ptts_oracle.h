@@ -55,6 +55,17 @@ void orc_mimi_decode(const orc_model* m, orc_state* s, const float* latent, floa
 void orc_encode(const orc_model* m, const float* pcm, int n, float* cond,
                 float* after_encoder, float* after_encoder_tr, float* latent);
 
+/* Same, with the Rust driver's chunking (tts_model.rs:520-541): chunk_frames frames per
+ * encode_to_latent call, each with step=0 (replicate padding re-applied per chunk);
+ * chunk_frames <= 0: one pass. */
+void orc_encode_ex(const orc_model* m, const float* pcm, int n, int chunk_frames, float* cond,
+                   float* after_encoder, float* after_encoder_tr, float* latent);
+
+/* scipy resample_poly rule (audio_utils.py:8-28): output length, and the resampled signal
+ * (returns its length). */
+int orc_resample_len(int n, int sr_from, int sr_to);
+int orc_resample(const float* x, int n, int sr_from, int sr_to, float* y);
+
 /* Time-embedding table for lsd_steps (mlp.rs:296-319): out [lsd_steps x 512]. */
 void orc_time_embeddings(const orc_model* m, int lsd_steps, float* out);
 

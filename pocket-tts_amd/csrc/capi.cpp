@@ -91,6 +91,25 @@ int ptts_voice_from_pcm(ptts_engine* e, const float* pcm, int n_samples, ptts_vo
   });
 }
 
+int ptts_voice_from_audio(ptts_engine* e, const float* samples, int n_samples, int sample_rate, int chunk_frames,
+                          ptts_voice** out) {
+  return guard([&] {
+    if (!out) throw ptts::Error(PTTS_ERR_INVALID, "null out");
+    *out = eng(e).voice_from_audio(samples, n_samples, sample_rate, chunk_frames);
+  });
+}
+
+int ptts_resample_len(int n_samples, int sr_from, int sr_to) {
+  if (n_samples <= 0 || sr_from <= 0 || sr_to <= 0) return 0;
+  const ptts::ResamplePlan p = ptts::resample_plan(sr_from, sr_to);
+  const long n = p.out_len(n_samples);
+  return n < (1L << 30) ? (int)n : 0;
+}
+
+int ptts_resample(ptts_engine* e, const float* x, int n_samples, int sr_from, int sr_to, float* y) {
+  return guard([&] { eng(e).resample_host(x, n_samples, sr_from, sr_to, y); });
+}
+
 int ptts_voice_len(const ptts_voice* v) { return v ? v->F : 0; }
 
 int ptts_voice_conditioning(const ptts_voice* v, float* out, int max_rows) {

@@ -908,14 +908,65 @@ void Engine::encoder_transformer(std::vector<Op>& ops, float* x, int T, float* h
   }
 }
 
-// Mimi encoder + speaker projection (tts_model.rs:504-553, mimi.rs:113-141), then prompt prefill.
-ptts_voice* Engine::voice_from_pcm(const float* pcm, int n) {
+namespace {
+// adaptive_voice_prompt_chunk_frames (tts_model.rs:562-577); override > 0 wins, < 0 = one pass.
+int voice_chunk_frames(int F, int override_frames) {
+  if (override_frames > 0) return override_frames;
+  if (override_frames < 0 || F <= 120) return std::max(F, 1);
+  if (F <= 600) return 120;
+  if (F <= 1800) return 180;
+  return 240;
+}
+}  // namespace
+
+// The GPU resampler on its own (test hook of the voice front end).
+void Engine::resample_host(const float* x, int n, int sr_from, int sr_to, float* y) {
+  PTTS_REQUIRE(x && y && n >= 1, "empty input");
+  PTTS_REQUIRE(sr_from > 0 && sr_to > 0, "sample rates must be positive");
+  const ResamplePlan rp = resample_plan(sr_from, sr_to);
+  const long n_out = rp.out_len(n);
+  PTTS_REQUIRE(rp.L <= (1 << 22) && n_out < (1L << 30), "resampling ratio or length too large");
+  sync();
+  const std::vector<float> taps = resample_taps(rp);
+  float *dx = nullptr, *dh = nullptr, *dy = nullptr;
+  try {
+    PTTS_HIP(hipMalloc(&dx, sizeof(float) * n));
+    PTTS_HIP(hipMalloc(&dh, sizeof(float) * taps.size()));
+    PTTS_HIP(hipMalloc(&dy, sizeof(float) * n_out));
+    PTTS_HIP(hipMemcpyAsync(dx, x, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(dh, taps.data(), sizeof(float) * taps.size(), hipMemcpyHostToDevice, stream_));
+    resample(dx, n, dh, rp, (int)n_out, (int)n_out, dy, stream_);
+    PTTS_HIP(hipGetLastError());
+    PTTS_HIP(hipMemcpyAsync(y, dy, sizeof(float) * n_out, hipMemcpyDeviceToHost, stream_));
+    PTTS_HIP(hipStreamSynchronize(stream_));
+  } catch (...) {
+    (void)hipStreamSynchronize(stream_);
+    (void)hipFree(dx), (void)hipFree(dh), (void)hipFree(dy);
+    throw;
+  }
+  (void)hipFree(dx), (void)hipFree(dh), (void)hipFree(dy);
+}
+
+// Voice cloning (tts_model.rs:428-577): samples at `sr` -> resampled to 24 kHz on the GPU
+// (resample_poly rule, kernels.h) -> zero-padded to whole frames (tts_model.rs:515-527) -> Mimi
+// encoder (mimi.rs:113-141) -> speaker projection (:543-553) -> FlowLM prompt prefill (:580-599).
+// The reference encodes chunk by chunk (adaptive chunk length, :530-541) with step=0 for every
+// chunk: the streaming convs and the encoder transformer carry their state, which equals the
+// single pass below, but ConvDownsample1d re-applies its replicate padding at each chunk's first
+// frame (conv.rs:116-123); the downsample conv is therefore run per chunk.
+ptts_voice* Engine::voice_from_audio(const float* pcm_in, int n_in, int sr, int chunk_frames) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
-  PTTS_REQUIRE(pcm != nullptr && n >= 1, "empty PCM");
+  PTTS_REQUIRE(pcm_in != nullptr && n_in >= 1, "empty PCM");
+  PTTS_REQUIRE(sr > 0, "sample rate must be positive");
+  const ResamplePlan rp = resample_plan(sr, PTTS_SAMPLE_RATE);
+  const long n_long = rp.identity() ? n_in : rp.out_len(n_in);
+  PTTS_REQUIRE(n_long >= 1 && n_long < (1L << 28) && rp.L <= (1 << 22), "voice prompt length or rate out of range");
+  const int n = (int)n_long;
   sync();
   const int Np = (n + FRAME - 1) / FRAME * FRAME;  // zero-pad to whole frames (mimi.py:103)
   const int F = Np / FRAME, Te = Np / 120;
   PTTS_REQUIRE(F < max_ctx_, "voice prompt longer than max_ctx");
+  const int cf = voice_chunk_frames(F, chunk_frames);
   std::vector<void*> tmp;
   auto talloc = [&](size_t cnt) {
     void* p = nullptr;
@@ -930,9 +981,20 @@ ptts_voice* Engine::voice_from_pcm(const float* pcm, int n) {
     float* Bf = talloc((size_t)Np * 64);
     float* V = talloc((size_t)Np * 32);
     float* zeros = talloc(16 * 512);
-    PTTS_HIP(hipMemsetAsync(dpcm, 0, sizeof(float) * Np, stream_));
     PTTS_HIP(hipMemsetAsync(zeros, 0, sizeof(float) * 16 * 512, stream_));
-    PTTS_HIP(hipMemcpyAsync(dpcm, pcm, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+    std::vector<float> taps;  // host copy must outlive the async upload
+    if (rp.identity()) {
+      PTTS_HIP(hipMemsetAsync(dpcm, 0, sizeof(float) * Np, stream_));
+      PTTS_HIP(hipMemcpyAsync(dpcm, pcm_in, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+    } else {  // resample straight into the frame-padded encoder input (zeros past n)
+      taps = resample_taps(rp);
+      float* dx = talloc(n_in);
+      float* dh = talloc(taps.size());
+      PTTS_HIP(hipMemcpyAsync(dx, pcm_in, sizeof(float) * n_in, hipMemcpyHostToDevice, stream_));
+      PTTS_HIP(hipMemcpyAsync(dh, taps.data(), sizeof(float) * taps.size(), hipMemcpyHostToDevice, stream_));
+      resample(dx, n_in, dh, rp, n, Np, dpcm, stream_);
+      PTTS_HIP(hipGetLastError());
+    }
     std::vector<Op> ops;
     {
       const float *w = W(L_.ec0_w), *b = W(L_.ec0_b);
@@ -960,12 +1022,24 @@ ptts_voice* Engine::voice_from_pcm(const float* pcm, int n) {
     float* u = talloc((size_t)Te * MFF);
     float* ring = talloc((size_t)MNL * 2 * MNH * Te * 64);
     encoder_transformer(ops, Bf, Te, h, qkv, q, o, u, ring);
-    // ConvDownsample1d k32 s16, replicate padding of the first frame (conv.rs:116-123)
-    float* Hd = talloc(16 * 512);
-    ops.push_back({"enc.replicate", [=](hipStream_t s) { copy2d(Bf, 0, Hd, 512, 16, 512, s); }});
+    // ConvDownsample1d k32 s16 per chunk of cf frames, each with the replicate padding of its first
+    // frame (conv.rs:116-123): full chunks run as one batched implicit GEMM (chunk = batch row,
+    // history = that chunk's replicated first row), a shorter last chunk as a second launch.
+    const int nfull = F / cf, rem = F - nfull * cf, nch = nfull + (rem ? 1 : 0);
+    float* Hd = talloc((size_t)nch * 16 * 512);
+    for (int c = 0; c < nch; ++c) {
+      const float* src = Bf + (size_t)c * cf * 16 * 512;
+      float* dst = Hd + (size_t)c * 16 * 512;
+      ops.push_back({"enc.replicate", [=](hipStream_t s) { copy2d(src, 0, dst, 512, 16, 512, s); }});
+    }
     float* lat = talloc((size_t)F * 512);
-    conv_op(ops, "enc.downsample", Bf, 1, Te, 512, Hd, 16, 16, 0, W(L_.down_w), 512, 32, 1, nullptr, nullptr, lat, F,
-            1);
+    if (nfull)
+      conv_op(ops, "enc.downsample", Bf, nfull, cf * 16, 512, Hd, 16, 16, 0, W(L_.down_w), 512, 32, 1, nullptr,
+              nullptr, lat, cf, 1);
+    if (rem)
+      conv_op(ops, "enc.downsample", Bf + (size_t)nfull * cf * 16 * 512, 1, rem * 16, 512,
+              Hd + (size_t)nfull * 16 * 512, 16, 16, 0, W(L_.down_w), 512, 32, 1, nullptr, nullptr,
+              lat + (size_t)nfull * cf * 512, rem, 1);
     float* cond = talloc((size_t)F * D);
     dense_op(ops, "enc.speaker_proj", lat, F, W(L_.speaker_proj), D, MD, nullptr, ACT_NONE, nullptr, nullptr, cond);
     run_ops(ops);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace ptts {
 
@@ -226,5 +227,20 @@ void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, co
 // the 6-sample zero history (constant padding, conv.py:90-108).
 void conv_cin1(const float* X, int T, int cout, int k, const float* w, const float* bias, float* Y,
                hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// Voice-prompt resampler: the polyphase FIR of scipy.signal.resample_poly (the Python reference's
+// convert_audio, data/audio_utils.py:8-28; audio.rs:197-255 claims the same for Rust). Rates
+// reduce by their gcd to up/down; taps h[0, L) with L = 2*half + 1, half = 10*max(up, down);
+// y[m] = sum_j x[j] * h[m*down + half - j*up] for m < n_out, zeros for n_out <= m < n_pad.
+struct ResamplePlan {
+  int up = 1, down = 1, half = 0, L = 1;
+  bool identity() const { return up == 1 && down == 1; }
+  long out_len(long n) const { return (n * up + down - 1) / down; }
+};
+ResamplePlan resample_plan(int sr_from, int sr_to);
+std::vector<float> resample_taps(const ResamplePlan& p);  // host FIR design (f32 taps x up)
+void resample(const float* x, int n_in, const float* taps, const ResamplePlan& p, int n_out, int n_pad, float* y,
+              hipStream_t s);
 
 }  // namespace ptts

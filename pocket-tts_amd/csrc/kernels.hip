@@ -1837,4 +1837,90 @@ void conv_cin1(const float* X, int T, int cout, int k, const float* w, const flo
   hipLaunchKernelGGL(k_conv_cin1, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, X, T, cout, k, w, bias, Y);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Polyphase resampler (see kernels.h). One lane per output sample: lanes of a wave walk
+// consecutive outputs, so their input windows overlap and the x reads coalesce in L1/L2; the
+// taps (L floats, <= 64 KB) are staged once per workgroup in LDS. Each output touches only the
+// ~L/up taps of its phase, accumulated in f64 (scipy's f32 upfirdn differs by f32 rounding only).
+__global__ __launch_bounds__(256) void k_resample(const float* __restrict__ x, int n_in,
+                                                  const float* __restrict__ taps, int L, int up, int down,
+                                                  int half, int n_out, int n_pad, int use_lds, float* y) {
+  extern __shared__ float sh_taps[];
+  if (use_lds) {
+    for (int i = threadIdx.x; i < L; i += blockDim.x) sh_taps[i] = taps[i];
+    __syncthreads();
+  }
+  const float* h = use_lds ? sh_taps : taps;
+  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n_pad) return;
+  if (m >= n_out) {
+    y[m] = 0.f;
+    return;
+  }
+  const long a = m * down + half;  // h index of x[0]; x[j] pairs with h[a - j*up]
+  const long jhi = min(a / up, (long)n_in - 1);
+  const long lo = a - (L - 1);
+  const long jlo = lo <= 0 ? 0 : (lo + up - 1) / up;
+  double acc = 0.0;
+  for (long j = jlo; j <= jhi; ++j) acc += (double)x[j] * (double)h[a - j * up];
+  y[m] = (float)acc;
+}
+
+namespace {
+int gcd_int(int a, int b) {
+  while (b) {
+    const int t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+double bessel_i0(double x) {  // power series; converges in a few dozen terms for beta = 5
+  double s = 1.0, t = 1.0;
+  const double q = 0.25 * x * x;
+  for (int k = 1; k < 500; ++k) {
+    t *= q / ((double)k * k);
+    s += t;
+    if (t < 1e-17 * s) break;
+  }
+  return s;
+}
+}  // namespace
+
+ResamplePlan resample_plan(int sr_from, int sr_to) {
+  ResamplePlan p;
+  const int g = gcd_int(sr_from, sr_to);
+  p.up = sr_to / g;
+  p.down = sr_from / g;
+  p.half = 10 * std::max(p.up, p.down);  // resample_poly: half_len = 10 * max_rate
+  p.L = 2 * p.half + 1;
+  return p;
+}
+
+// firwin(L, 1/max_rate, window=("kaiser", 5.0)): windowed sinc normalised to unit DC gain,
+// then cast to f32 and multiplied by `up` in f32, as resample_poly does for f32 input.
+std::vector<float> resample_taps(const ResamplePlan& p) {
+  std::vector<double> hd(p.L);
+  const double fc = 1.0 / std::max(p.up, p.down), alpha = 0.5 * (p.L - 1), i0b = bessel_i0(5.0);
+  double sum = 0.0;
+  for (int i = 0; i < p.L; ++i) {
+    const double v = fc * (i - alpha), r = (i - alpha) / alpha;
+    const double sinc = v == 0.0 ? 1.0 : std::sin(M_PI * v) / (M_PI * v);
+    hd[i] = fc * sinc * (bessel_i0(5.0 * std::sqrt(std::max(0.0, 1.0 - r * r))) / i0b);
+    sum += hd[i];
+  }
+  std::vector<float> h(p.L);
+  for (int i = 0; i < p.L; ++i) h[i] = (float)(hd[i] / sum) * (float)p.up;
+  return h;
+}
+
+void resample(const float* x, int n_in, const float* taps, const ResamplePlan& p, int n_out, int n_pad, float* y,
+              hipStream_t s) {
+  if (n_pad <= 0) return;
+  const int use_lds = p.L <= 16384 ? 1 : 0;
+  const size_t lds = use_lds ? sizeof(float) * (size_t)p.L : 0;
+  hipLaunchKernelGGL(k_resample, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), lds, s, x, n_in, taps, p.L, p.up,
+                     p.down, p.half, n_out, n_pad, use_lds, y);
+}
+
 }  // namespace ptts

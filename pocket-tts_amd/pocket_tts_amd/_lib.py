@@ -57,6 +57,9 @@ SIGNATURES = [
     ("ptts_engine_weight_blob", C.c_void_p, [C.c_void_p]),
     ("ptts_voice_from_prompt", C.c_int, [C.c_void_p, F32P, C.c_int, C.POINTER(C.c_void_p)]),
     ("ptts_voice_from_pcm", C.c_int, [C.c_void_p, F32P, C.c_int, C.POINTER(C.c_void_p)]),
+    ("ptts_voice_from_audio", C.c_int, [C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    ("ptts_resample_len", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("ptts_resample", C.c_int, [C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, F32P]),
     ("ptts_voice_len", C.c_int, [C.c_void_p]),
     ("ptts_voice_conditioning", C.c_int, [C.c_void_p, F32P, C.c_int]),
     ("ptts_voice_destroy", None, [C.c_void_p]),

@@ -123,6 +123,22 @@ class Engine:
         check(lib().ptts_voice_from_pcm(self.handle, fptr(x), x.size, C.byref(h)))
         return Voice(self, h.value)
 
+    def voice_from_audio(self, samples: np.ndarray, sample_rate: int, chunk_frames: int = 0) -> Voice:
+        """Mono samples at any rate -> GPU resample to 24 kHz -> chunked Mimi encode -> voice.
+        chunk_frames: 0 = the reference's adaptive rule, > 0 = that many frames, < 0 = one pass."""
+        x = np.ascontiguousarray(samples, np.float32).reshape(-1)
+        h = C.c_void_p()
+        check(lib().ptts_voice_from_audio(self.handle, fptr(x), x.size, int(sample_rate), int(chunk_frames),
+                                          C.byref(h)))
+        return Voice(self, h.value)
+
+    def resample(self, x: np.ndarray, sr_from: int, sr_to: int = 24000) -> np.ndarray:
+        """The GPU resampler on its own (ptts_resample)."""
+        x = np.ascontiguousarray(x, np.float32).reshape(-1)
+        y = np.zeros(max(lib().ptts_resample_len(x.size, sr_from, sr_to), 1), np.float32)
+        check(lib().ptts_resample(self.handle, fptr(x), x.size, int(sr_from), int(sr_to), fptr(y)))
+        return y[:lib().ptts_resample_len(x.size, sr_from, sr_to)]
+
     # -- slots
     def open(self, slot: int, voice: Voice, ids, params: GenerationParams):
         a = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1))

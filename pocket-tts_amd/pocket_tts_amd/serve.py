@@ -39,25 +39,14 @@ from typing import Callable, Iterator, Sequence
 import numpy as np
 
 from ._lib import FRAME, SAMPLE_RATE
+from .audio import pcm_i16_le_bytes, wav_bytes  # noqa: F401 (re-exported wire formats)
 from .engine import GenerationParams, Voice
 from .tts_model import estimate_frames_after_eos, max_gen_len, prepare_text_prompt
 
 VERSION = "0.1.0"
 
 
-# ---------------------------------------------------------------------------------------------
-# wire formats (audio.rs:110-185)
-def pcm_i16_le_bytes(samples: np.ndarray) -> bytes:
-    x = np.clip(np.asarray(samples, np.float32).reshape(-1), -1.0, 1.0) * 32767.0
-    return x.astype(np.int16).astype("<i2").tobytes()  # float -> int cast truncates toward zero
-
-
-def wav_bytes(samples: np.ndarray, sample_rate: int = SAMPLE_RATE) -> bytes:
-    data = pcm_i16_le_bytes(samples)
-    hdr = b"RIFF" + struct.pack("<I", 36 + len(data)) + b"WAVE"
-    hdr += b"fmt " + struct.pack("<IHHIIHH", 16, 1, 1, sample_rate, sample_rate * 2, 2, 16)
-    hdr += b"data" + struct.pack("<I", len(data))
-    return hdr + data
+# wire formats (audio.rs:110-185) live in .audio: pcm_i16_le_bytes, wav_bytes
 
 
 # ---------------------------------------------------------------------------------------------

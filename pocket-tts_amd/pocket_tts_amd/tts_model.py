@@ -12,12 +12,12 @@ tokenizer and sentence splitting are the next row of the build (SURVEY.md §8f f
 
 from __future__ import annotations
 
-import wave
 from typing import Callable, Iterator, Sequence
 
 import numpy as np
 
 from ._lib import FRAME, SAMPLE_RATE
+from .audio import read_wav, read_wav_from_bytes
 from .engine import Engine, GenerationParams, Voice
 
 DEFAULT_VARIANT = "b6369a24"
@@ -49,21 +49,12 @@ def max_gen_len(prepared_text: str) -> int:
     return (len(prepared_text.split()) + 2) * 13
 
 
-def read_wav_mono(path: str) -> np.ndarray:
-    """16-bit PCM WAV -> mono float32 at 24 kHz (audio.rs:12-108: channel mean, /32768; the
-    resampler is scipy's polyphase resample_poly where the reference uses rubato)."""
-    with wave.open(str(path), "rb") as w:
-        sr, ch, sw, n = w.getframerate(), w.getnchannels(), w.getsampwidth(), w.getnframes()
-        raw = w.readframes(n)
-    if sw != 2:
-        raise ValueError("only 16-bit PCM WAV is supported")
-    x = np.frombuffer(raw, np.int16).astype(np.float32).reshape(-1, ch).mean(axis=1) / 32768.0
-    if sr != SAMPLE_RATE:
-        from scipy.signal import resample_poly
-
-        g = np.gcd(sr, SAMPLE_RATE)
-        x = resample_poly(x, SAMPLE_RATE // g, sr // g).astype(np.float32)
-    return x.astype(np.float32)
+def _mono(audio: np.ndarray) -> np.ndarray:
+    """[channels, n] -> [n]. The reference's Mimi encoder has one input channel, so a multi-channel
+    prompt is an error there too (get_voice_state_from_tensor on [1, C, T])."""
+    if audio.shape[0] != 1:
+        raise ValueError(f"voice prompt must be mono, got {audio.shape[0]} channels")
+    return audio[0]
 
 
 class TTSModel:
@@ -76,6 +67,7 @@ class TTSModel:
         self.noise_clamp = noise_clamp
         self.sample_rate = SAMPLE_RATE
         self.tokenizer = tokenizer
+        self.voice_prompt_chunk_frames: int | None = None  # tts_model.rs:417 (None = adaptive rule)
         self._seed = 0
 
     @classmethod
@@ -97,11 +89,38 @@ class TTSModel:
     def get_voice_state_from_prompt_tensor(self, prompt: np.ndarray) -> Voice:
         return self.engine.voice_from_prompt(np.asarray(prompt, np.float32).reshape(-1, 1024))
 
-    def get_voice_state_from_tensor(self, audio: np.ndarray) -> Voice:
-        return self.engine.voice_from_pcm(np.asarray(audio, np.float32).reshape(-1))
+    def get_voice_state_from_tensor(self, audio: np.ndarray, sample_rate: int = SAMPLE_RATE) -> Voice:
+        """tts_model.rs:504-577 (24 kHz mono PCM); other rates are resampled on the GPU first."""
+        return self.engine.voice_from_audio(np.asarray(audio, np.float32).reshape(-1), sample_rate,
+                                            self.voice_prompt_chunk_frames or 0)
+
+    def get_voice_state_from_bytes(self, data: bytes) -> Voice:
+        """tts_model.rs:428-444: WAV bytes -> (GPU) resample -> encode -> prompt prefill."""
+        audio, sr = read_wav_from_bytes(data)
+        return self.get_voice_state_from_tensor(_mono(audio), sr)
 
     def get_voice_state(self, path: str) -> Voice:
-        return self.get_voice_state_from_tensor(read_wav_mono(path))
+        """tts_model.rs:446-463."""
+        audio, sr = read_wav(path)
+        return self.get_voice_state_from_tensor(_mono(audio), sr)
+
+    def get_voice_state_from_prompt_file(self, path: str) -> Voice:
+        """tts_model.rs:465-477: a safetensors file holding `audio_prompt` [1, F, 1024]."""
+        from safetensors.numpy import load_file
+
+        t = load_file(str(path))
+        if "audio_prompt" not in t:
+            raise KeyError("'audio_prompt' not found in safetensors file")
+        return self.get_voice_state_from_prompt_tensor(t["audio_prompt"])
+
+    def get_voice_state_from_prompt_bytes(self, data: bytes) -> Voice:
+        """tts_model.rs:479-487."""
+        from safetensors.numpy import load
+
+        t = load(data)
+        if "audio_prompt" not in t:
+            raise KeyError("'audio_prompt' not found in safetensors bytes")
+        return self.get_voice_state_from_prompt_tensor(t["audio_prompt"])
 
     # ---- generation
     def _ids(self, text_or_ids) -> tuple[np.ndarray, int, int]:

@@ -33,6 +33,9 @@ def lib() -> C.CDLL:
         L.orc_step.argtypes = [C.c_void_p, C.c_void_p, F32P, F32P, C.c_int] + [F32P] * 7
         L.orc_mimi_decode.argtypes = [C.c_void_p, C.c_void_p, F32P, F32P]
         L.orc_encode.argtypes = [C.c_void_p, F32P, C.c_int, F32P, F32P, F32P, F32P]
+        L.orc_encode_ex.argtypes = [C.c_void_p, F32P, C.c_int, C.c_int, F32P, F32P, F32P, F32P]
+        L.orc_resample_len.argtypes = [C.c_int, C.c_int, C.c_int]
+        L.orc_resample.argtypes = [F32P, C.c_int, C.c_int, C.c_int, F32P]
         L.orc_time_embeddings.argtypes = [C.c_void_p, C.c_int, F32P]
         L.orc_bench.restype = C.c_double
         L.orc_bench.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
@@ -74,7 +77,8 @@ class Oracle:
         self.L.orc_time_embeddings(self.m, n, fp(out))
         return out
 
-    def encode(self, pcm: np.ndarray):
+    def encode(self, pcm: np.ndarray, chunk_frames: int = -1):
+        """chunk_frames <= 0: one pass (Python reference); else the Rust chunked encode."""
         pcm = np.ascontiguousarray(pcm, np.float32)
         F = pcm.size // 1920
         T = pcm.size // 120
@@ -82,11 +86,20 @@ class Oracle:
         enc = np.zeros((T, 512), np.float32)
         tr = np.zeros((T, 512), np.float32)
         lat = np.zeros((F, 512), np.float32)
-        self.L.orc_encode(self.m, fp(pcm), pcm.size, fp(cond), fp(enc), fp(tr), fp(lat))
+        self.L.orc_encode_ex(self.m, fp(pcm), pcm.size, chunk_frames, fp(cond), fp(enc), fp(tr), fp(lat))
         return cond, enc, tr, lat
 
     def bench(self, n_utt, F, S, n_frames, threads):
         return self.L.orc_bench(self.m, n_utt, F, S, n_frames, threads)
+
+
+def resample(x: np.ndarray, sr_from: int, sr_to: int = 24000) -> np.ndarray:
+    """The oracle's restatement of the reference resampler (scipy resample_poly rule)."""
+    L = lib()
+    x = np.ascontiguousarray(x, np.float32).reshape(-1)
+    y = np.zeros(max(L.orc_resample_len(x.size, sr_from, sr_to), 1), np.float32)
+    n = L.orc_resample(fp(x), x.size, sr_from, sr_to, fp(y))
+    return y[:n]
 
 
 class OracleState:

@@ -166,12 +166,80 @@ def run_encoder(torch, mimi, speaker_proj, n_frames, tag):
             "meta": np.array([SEED, n_frames], np.int64)}
 
 
+def run_encoder_chunked(torch, mimi, speaker_proj, n_frames, chunk_frames, tag):
+    """The Rust voice encode (tts_model.rs:520-541): PCM cut into chunks of `chunk_frames` frames,
+    each pushed through `encode_to_latent(chunk, &mut model_state, 0)` with ONE carried state.
+    Every chunk passes step=0, so the replicate-padded ConvDownsample1d re-pads from each chunk's
+    first frame (conv.rs:116-123) instead of using its carried `previous`. Emulated with the
+    reference's own Python streaming modules: one state from `init_states`, and the downsample
+    conv's `first` flag raised before every chunk (conv.py:101-106)."""
+    from pocket_tts.modules.stateful_module import increment_steps, init_states
+
+    pcm = synth.gaussian(4, f"{tag}/pcm", n_frames * 1920, 0.1)
+    with torch.no_grad():
+        state = init_states(mimi, batch_size=1, sequence_length=1000)
+        down_keys = [k for k in state if k.startswith("downsample") and "first" in state[k]]
+        assert down_keys, "downsample conv state not found"
+        lats = []
+        for c0 in range(0, n_frames, chunk_frames):
+            c1 = min(n_frames, c0 + chunk_frames)
+            x = torch.from_numpy(pcm[c0 * 1920:c1 * 1920])[None, None]
+            emb = mimi.encoder(x, model_state=state)
+            (tr,) = mimi.encoder_transformer(emb, state)
+            for k in down_keys:
+                state[k]["first"][:] = True
+            lats.append(mimi.downsample(tr, model_state=state))
+            increment_steps(mimi, state, increment=tr.shape[-1])
+        lat = torch.cat(lats, dim=-1)
+        cond = torch.nn.functional.linear(lat.transpose(-1, -2), speaker_proj)
+        # one-pass encode of the same PCM (tts_model.py:258-262), for the quirk's size
+        one = mimi._to_framerate(mimi.encoder_transformer(mimi.encoder(torch.from_numpy(pcm)[None, None], None),
+                                                          None)[0])
+    return {"pcm": pcm, "latent": lat[0].numpy(), "conditioning": cond[0].numpy(),
+            "latent_one_pass": one[0].numpy(), "meta": np.array([SEED, n_frames, chunk_frames], np.int64)}
+
+
+def run_resample(torch, tag):
+    """The Python reference's resampler, `convert_audio` (data/audio_utils.py:8-28, scipy
+    resample_poly with the default Kaiser(5.0) FIR), on synthetic mono signals."""
+    from pocket_tts.data.audio_utils import convert_audio
+
+    out = {}
+    for i, (sr, n) in enumerate(((48000, 12345), (44100, 8821), (16000, 4000), (22050, 5001), (8000, 1))):
+        t = np.arange(n) / sr
+        x = (0.5 * np.sin(2 * np.pi * 440.0 * t) + 0.3 * synth.gaussian(5 + i, f"{tag}/{sr}", n, 0.3)).astype(np.float32)
+        y = convert_audio(torch.from_numpy(x)[None], sr, 24000, 1)[0].numpy()
+        out[f"x_{sr}"] = x
+        out[f"y_{sr}"] = np.ascontiguousarray(y, np.float32)
+    # The reference's own real-data pair (its test_input_parity, parity_tests.rs:379-433):
+    # assets/ref.wav (48 kHz s16 mono) and assets/ref_mimi_input.safetensors (its convert_audio
+    # output, zero-padded to whole frames). Output sample m reads input samples <= 2m + 20, so the
+    # head below is exact: the first 0.5 s of output and the input samples it depends on.
+    import wave
+
+    with wave.open(str(REF.parent / "assets" / "ref.wav"), "rb") as w:
+        raw = np.frombuffer(w.readframes(w.getnframes()), np.int16)
+    from safetensors.numpy import load_file
+
+    mimi_input = load_file(str(REF.parent / "assets" / "ref_mimi_input.safetensors"))["mimi_input"].reshape(-1)
+    out["refwav_head_i16"] = np.ascontiguousarray(raw[:24064])
+    out["ref_mimi_input_head"] = np.ascontiguousarray(mimi_input[:12000], np.float32)
+    out["ref_lengths"] = np.array([raw.size, mimi_input.size], np.int64)
+    return out
+
+
 def main():
     torch = _import_reference()
     torch.set_num_threads(8)
     from safetensors.numpy import save_file
 
     flm, mimi, speaker_proj = build_models(torch)
+    if len(sys.argv) > 1 and sys.argv[1] == "voice":  # only the voice-cloning front-end fixtures
+        fx = run_encoder_chunked(torch, mimi, speaker_proj, n_frames=5, chunk_frames=2, tag="encc5")
+        save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / "encoder_chunked_5f.safetensors"))
+        save_file(run_resample(torch, "resample"), str(HERE / "resample.safetensors"))
+        print("voice fixtures written to", HERE)
+        return
     fx = run_e2e(torch, flm, mimi, F=20, S=10, N=12, lsd_steps=1, tag="e2e_lsd1")
     save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / "e2e_lsd1.safetensors"))
     fx = run_e2e(torch, flm, mimi, F=8, S=6, N=4, lsd_steps=2, tag="e2e_lsd2")

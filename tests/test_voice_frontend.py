@@ -1,0 +1,233 @@
+"""Voice-cloning front end: WAV I/O, the resampler, the chunked
+encoder and the whole WAV -> voice path.
+
+Pinning:
+  * resampler: the reference's own real-data pair, assets/ref.wav -> assets/ref_mimi_input
+    (test_input_parity, parity_tests.rs:379-433; the head is committed in
+    tests/golden/resample.safetensors, and the full pair is checked when /root/reference is
+    present), plus synthetic signals through the Python reference's convert_audio at 5 rates;
+  * chunked encode: the reference's Python streaming modules driven the way the Rust driver
+    chunks (gen_golden.py:run_encoder_chunked).
+Tolerances: resampler 1e-6 abs (f64 accumulation here vs scipy's f32 upfirdn); encoder
+conditioning 1e-5 abs (fp32, reduction order only)."""
+
+import struct
+from pathlib import Path
+
+import numpy as np
+import pytest
+from conftest import load_golden
+
+REF_ASSETS = Path("/root/reference/assets")
+RATES = (48000, 44100, 16000, 22050, 8000)
+
+
+# ------------------------------------------------------------------ WAV I/O (audio.rs:12-185)
+def test_pcm_i16_interleave_and_clamp():
+    """audio.rs test_pcm_i16_le_bytes_clamp_and_interleave (audio.rs:242-259)."""
+    from pocket_tts_amd.audio import pcm_i16_le_bytes
+
+    t = np.array([[-1.0, 0.0, 1.0], [0.5, -0.5, 2.0]], np.float32)
+    got = np.frombuffer(pcm_i16_le_bytes(t), "<i2").tolist()
+    assert got == [-32767, 16383, 0, -16383, 32767, 32767]
+
+
+def test_normalize_peak():
+    """audio.rs test_normalize_peak (audio.rs:230-239)."""
+    from pocket_tts_amd.audio import normalize_peak
+
+    assert normalize_peak(np.array([[-0.5, 0.2, 0.5]], np.float32)).tolist() == [[-1.0, np.float32(0.4), 1.0]]
+    assert normalize_peak(np.zeros((1, 3), np.float32)).tolist() == [[0.0, 0.0, 0.0]]
+
+
+def test_wav_roundtrip(tmp_path):
+    """audio.rs test_wav_io (audio.rs:289-312): 16-bit write then read within 1e-3."""
+    from pocket_tts_amd.audio import read_wav, write_wav
+
+    t = np.array([[0.0, 0.5, -0.5, 0.1]], np.float32)
+    write_wav(tmp_path / "io.wav", t, 16000)
+    x, sr = read_wav(tmp_path / "io.wav")
+    assert sr == 16000 and x.shape == (1, 4)
+    assert np.abs(x - t).max() < 1e-3
+
+
+def _riff(fmt_tag, ch, sr, bits, payload, extensible=False, declared=None):
+    align = ch * bits // 8
+    if extensible:
+        fmt = struct.pack("<HHIIHH", 0xFFFE, ch, sr, sr * align, align, bits)
+        fmt += struct.pack("<HHI", 22, bits, 0) + struct.pack("<H", fmt_tag) + b"\x00\x00\x00\x00\x10\x00\x80\x00\x00\xaa\x00\x38\x9b\x71"
+    else:
+        fmt = struct.pack("<HHIIHH", fmt_tag, ch, sr, sr * align, align, bits)
+    body = b"fmt " + struct.pack("<I", len(fmt)) + fmt
+    body += b"LIST" + struct.pack("<I", 3) + b"abc\x00"  # odd-sized chunk: word-aligned skip
+    body += b"data" + struct.pack("<I", declared if declared is not None else len(payload)) + payload
+    return b"RIFF" + struct.pack("<I", 4 + len(body)) + b"WAVE" + body
+
+
+@pytest.mark.parametrize("bits", [8, 16, 24, 32])
+def test_read_wav_int_formats(bits):
+    """hound semantics: integer samples / 2^(bits-1), 8-bit stored unsigned; channels
+    de-interleaved to [C, T]."""
+    from pocket_tts_amd.audio import read_wav_from_bytes
+
+    rng = np.random.default_rng(bits)
+    full = 1 << (bits - 1)
+    v = rng.integers(-full, full, size=(5, 2), dtype=np.int64)
+    if bits == 8:
+        payload = (v + 128).astype(np.uint8).tobytes()
+    else:
+        w = bits // 8
+        payload = b"".join(int(s).to_bytes(w, "little", signed=True) for s in v.reshape(-1))
+    for ext in (False, True):
+        x, sr = read_wav_from_bytes(_riff(1, 2, 22050, bits, payload, extensible=ext))
+        assert sr == 22050 and x.shape == (2, 5)
+        np.testing.assert_array_equal(x, (v.T.astype(np.float32) / np.float32(full)))
+
+
+def test_read_wav_float_and_truncated():
+    from pocket_tts_amd.audio import WavError, read_wav_from_bytes
+
+    f = np.array([0.25, -0.75, 1.5], np.float32)
+    x, _ = read_wav_from_bytes(_riff(3, 1, 24000, 32, f.tobytes()))
+    np.testing.assert_array_equal(x[0], f)
+    # data chunk declared longer than the file: the whole samples present are kept (audio.rs:33-49)
+    s16 = np.array([100, -200, 300], "<i2").tobytes() + b"\x01"
+    x, _ = read_wav_from_bytes(_riff(1, 1, 24000, 16, s16, declared=1000))
+    np.testing.assert_array_equal(x[0], np.array([100, -200, 300], np.float32) / 32768.0)
+    with pytest.raises(WavError):
+        read_wav_from_bytes(b"RIFX0000WAVE")
+    with pytest.raises(WavError):
+        read_wav_from_bytes(_riff(2, 1, 24000, 16, s16))  # ADPCM: unsupported
+
+
+def test_read_reference_wav():
+    """The reference's own assets/ref.wav: 48 kHz mono s16, 331,708 samples."""
+    if not (REF_ASSETS / "ref.wav").exists():
+        pytest.skip("reference assets not present")
+    from pocket_tts_amd.audio import read_wav
+
+    x, sr = read_wav(REF_ASSETS / "ref.wav")
+    g = load_golden("resample.safetensors")
+    assert sr == 48000 and x.shape == (1, int(g["ref_lengths"][0]))
+    np.testing.assert_array_equal(x[0, :24064], g["refwav_head_i16"].astype(np.float32) / 32768.0)
+
+
+# ------------------------------------------------------------------ oracle pinning (CPU)
+def test_oracle_resample_matches_reference_convert_audio():
+    from _oracle import resample
+
+    g = load_golden("resample.safetensors")
+    for sr in RATES:
+        y = resample(g[f"x_{sr}"], sr)
+        assert y.shape == g[f"y_{sr}"].shape, sr
+        assert np.abs(y - g[f"y_{sr}"]).max() <= 1e-6, sr
+
+
+def test_oracle_resample_matches_reference_ref_wav_pair():
+    """assets/ref.wav -> assets/ref_mimi_input (the reference's real-data resampler pair)."""
+    from _oracle import resample
+
+    g = load_golden("resample.safetensors")
+    x = g["refwav_head_i16"].astype(np.float32) / 32768.0
+    y = resample(x, 48000)[:12000]
+    assert np.abs(y - g["ref_mimi_input_head"]).max() <= 1e-6
+    if (REF_ASSETS / "ref_mimi_input.safetensors").exists():  # the whole file, when present
+        import wave
+
+        from safetensors.numpy import load_file
+
+        with wave.open(str(REF_ASSETS / "ref.wav"), "rb") as w:
+            xs = np.frombuffer(w.readframes(w.getnframes()), np.int16).astype(np.float32) / 32768.0
+        m = load_file(str(REF_ASSETS / "ref_mimi_input.safetensors"))["mimi_input"].reshape(-1)
+        y = resample(xs, 48000)
+        assert np.abs(y - m[:y.size]).max() <= 1e-6 and not m[y.size:].any()
+        assert m.size == (y.size + 1919) // 1920 * 1920
+
+
+def test_oracle_chunked_encoder_matches_reference():
+    from _oracle import Oracle
+
+    d = load_golden("encoder_chunked_5f.safetensors")
+    o = Oracle(0x5EED)
+    cond, _, _, lat = o.encode(d["pcm"], int(d["meta"][2]))
+    assert np.abs(lat - d["latent"].T).max() <= 1e-5
+    assert np.abs(cond - d["conditioning"]).max() <= 1e-5
+    _, _, _, lat1 = o.encode(d["pcm"], -1)
+    assert np.abs(lat1 - d["latent_one_pass"].T).max() <= 1e-5
+    # the quirk is real: chunk-start frames 2 and 4 differ from the one-pass encode, others do not
+    per_frame = np.abs(d["latent"] - d["latent_one_pass"]).max(axis=0)
+    assert per_frame[[2, 4]].min() > 1e-3 and per_frame[[0, 1, 3]].max() < 1e-6
+
+
+# ------------------------------------------------------------------ GPU (through the C ABI)
+@pytest.mark.gpu
+def test_gpu_resampler_matches_oracle_and_reference(gpu_engine):
+    from _oracle import resample
+
+    g = load_golden("resample.safetensors")
+    for sr in RATES:
+        y = gpu_engine.resample(g[f"x_{sr}"], sr)
+        assert y.shape == g[f"y_{sr}"].shape, sr
+        assert np.abs(y - resample(g[f"x_{sr}"], sr)).max() <= 1e-7, sr
+        assert np.abs(y - g[f"y_{sr}"]).max() <= 1e-6, sr
+    x = g["refwav_head_i16"].astype(np.float32) / 32768.0
+    assert np.abs(gpu_engine.resample(x, 48000)[:12000] - g["ref_mimi_input_head"]).max() <= 1e-6
+    # 10 s at 44.1 kHz (a long, non-trivial ratio: up 80, down 147, 2941 taps)
+    x = (0.3 * np.sin(np.arange(441000) * 0.01)).astype(np.float32)
+    y = gpu_engine.resample(x, 44100)
+    assert y.size == 240000 and np.abs(y - resample(x, 44100)).max() <= 1e-7
+
+
+@pytest.mark.gpu
+def test_gpu_chunked_voice_matches_reference(gpu_engine):
+    d = load_golden("encoder_chunked_5f.safetensors")
+    v = gpu_engine.voice_from_audio(d["pcm"], 24000, int(d["meta"][2]))
+    assert v.n_frames == 5
+    np.testing.assert_allclose(v.conditioning(), d["conditioning"], atol=1e-5)
+    v1 = gpu_engine.voice_from_audio(d["pcm"], 24000, -1)  # one pass = the Python reference
+    e = load_golden("encoder_4f.safetensors")
+    v4 = gpu_engine.voice_from_audio(e["pcm"], 24000, 0)  # adaptive rule: 4 frames -> one chunk
+    np.testing.assert_allclose(v4.conditioning(), e["conditioning"], atol=1e-5)
+    for x in (v, v1, v4):
+        x.close()
+
+
+@pytest.mark.gpu
+def test_gpu_wav_voice_path_matches_oracle(gpu_engine, oracle, tmp_path):
+    """WAV at 48 kHz -> read_wav -> GPU resample + encode, vs oracle resample + chunked encode,
+    then a generation step from that voice on both sides."""
+    import pocket_tts_amd as pt
+    from _oracle import resample
+    from pocket_tts_amd.audio import read_wav, write_wav
+
+    rng = np.random.default_rng(3)
+    x48 = (0.2 * rng.standard_normal(3 * 3840 + 77)).astype(np.float32)
+    write_wav(tmp_path / "v.wav", x48[None], 48000)
+    xr, sr = read_wav(tmp_path / "v.wav")
+    v = gpu_engine.voice_from_audio(xr[0], sr, 2)
+    y = resample(xr[0], sr)
+    pad = np.zeros((y.size + 1919) // 1920 * 1920, np.float32)
+    pad[:y.size] = y
+    cond, _, _, _ = oracle.encode(pad, 2)
+    assert v.n_frames == cond.shape[0] == 4
+    np.testing.assert_allclose(v.conditioning(), cond, atol=1e-5)
+    ids = np.array([260, 2994, 262], np.int32)
+    gpu_engine.open(0, v, ids, pt.GenerationParams(temp=0.0, eos_threshold=float("inf"), max_frames=2))
+    s = oracle.new_state(64)
+    s.prefill(cond)
+    s.prefill_tokens(ids)
+    r = gpu_engine.step(1)
+    ref = s.step(None)
+    np.testing.assert_allclose(r.latents[0], ref["latent"], atol=1e-4)
+    gpu_engine.close_slot(0)
+    v.close()
+
+
+@pytest.mark.gpu
+def test_gpu_voice_errors(gpu_engine):
+    from pocket_tts_amd import PocketTTSError
+
+    with pytest.raises(PocketTTSError):
+        gpu_engine.voice_from_audio(np.zeros(100, np.float32), 0)
+    with pytest.raises(PocketTTSError):
+        gpu_engine.voice_from_audio(np.zeros(1920 * 600, np.float32), 24000)  # > max_ctx frames
