@@ -2,7 +2,10 @@
 
 from ._lib import FRAME, LIB_PATH, SAMPLE_RATE, PocketTTSError, lib
 from .engine import Engine, GenerationParams, StepResult, Voice
-from .tts_model import TTSModel, estimate_frames_after_eos, max_gen_len, prepare_text_prompt
+from .text import (Tokenizer, estimate_frames_after_eos, load_tokenizer, max_gen_len, prepare_text_prompt,
+                   split_into_best_sentences)
+from .tts_model import TTSModel
 
 __all__ = ["Engine", "GenerationParams", "StepResult", "Voice", "TTSModel", "PocketTTSError", "FRAME",
-           "SAMPLE_RATE", "LIB_PATH", "lib", "prepare_text_prompt", "estimate_frames_after_eos", "max_gen_len"]
+           "SAMPLE_RATE", "LIB_PATH", "lib", "prepare_text_prompt", "estimate_frames_after_eos", "max_gen_len",
+           "Tokenizer", "load_tokenizer", "split_into_best_sentences"]

@@ -41,7 +41,7 @@ import numpy as np
 from ._lib import FRAME, SAMPLE_RATE
 from .audio import pcm_i16_le_bytes, wav_bytes  # noqa: F401 (re-exported wire formats)
 from .engine import GenerationParams, Voice
-from .tts_model import estimate_frames_after_eos, max_gen_len, prepare_text_prompt
+from .text import estimate_frames_after_eos, max_gen_len, prepare_text_prompt
 
 VERSION = "0.1.0"
 
@@ -178,15 +178,11 @@ class MultiGpuScheduler:
 
 # ---------------------------------------------------------------------------------------------
 def load_tokenizer(path: str) -> Callable[[str], list[int]]:
-    """SentencePiece-Unigram tokenizer.json with the native Rust settings (text.rs:71-79):
-    Metaspace with prepend "always" and no BOS post-processor."""
-    from tokenizers import Tokenizer, decoders, pre_tokenizers
+    """tokenizer.model (SentencePiece) or tokenizer.json; a .json file is read with the native
+    Rust settings (text.rs:71-79: Metaspace prepend "always", no BOS), see text.py."""
+    from .text import Tokenizer
 
-    tok = Tokenizer.from_file(path)
-    tok.pre_tokenizer = pre_tokenizers.Metaspace(replacement="▁", prepend_scheme="always")
-    tok.decoder = decoders.Metaspace(replacement="▁", prepend_scheme="always")
-    tok.post_processor = None
-    return lambda text: tok.encode(text, add_special_tokens=False).ids
+    return Tokenizer.from_file(path, native=True)
 
 
 class TTSService:

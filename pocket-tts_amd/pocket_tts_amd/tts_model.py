@@ -1,13 +1,20 @@
 """Host-side mirror of the reference's `TTSModel` API (crates/pocket-tts/src/tts_model.rs),
 running the generation hot path through the HIP engine.
 
-Reference surface kept: `TTSModel.load / load_with_params`, public fields `temp`,
-`lsd_decode_steps`, `eos_threshold`, `noise_clamp`, `sample_rate`,
-`get_voice_state_from_prompt_tensor` (:490-501), `get_voice_state_from_tensor` (:504-560),
-`get_voice_state` (:449-463, 24 kHz mono WAV), `generate` (:687-703) and `generate_stream`
-(:894-913, one frame of 1920 samples per item). Text enters as token ids; the SentencePiece
-tokenizer and sentence splitting are the next row of the build, so a
-`tokenizer` callable may be supplied for text input.
+Reference surface kept:
+  * `TTSModel.load / load_with_params`, public fields `temp`, `lsd_decode_steps`,
+    `eos_threshold`, `noise_clamp`, `sample_rate`, `voice_prompt_chunk_frames` (:22-49, :417);
+  * voices: `get_voice_state` (:446-463), `get_voice_state_from_bytes` (:428-444),
+    `get_voice_state_from_tensor` (:504-577), `get_voice_state_from_prompt_file / _bytes /
+    _tensor` (:465-501). WAV decode on the host (audio.py), resampling and the Mimi encoder on
+    the GPU;
+  * generation: `generate` (:687-703), `generate_stream` (:894-913: sentence chunks of at most
+    50 tokens, one segment each from a fresh copy of the voice state), `generate_stream_long`
+    and `generate_with_pauses` (:856-883, 1074-1131: pause markers become silence), one
+    [1, 1, 1920] frame per item; `split_into_best_sentences` (:601-684),
+    `estimate_generation_steps` (:1187-1190).
+Text goes through the text front end (text.py: tokenizer, prompt preparation); token-id input
+is accepted too (one segment, no splitting).
 """
 
 from __future__ import annotations
@@ -19,34 +26,12 @@ import numpy as np
 from ._lib import FRAME, SAMPLE_RATE
 from .audio import read_wav, read_wav_from_bytes
 from .engine import Engine, GenerationParams, Voice
+from .text import (estimate_frames_after_eos, load_tokenizer, long_text_segments, max_gen_len,
+                   prepare_text_prompt, silence_samples, split_into_best_sentences)
 
 DEFAULT_VARIANT = "b6369a24"
 
-
-def prepare_text_prompt(text: str) -> str:
-    """tts_model.rs:1194-1227 (pause markers are not parsed here)."""
-    text = text.strip()
-    if not text:
-        return "."
-    text = text.replace("\n", " ").replace("\r", " ").replace("  ", " ")
-    words = len(text.split())
-    if not text[0].isupper():
-        text = text[0].upper() + text[1:]
-    if text[-1].isalnum():
-        text += "."
-    if words < 5:
-        text = " " * 8 + text
-    return text
-
-
-def estimate_frames_after_eos(text: str) -> int:
-    """tts_model.rs:1230-1237."""
-    return 5 if len(text.split()) <= 4 else 3
-
-
-def max_gen_len(prepared_text: str) -> int:
-    """tts_model.rs:968."""
-    return (len(prepared_text.split()) + 2) * 13
+__all__ = ["TTSModel", "prepare_text_prompt", "estimate_frames_after_eos", "max_gen_len", "DEFAULT_VARIANT"]
 
 
 def _mono(audio: np.ndarray) -> np.ndarray:
@@ -77,10 +62,14 @@ class TTSModel:
     @classmethod
     def load_with_params(cls, variant: str = DEFAULT_VARIANT, temp: float = 0.7, lsd_decode_steps: int = 1,
                          eos_threshold: float = -4.0, noise_clamp: float | None = None, *,
-                         weights_path: str | None = None, seed: int = 0x5EED, device: int = 0,
-                         max_ctx: int = 1024, tokenizer=None) -> "TTSModel":
+                         weights_path: str | None = None, tokenizer_path: str | None = None, seed: int = 0x5EED,
+                         device: int = 0, max_ctx: int = 1024, tokenizer=None) -> "TTSModel":
+        """weights_path: local safetensors with the TTSModel state-dict names (synthetic weights
+        from `seed` when None); tokenizer_path: tokenizer.model (SentencePiece) or tokenizer.json."""
         if variant != DEFAULT_VARIANT:
             raise ValueError(f"unsupported variant {variant!r} (only {DEFAULT_VARIANT})")
+        if tokenizer is None and tokenizer_path:
+            tokenizer = load_tokenizer(tokenizer_path)
         eng = Engine(device=device, max_slots=1, max_ctx=max_ctx, lsd_decode_steps=lsd_decode_steps, seed=seed,
                      weights_path=weights_path)
         return cls(eng, temp, lsd_decode_steps, eos_threshold, noise_clamp, tokenizer)
@@ -122,29 +111,35 @@ class TTSModel:
             raise KeyError("'audio_prompt' not found in safetensors bytes")
         return self.get_voice_state_from_prompt_tensor(t["audio_prompt"])
 
-    # ---- generation
-    def _ids(self, text_or_ids) -> tuple[np.ndarray, int, int]:
-        if isinstance(text_or_ids, str):
-            if self.tokenizer is None:
-                raise ValueError("text input needs a tokenizer callable (TTSModel(..., tokenizer=...)); "
-                                 "or pass token ids")
-            prepared = prepare_text_prompt(text_or_ids)
-            ids = np.asarray(self.tokenizer(prepared), np.int32)
-            return ids, max_gen_len(prepared), estimate_frames_after_eos(text_or_ids)
-        ids = np.asarray(text_or_ids, np.int32).reshape(-1)
-        return ids, (max(1, ids.size // 2) + 2) * 13, 3
+    # ---- text
+    def _tok(self):
+        if self.tokenizer is None:
+            raise ValueError("text input needs a tokenizer (TTSModel.load(..., tokenizer_path=...) or "
+                             "tokenizer=callable); or pass token ids")
+        return self.tokenizer
 
+    def count_tokens(self, text: str) -> int:
+        tok = self._tok()
+        return tok.count_tokens(text) if hasattr(tok, "count_tokens") else len(tok(text))
+
+    def split_into_best_sentences(self, text: str) -> list[str]:
+        return split_into_best_sentences(text, self.count_tokens)
+
+    def estimate_generation_steps(self, text: str) -> int:
+        return max_gen_len(prepare_text_prompt(text))
+
+    # ---- generation
     def _params(self, max_frames: int, frames_after_eos: int) -> GenerationParams:
         self._seed += 1
         return GenerationParams(temp=self.temp, eos_threshold=self.eos_threshold, noise_clamp=self.noise_clamp,
                                 frames_after_eos=frames_after_eos, max_frames=max_frames, seed=self._seed)
 
-    def generate_stream(self, text_or_ids, voice_state: Voice, max_frames: int | None = None) -> Iterator[np.ndarray]:
+    def _segment(self, ids: np.ndarray, voice_state: Voice, max_frames: int, frames_after_eos: int
+                 ) -> Iterator[np.ndarray]:
+        """generate_stream_segment (tts_model.rs:935-1071) on engine row 0."""
         if self.lsd_decode_steps != self.engine.lsd_decode_steps:
             raise ValueError("lsd_decode_steps is fixed at engine creation")
-        ids, mgl, fae = self._ids(text_or_ids)
-        p = self._params(max_frames or mgl, fae)
-        self.engine.open(0, voice_state, ids, p)
+        self.engine.open(0, voice_state, ids, self._params(max_frames, frames_after_eos))
         first = True
         while True:
             r = self.engine.step(1)
@@ -158,8 +153,38 @@ class TTSModel:
             if r.last[0]:
                 return
 
+    def generate_stream(self, text_or_ids, voice_state: Voice, max_frames: int | None = None) -> Iterator[np.ndarray]:
+        """tts_model.rs:894-913. Text: one segment per sentence chunk; max_gen_len and the EOS tail
+        from each chunk (:968-969). Token ids: one segment (max_frames or a length estimate)."""
+        if not isinstance(text_or_ids, str):
+            ids = np.asarray(text_or_ids, np.int32).reshape(-1)
+            yield from self._segment(ids, voice_state, max_frames or (max(1, ids.size // 2) + 2) * 13, 3)
+            return
+        tok = self._tok()
+        for chunk in self.split_into_best_sentences(text_or_ids):
+            prepared = prepare_text_prompt(chunk)
+            ids = np.asarray(tok(prepared), np.int32)
+            yield from self._segment(ids, voice_state, max_frames or max_gen_len(prepared),
+                                     estimate_frames_after_eos(chunk))
+
     def generate(self, text_or_ids, voice_state: Voice, max_frames: int | None = None) -> np.ndarray:
+        """tts_model.rs:687-703: all frames concatenated, [1, N*1920]."""
         frames = list(self.generate_stream(text_or_ids, voice_state, max_frames))
         if not frames:
             raise RuntimeError("No audio generated")
         return np.concatenate(frames, axis=2)[0]
+
+    def generate_stream_long(self, text: str, voice_state: Voice) -> Iterator[np.ndarray]:
+        """tts_model.rs:1074-1131: text segments between pause markers, silence for each pause."""
+        for kind, val in long_text_segments(text):
+            if kind == "text":
+                yield from self.generate_stream(val, voice_state)
+            else:
+                yield np.zeros((1, 1, silence_samples(val, self.sample_rate)), np.float32)
+
+    def generate_with_pauses(self, text: str, voice_state: Voice) -> np.ndarray:
+        """tts_model.rs:856-883."""
+        chunks = list(self.generate_stream_long(text, voice_state))
+        if not chunks:
+            raise RuntimeError("No audio generated")
+        return np.concatenate(chunks, axis=2)[0]
