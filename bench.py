@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--ops-out", default="", help="write per-op timings of the step plan (JSON)")
     ap.add_argument("--no-op-times", action="store_true", help="skip the per-op HIP-event pass (PMC runs)")
+    ap.add_argument("--no-quant-variant", action="store_true",
+                    help="skip the second job on an int8-weight engine (weight_quant = QUANT_FLOW_LM)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sequential stepping (no FlowLM / Mimi overlap across consecutive frames)")
     args = ap.parse_args()
@@ -127,19 +129,6 @@ def main():
         if rank != 0:
             eng.finalize()
 
-    voice = eng.voice_from_prompt(synth_prompt())  # voice state precomputed (shared by all rows)
-
-    def admit(round_id):  # batched admission (ptts_slots_open): one shared text-prefill pass
-        eng.open_many(list(range(B)), [voice] * B, [text_ids(b) for b in range(B)],
-                      [pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), frames_after_eos=3, max_frames=K,
-                                           seed=slot_seed(round_id, rank, b)) for b in range(B)])
-
-    # warmup: a short job on the same rows (graph capture, caches), then the rows are re-admitted
-    admit(0)
-    for _ in range(W):
-        eng.step_async(B)
-    eng.sync()
-
     def barrier():
         if dist is not None:
             import torch
@@ -147,25 +136,41 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    # timed job: admission of all B utterances (voice KV copy + text prefill) and exactly K
-    # batched steps, i.e. first prefill to last PCM frame of B utterances of K frames
-    barrier()
-    eng.sync()
-    t0 = time.perf_counter()
-    admit(1)
-    eng.sync()
-    ta = time.perf_counter()
-    for _ in range(calls):
-        eng.step_async(B)
-    eng.sync()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    admit_s = ta - t0
-    if dist is not None:
-        elapsed, admit_s = max_over_ranks(dist, [elapsed, admit_s], f"cuda:{local_rank}")
-    r = eng.fetch(B)
-    assert r.valid.all() and r.last.all() and np.isfinite(r.pcm).all(), "bench produced invalid frames"
+    def timed_job(eng):
+        """Warmup job, then the timed one: admission of all B utterances (voice KV copy + text
+        prefill) and exactly K batched steps, i.e. first prefill to last PCM frame of B
+        utterances of K frames. Returns (elapsed, admission) seconds, max over ranks."""
+        voice = eng.voice_from_prompt(synth_prompt())  # voice state precomputed (shared by all rows)
+
+        def admit(round_id):  # batched admission (ptts_slots_open): one shared text-prefill pass
+            eng.open_many(list(range(B)), [voice] * B, [text_ids(b) for b in range(B)],
+                          [pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), frames_after_eos=3,
+                                               max_frames=K, seed=slot_seed(round_id, rank, b)) for b in range(B)])
+
+        # warmup: a short job on the same rows (graph capture, caches), then the rows are re-admitted
+        admit(0)
+        for _ in range(W):
+            eng.step_async(B)
+        eng.sync()
+        barrier()
+        eng.sync()
+        t0 = time.perf_counter()
+        admit(1)
+        eng.sync()
+        ta = time.perf_counter()
+        for _ in range(calls):
+            eng.step_async(B)
+        eng.sync()
+        t1 = time.perf_counter()
+        barrier()
+        elapsed, admit_s = t1 - t0, ta - t0
+        if dist is not None:
+            elapsed, admit_s = max_over_ranks(dist, [elapsed, admit_s], f"cuda:{local_rank}")
+        r = eng.fetch(B)
+        assert r.valid.all() and r.last.all() and np.isfinite(r.pcm).all(), "bench produced invalid frames"
+        return elapsed, admit_s
+
+    elapsed, admit_s = timed_job(eng)
 
     audio_sec = world * B * K * 1920 / 24000.0
     value = audio_sec / elapsed
@@ -227,6 +232,21 @@ def main():
         p50 = float(np.median(lat[5:]) * 1000.0)
         e1.close()
 
+    # ---- configs[4] variant: the same job on an engine with the reference's int8 weight
+    # quantization of the FlowLM (quantize.rs); its step GEMMs stream int8 codes. Reported beside
+    # `value`, never as it (different weights from the f32 model).
+    quant = None
+    if not args.no_quant_variant and world == 1:
+        eq = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
+                       pipeline=pipeline, weight_quant=pt.QUANT_FLOW_LM)
+        q_el, q_ad = timed_job(eq)
+        quant = {"value": round(B * K * 1920 / 24000.0 / q_el, 2), "unit": "audio-sec/wall-sec",
+                 "ms_per_step": round(1000.0 * q_el / K, 4),
+                 "steady_ms_per_step": round(1000.0 * (q_el - q_ad) / K, 4),
+                 "weight_quant": "flow_lm int8 (quantize.rs QuantizeConfig::default, per-tensor symmetric)",
+                 "int8_matrices": eq.int8_matrices}
+        eq.close()
+
     # ---- CPU baseline: the oracle (C port of the reference algorithm) on the host cores
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -263,6 +283,7 @@ def main():
                    "stepping": "pipelined (Mimi decode of frame k overlaps FlowLM step k+1)" if pipeline
                    else "sequential"},
         "p50_first_chunk_ms": None if p50 is None else round(p50, 3),
+        "int8_flowlm_variant": quant,
         "roofline": roof,
         "cpu_baseline": cpu,
         "top_ops": top,

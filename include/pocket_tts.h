@@ -54,7 +54,17 @@ typedef struct ptts_engine_config {
                                call returns the frame computed by the PREVIOUS call (one extra
                                call drains the last frame; the first call after admission
                                returns no frame for the admitted rows). */
+  int weight_quant;         /* PTTS_QUANT_*: the reference's weight quantization (quantize.rs,
+                               QuantizeConfig::default(): symmetric per-tensor int8 levels) applied
+                               when the weights are packed (TTSModel::load_quantized*,
+                               tts_model.rs:108-171). The FlowLM step GEMMs then stream int8 codes
+                               (float(q) * scale rebuilt in-kernel = the simulated f32 weight).
+                               A deferred blob must have been packed with the same mode. */
 } ptts_engine_config;
+
+#define PTTS_QUANT_NONE 0
+#define PTTS_QUANT_FLOW_LM 1 /* quantize_weights() over the flow_lm.* tensors */
+#define PTTS_QUANT_ALL 2     /* ... over the whole state dict (Mimi included) */
 
 /* Per-utterance generation parameters: TTSModel's public fields temp / eos_threshold /
  * noise_clamp (tts_model.rs:22-49) plus what generate_stream_segment derives from the text
@@ -77,6 +87,18 @@ size_t ptts_weight_blob_bytes(void);
  * (cfg.weight_blob + defer_weights) and calls ptts_engine_finalize(). Replaces the per-process
  * VarBuilder load of TTSModel::load_with_params_device (tts_model.rs:86-106). */
 int ptts_pack_weights(uint64_t synth_seed, const char* weights_path, float* host_out, size_t n_bytes);
+/* Same with the reference's weight quantization applied (weight_quant = PTTS_QUANT_*;
+ * quantize.rs:126-150 quantize_weights with QuantizeConfig::default()). */
+int ptts_pack_weights_ex(uint64_t synth_seed, const char* weights_path, int weight_quant, float* host_out,
+                         size_t n_bytes);
+/* The quantizer alone (QuantizedTensor::quantize, quantize.rs:66-90): out = simulated values,
+ * *scale = the per-tensor scale. Host only. */
+int ptts_quantize_tensor(const float* x, size_t n, int num_levels, float* out, float* scale);
+/* 1 if quantize_weights() with QuantizeConfig::default() quantizes tensor `name` of `numel`
+ * elements in scope `weight_quant` (should_skip_layer + min_size, quantize.rs:120-150). */
+int ptts_quant_applies(const char* name, size_t numel, int weight_quant);
+/* Number of FlowLM GEMM weight matrices the engine streams as int8 codes (0 when not quantized). */
+int ptts_engine_int8_matrices(ptts_engine* e);
 
 /* TTSModel::load / load_with_params_device (tts_model.rs:59-106,182-236). */
 int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out);

@@ -90,6 +90,7 @@ typedef struct { float *w, *b; int cin, cout, r; } ConvTr;     /* w as torch [ci
 
 struct orc_model {
   uint64_t seed;
+  int quant; /* weight quantization scope: 0 none, 1 flow_lm.*, 2 all (quantize.rs) */
   /* FlowLM (flow_lm.rs:24-37) */
   float *embed, *bos, *emb_mean, *emb_std, *input_linear, *out_norm_w, *out_norm_b, *eos_w, *eos_b;
   Layer fl[NL];
@@ -107,12 +108,41 @@ struct orc_model {
   Conv econv0, eres_a[3], eres_b[3], edown[3], efinal;
 };
 
+/* ---------------- weight quantization (crates/pocket-tts/src/quantize.rs) ----------------
+ * QuantizeConfig::default() (quantize.rs:27-40): skip names containing embed/lut/out_proj/
+ * eos_head, keep tensors under min_size = 1024 elements, 256 levels. should_skip_layer is a
+ * substring test (quantize.rs:120-123); quantize_weights applies it per tensor (:126-150). */
+int orc_quant_applies(const char* name, int64_t numel, int mode) {
+  static const char* skip[] = {"embed", "lut", "out_proj", "eos_head"};
+  if (mode == 0 || numel < 1024) return 0;
+  for (int i = 0; i < 4; ++i)
+    if (contains(name, skip[i])) return 0;
+  return mode == 2 || strncmp(name, "flow_lm.", 8) == 0;
+}
+/* QuantizedTensor::quantize (quantize.rs:66-90), f32 throughout as Candle computes it:
+ * scale = max|x| / (levels/2 - 1) (1 if all zero); data = clamp(round(x / scale)) * scale,
+ * round half away from zero (f32::round). Returns the scale. */
+float orc_quantize(const float* x, int64_t n, int num_levels, float* out) {
+  float amax = 0.f;
+  for (int64_t i = 0; i < n; ++i) amax = fmaxf(amax, fabsf(x[i]));
+  const float half = (float)(num_levels / 2);
+  const float scale = amax > 0.f ? amax / (half - 1.0f) : 1.0f;
+  const float lim = half - 1.0f;
+  for (int64_t i = 0; i < n; ++i) {
+    float q = roundf(x[i] / scale);
+    q = fminf(fmaxf(q, -lim), lim);
+    out[i] = q * scale;
+  }
+  return scale;
+}
+
 static float* orc_getw(const orc_model* m, const char* name, int64_t s0, int64_t s1, int64_t s2) {
   int64_t shape[3] = {s0, s1, s2};
   int nd = s2 ? 3 : (s1 ? 2 : 1);
   int64_t n = s0 * (s1 ? s1 : 1) * (s2 ? s2 : 1);
   float* p = (float*)malloc(sizeof(float) * (size_t)n);
   synth_fill(m->seed, name, shape, nd, p, n);
+  if (orc_quant_applies(name, n, m->quant)) orc_quantize(p, n, 256, p);
   return p;
 }
 /* torch Conv1d weight [cout][cin][k] -> [cout][k][cin] */
@@ -162,10 +192,13 @@ static void mklayer(const orc_model* m, Layer* L, const char* pfx, int d, int ff
 #undef W_
 }
 
-orc_model* orc_model_create(uint64_t seed) {
+orc_model* orc_model_create(uint64_t seed) { return orc_model_create_ex(seed, 0); }
+
+orc_model* orc_model_create_ex(uint64_t seed, int quant) {
   orc_model* m = (orc_model*)calloc(1, sizeof(orc_model));
   char nm[256];
   m->seed = seed;
+  m->quant = quant;
   m->embed = orc_getw(m, "flow_lm.conditioner.embed.weight", VOCAB, D, 0);
   m->bos = orc_getw(m, "flow_lm.bos_emb", LDIM, 0, 0);
   m->emb_mean = orc_getw(m, "flow_lm.emb_mean", LDIM, 0, 0);

@@ -22,6 +22,14 @@ typedef struct orc_state orc_state;
 
 /* Build the b6369a24 model with synthetic weights (tests/golden/synth.py rule). */
 orc_model* orc_model_create(uint64_t seed);
+/* Same, with the reference's weight quantization applied to the synthetic weights
+ * (quantize.rs quantize_weights + QuantizeConfig::default()): quant 0 none, 1 the flow_lm.*
+ * tensors, 2 every tensor. */
+orc_model* orc_model_create_ex(uint64_t seed, int quant);
+/* quantize.rs restatements: QuantizedTensor::quantize (returns the scale; out may alias x) and
+ * the quantize_weights selection rule. */
+float orc_quantize(const float* x, int64_t n, int num_levels, float* out);
+int orc_quant_applies(const char* name, int64_t numel, int mode);
 void orc_model_destroy(orc_model* m);
 /* First n elements of a synthetic tensor (PRNG pinning). Returns 0 on success. */
 int orc_synth_head(uint64_t seed, const char* name, const int64_t* shape, int ndim, float* out, int64_t n);

@@ -40,6 +40,11 @@ extern "C" {
 size_t ptts_weight_blob_bytes(void) { return ptts::pack_weights(nullptr, nullptr).total * sizeof(float); }
 
 int ptts_pack_weights(uint64_t synth_seed, const char* weights_path, float* host_out, size_t n_bytes) {
+  return ptts_pack_weights_ex(synth_seed, weights_path, PTTS_QUANT_NONE, host_out, n_bytes);
+}
+
+int ptts_pack_weights_ex(uint64_t synth_seed, const char* weights_path, int weight_quant, float* host_out,
+                         size_t n_bytes) {
   return guard([&] {
     if (!host_out) throw ptts::Error(PTTS_ERR_INVALID, "null output buffer");
     const size_t need = ptts::pack_weights(nullptr, nullptr).total * sizeof(float);
@@ -47,10 +52,28 @@ int ptts_pack_weights(uint64_t synth_seed, const char* weights_path, float* host
     std::unique_ptr<ptts::TensorSource> src = weights_path && weights_path[0]
                                                   ? ptts::make_safetensors_source(weights_path)
                                                   : ptts::make_synth_source(synth_seed);
+    src = ptts::make_quant_source(std::move(src), weight_quant);
     std::memset(host_out, 0, need);
     ptts::pack_weights(src.get(), host_out);
   });
 }
+
+int ptts_quantize_tensor(const float* x, size_t n, int num_levels, float* out, float* scale) {
+  return guard([&] {
+    if ((!x || !out) && n) throw ptts::Error(PTTS_ERR_INVALID, "null tensor");
+    if (num_levels < 4) throw ptts::Error(PTTS_ERR_INVALID, "num_levels must be >= 4");
+    std::vector<float> v(x, x + n);
+    const float s = ptts::quantize_inplace(v, num_levels);
+    if (n) std::memcpy(out, v.data(), n * sizeof(float));
+    if (scale) *scale = s;
+  });
+}
+
+int ptts_quant_applies(const char* name, size_t numel, int weight_quant) {
+  return name && ptts::quant_applies(name, numel, weight_quant) ? 1 : 0;
+}
+
+int ptts_engine_int8_matrices(ptts_engine* e) { return (e && e->impl) ? e->impl->int8_matrices() : 0; }
 
 int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out) {
   return guard([&] {

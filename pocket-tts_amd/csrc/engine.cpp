@@ -41,6 +41,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
   max_slots_ = cfg.max_slots;
   max_ctx_ = cfg.max_ctx;
   lsd_ = cfg.lsd_decode_steps;
+  PTTS_REQUIRE(cfg.weight_quant >= QUANT_NONE && cfg.weight_quant <= QUANT_ALL, "unknown weight_quant mode");
+  wq_ = cfg.weight_quant;
   int ndev = 0;
   PTTS_HIP(hipGetDeviceCount(&ndev));
   PTTS_REQUIRE(dev_ >= 0 && dev_ < ndev, "HIP device ordinal out of range");
@@ -147,6 +149,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
     std::unique_ptr<TensorSource> src = cfg.weights_path && cfg.weights_path[0]
                                             ? make_safetensors_source(cfg.weights_path)
                                             : make_synth_source(cfg.synth_seed);
+    src = make_quant_source(std::move(src), wq_);
     upload_weights(src.get());
     finalize();
   }
@@ -179,6 +182,7 @@ void Engine::upload_weights(TensorSource* src) {
 
 void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
+  if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   TimeEmbedWeights tw;
   for (int i = 0; i < 2; ++i) {
     tw.l1w[i] = W(L_.te_l1w[i]);
@@ -201,6 +205,46 @@ void Engine::run_ops(const std::vector<Op>& ops) {
   }
 }
 
+// int8 code matrices of the quantized FlowLM GEMM weights, derived on the device from the
+// blob (so a blob received over RCCL needs nothing else): every Layout::Q8 matrix whose rows
+// all carry a scale gets codes; quant_codes checks float(q) * s == W bit for bit.
+void Engine::derive_int8() {
+  float mode = 0.f;
+  PTTS_HIP(hipMemcpy(&mode, blob_ + L_.qmode, sizeof(float), hipMemcpyDeviceToHost));
+  PTTS_REQUIRE((int)mode == wq_, "weight blob was packed with a different weight_quant mode");
+  std::vector<const Layout::Q8*> use;
+  size_t bytes = 0;
+  for (const Layout::Q8& q : L_.q8) {
+    std::vector<float> s((size_t)q.N);
+    PTTS_HIP(hipMemcpy(s.data(), blob_ + q.s, s.size() * sizeof(float), hipMemcpyDeviceToHost));
+    if (std::all_of(s.begin(), s.end(), [](float v) { return v > 0.f; })) {
+      use.push_back(&q);
+      bytes += ((size_t)q.N * q.K + 255) / 256 * 256;
+    }
+  }
+  if (use.empty()) return;
+  void* codes = nullptr;
+  PTTS_HIP(hipMalloc(&codes, bytes));
+  allocs_.push_back(codes);
+  int* bad = (int*)dalloc(1);
+  size_t off = 0;
+  for (const Layout::Q8* q : use) {
+    int8_t* c = (int8_t*)codes + off;
+    quant_codes(W(q->w), W(q->s), q->N, q->K, c, bad, stream_);
+    q8map_[W(q->w)] = {c, W(q->s)};
+    off += ((size_t)q->N * q->K + 255) / 256 * 256;
+  }
+  PTTS_HIP(hipGetLastError());
+  int nbad = 0;
+  PTTS_HIP(hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, stream_));
+  PTTS_HIP(hipStreamSynchronize(stream_));
+  if (nbad) {
+    q8map_.clear();
+    throw Error(PTTS_ERR_INVALID, "quantized weights are not on their int8 grid (" + std::to_string(nbad) +
+                                      " elements): blob not packed by the quantizer");
+  }
+}
+
 // ------------------------------------------------------------------ op builders
 void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M,
                           const float* Wt, int N, int K, int* S_out) {
@@ -216,9 +260,24 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
     layout = 12;
     S = 1;
   }
+  // quantized FlowLM weights on the step path: stream int8 codes (k_gemm_w8, 32x64 tiles, enough
+  // z-slices for ~384 workgroups, >= 4 K chunks per slice). Prefill passes (M >= 256) keep the
+  // f32 copy of the same values: they are MFMA-bound.
+  auto q8 = q8map_.find(Wt);
+  const bool w8 = q8 != q8map_.end() && M <= 64;
+  if (w8) {
+    const int tn = getenv("PTTS_W8_TN1") ? 1 : 2;
+    layout = tn == 1 ? 1 : 0;
+    const int tiles = ((N + 32 * tn - 1) / (32 * tn)) * ((M + 31) / 32);
+    S = std::max(1, std::min({16, std::max(1, (K / 32) / 4), (384 + tiles - 1) / tiles}));
+  }
   while (S > 1 && (size_t)S * M * N > pcap_) --S;
   PTTS_REQUIRE((size_t)S * M * N <= pcap_, "split-K partial buffer too small");
   GemmArgs a{};
+  if (w8) {
+    a.Wq = q8->second.first;
+    a.wscale = q8->second.second;
+  }
   a.mode = 0;
   a.layout = layout;
   a.M = M;
@@ -231,7 +290,7 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   a.S = S;
   a.partial = partial_;
   ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
-                 4.0 * ((double)N * K + (double)M * K + (double)S * M * N)});
+                 (w8 ? (double)N * K + 4.0 * N : 4.0 * N * K) + 4.0 * ((double)M * K + (double)S * M * N)});
   last_split_ = a;
   last_split_op_ = ops.size() - 1;
   *S_out = S;

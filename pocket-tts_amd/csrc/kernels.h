@@ -60,6 +60,10 @@ struct GemmArgs {
   // B operand
   const float* W;
   long w_phase_stride;  // floats between polyphase weight blocks (mode 1)
+  // int8 B operand (weight_quant; mode 0, split-K slabs only): W[n][k] = float(Wq[n][k]) *
+  // wscale[n], formed per element before the MFMA. Replaces W when non-null.
+  const int8_t* Wq;
+  const float* wscale;
   // split-K
   int S;
   float* partial;  // [S][M][N] when S > 1
@@ -82,6 +86,11 @@ struct GemmArgs {
   RowReduceArgs rr;  // rr.P == partial, rr.S == S
 };
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
+
+// int8 codes of a quantized weight matrix: q[n][k] = W[n][k] / s[n] (exact integers in
+// [-127, 127] for a blob packed by the quantizer); rows with s[n] == 0 get code 0. Any element
+// with float(q) * s[n] != W[n][k] (bitwise) increments *bad.
+void quant_codes(const float* W, const float* s, int N, int K, int8_t* q, int* bad, hipStream_t st);
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s);
 

@@ -719,6 +719,117 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// int8-weight split-K GEMM for the FlowLM step under weight_quant. The weights hold the
+// reference's simulated quantization (QuantizedTensor::quantize, quantize.rs:66-90: data =
+// clamp(round(x/scale)) * scale, in f32), so the f32 weight is rebuilt per element as
+// float(q) * scale[n] - bit-for-bit the value the reference multiplies with - and only the
+// int8 code is streamed from HBM: 4x fewer weight bytes on the weight-bound skinny GEMMs.
+// Structure of LAYOUT 0: 4 waves on one 32 x (32*TN) tile, the tile's K chunks dealt
+// round-robin to the waves (one chunk in flight ahead of the MFMAs), partial tiles summed
+// through LDS into split-K slab z. Lane (r, h) reads the 16 codes k0+16h..+15 of row
+// n0+32t+r with one 16-byte load; each A fragment feeds TN MFMAs.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float i8_to_f(unsigned d, int b) { return (float)((int)(d << (24 - 8 * b)) >> 24); }
+
+template <int TN>
+__global__ __launch_bounds__(256) void k_gemm_w8(GemmArgs a) {
+  __shared__ float red[4 * 16 * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.x * 32 * TN, m0 = blockIdx.y * 32, z = blockIdx.z;
+  const int nchunks = a.K >> 5;
+  const int cb = (int)((long)nchunks * z / a.S), ce = (int)((long)nchunks * (z + 1) / a.S);
+  // rows past M / N are clamped to valid ones: their results are never stored
+  const float* xrow = a.X + (long)min(m0 + r, a.M - 1) * a.ldx + 16 * h;
+  const int8_t* wrow[TN];
+  float sc[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int n = min(n0 + 32 * t + r, a.N - 1);
+    wrow[t] = a.Wq + (long)n * a.K + 16 * h;
+    sc[t] = a.wscale[n];
+  }
+  floatx16 acc[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
+
+  auto load = [&](int cc, float4 (&A)[4], uint4 (&Q)[TN]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A[i] = *reinterpret_cast<const float4*>(xrow + (cc << 5) + 4 * i);
+#pragma unroll
+    for (int t = 0; t < TN; ++t) Q[t] = *reinterpret_cast<const uint4*>(wrow[t] + (cc << 5));
+  };
+  auto mma = [&](float4 (&A)[4], uint4 (&Q)[TN]) {
+    float af[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[4 * i + 0] = A[i].x; af[4 * i + 1] = A[i].y; af[4 * i + 2] = A[i].z; af[4 * i + 3] = A[i].w;
+    }
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const unsigned d[4] = {Q[t].x, Q[t].y, Q[t].z, Q[t].w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float w = i8_to_f(d[j >> 2], j & 3) * sc[t];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], w, acc[t], 0, 0, 0);
+      }
+    }
+  };
+  float4 a0[4], a1[4];
+  uint4 q0[TN], q1[TN];
+  const int c = cb + wave;
+  const int n = c < ce ? (ce - c + 3) / 4 : 0;
+  const int clast = c + (n - 1) * 4;
+  auto chunk = [&](int i) { return i < n ? c + i * 4 : clast; };
+  if (n > 0) {
+    load(c, a0, q0);
+    int i = 0;
+    for (; i + 2 <= n; i += 2) {
+      load(chunk(i + 1), a1, q1);
+      mma(a0, q0);
+      load(chunk(i + 2), a0, q0);
+      mma(a1, q1);
+    }
+    if (i < n) mma(a0, q0);
+  }
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[t][g];
+    __syncthreads();
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int g = wave * 4 + gg;
+      const float v = red[g * 64 + lane] + red[(16 + g) * 64 + lane] + red[(32 + g) * 64 + lane] +
+                      red[(48 + g) * 64 + lane];
+      const int row = m0 + (g & 3) + 8 * (g >> 2) + 4 * h;
+      const int col = n0 + 32 * t + r;
+      if (row < a.M && col < a.N) a.partial[((long)z * a.M + row) * a.N + col] = v;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_quant_codes(const float* W, const float* s, int N, int K, int8_t* q,
+                                                     int* bad) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * K) return;
+  const float sc = s[i / K], w = W[i];
+  float c = sc > 0.f ? rintf(w / sc) : 0.f;
+  c = fminf(fmaxf(c, -127.f), 127.f);
+  q[i] = (int8_t)c;
+  if (sc > 0.f && c * sc != w) atomicAdd(bad, 1);
+}
+
+void quant_codes(const float* W, const float* s, int N, int K, int8_t* q, int* bad, hipStream_t st) {
+  const long n = (long)N * K;
+  hipLaunchKernelGGL(k_quant_codes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, s, N, K, q, bad);
+}
+
 template <int MODE>
 static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
   switch (a.layout) {
@@ -783,6 +894,13 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
 }
 
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s) {
+  if (a.Wq) {  // int8 weights: layout 1 = 32x32 tiles, else 32x64
+    if (a.layout == 1)
+      hipLaunchKernelGGL((k_gemm_w8<1>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_gemm_w8<2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+    return;
+  }
   if (a.mode == 0) gemm_launch<0>(a, grid_z, s);
   else gemm_launch<1>(a, grid_z, s);
 }

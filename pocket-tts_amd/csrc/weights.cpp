@@ -14,6 +14,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -263,6 +264,61 @@ class SafetensorsSource : public TensorSource {
 };
 }  // namespace
 
+// ------------------------------------------------------------------ quantization (quantize.rs)
+namespace {
+class QuantSource : public TensorSource {
+ public:
+  QuantSource(std::unique_ptr<TensorSource> base, int mode) : base_(std::move(base)), mode_(mode) {}
+  std::vector<float> get(const std::string& name, const std::vector<int64_t>& shape) override {
+    std::vector<float> v = base_->get(name, shape);
+    if (quant_applies(name, v.size(), mode_)) scales_[name] = quantize_inplace(v);
+    return v;
+  }
+  int quant_mode() const override { return mode_; }
+  float quant_scale(const std::string& name) const override {
+    auto it = scales_.find(name);
+    return it == scales_.end() ? 0.f : it->second;
+  }
+
+ private:
+  std::unique_ptr<TensorSource> base_;
+  int mode_;
+  std::map<std::string, float> scales_;
+};
+}  // namespace
+
+bool quant_applies(const std::string& name, size_t numel, int mode) {
+  // QuantizeConfig::default() (quantize.rs:27-40): skip_layers, min_size 1024
+  static const char* const kSkip[] = {"embed", "lut", "out_proj", "eos_head"};
+  if (mode == QUANT_NONE || numel < 1024) return false;
+  for (const char* k : kSkip)
+    if (has(name, k)) return false;  // should_skip_layer (quantize.rs:120-123): substring match
+  return mode == QUANT_ALL || name.compare(0, 8, "flow_lm.") == 0;
+}
+
+float quantize_inplace(std::vector<float>& v, int num_levels) {
+  // QuantizedTensor::quantize (quantize.rs:66-90), all in f32 as Candle computes it:
+  // abs_max = max|x|; scale = abs_max / (half - 1); q = clamp(round(x / scale), +-(half - 1));
+  // data = q * scale. round() is half away from zero (Rust f32::round).
+  float amax = 0.f;
+  for (float x : v) amax = std::max(amax, std::fabs(x));
+  const float half = (float)(num_levels / 2);
+  const float scale = amax > 0.f ? amax / (half - 1.0f) : 1.0f;
+  const float lim = half - 1.0f;
+  for (float& x : v) {
+    float q = std::round(x / scale);
+    q = std::min(std::max(q, -lim), lim);
+    x = q * scale;
+  }
+  return scale;
+}
+
+std::unique_ptr<TensorSource> make_quant_source(std::unique_ptr<TensorSource> base, int mode) {
+  if (mode < QUANT_NONE || mode > QUANT_ALL) throw Error(PTTS_ERR_INVALID, "unknown weight_quant mode");
+  if (mode == QUANT_NONE) return base;
+  return std::make_unique<QuantSource>(std::move(base), mode);
+}
+
 std::unique_ptr<TensorSource> make_synth_source(uint64_t seed) { return std::make_unique<SynthSource>(seed); }
 std::unique_ptr<TensorSource> make_safetensors_source(const std::string& path) {
   return std::make_unique<SafetensorsSource>(path);
@@ -431,6 +487,45 @@ Layout pack_weights(TensorSource* src, float* dst) {
   L.efin_w = put_conv("mimi.encoder.model.11.conv.weight", 512, 512, 3, 512);
   L.efin_b = put("mimi.encoder.model.11.conv.bias", {512});
   L.down_w = put_conv("mimi.downsample.conv.conv.weight", 512, 512, 32, 512);
+
+  // ---------------- quantized storage: mode marker and int8-code row scales. Rows take the
+  // scale of the tensor they were packed from; a matrix with any unquantized part is skipped
+  // at finalize (its scale rows hold 0 there).
+  L.qmode = alloc(1);
+  if (dst) dst[L.qmode] = src ? (float)src->quant_mode() : 0.f;
+  auto q8 = [&](size_t w, int N, int K, std::vector<std::pair<std::string, int>> parts) {
+    Layout::Q8 q{w, alloc((size_t)N), N, K};
+    if (dst) {
+      int row = 0;
+      for (auto& pr : parts) {
+        const float sc = src ? src->quant_scale(pr.first) : 0.f;
+        for (int i = 0; i < pr.second; ++i) dst[q.s + row++] = sc;
+      }
+      if (row != N) throw Error(PTTS_ERR_INVALID, "int8 scale rows do not cover the matrix");
+    }
+    L.q8.push_back(q);
+  };
+  for (int l = 0; l < NL; ++l) {
+    const std::string p = F + "transformer.layers." + std::to_string(l);
+    q8(L.fl[l].in_proj, 3 * D, D, {{p + ".self_attn.in_proj.weight", 3 * D}});
+    q8(L.fl[l].l1, FF, D, {{p + ".linear1.weight", FF}});
+    q8(L.fl[l].l2, D, FF, {{p + ".linear2.weight", D}});
+  }
+  q8(L.input_linear, D, LDIM, {{F + "input_linear.weight", D}});
+  q8(L.inproj_w, FD, LDIM, {{FN + "input_proj.weight", FD}});
+  {
+    std::vector<std::pair<std::string, int>> parts;
+    for (int b = 0; b < FDEPTH; ++b)
+      parts.push_back({FN + "res_blocks." + std::to_string(b) + ".adaLN_modulation.1.weight", 3 * FD});
+    parts.push_back({FN + "final_layer.adaLN_modulation.1.weight", 2 * FD});
+    q8(L.ada_w, NADA, FD, parts);
+  }
+  for (int b = 0; b < FDEPTH; ++b) {
+    const std::string p = FN + "res_blocks." + std::to_string(b) + ".";
+    q8(L.rb_w0[b], FD, FD, {{p + "mlp.0.weight", FD}});
+    q8(L.rb_w2[b], FD, FD, {{p + "mlp.2.weight", FD}});
+  }
+  q8(L.fin_w, LDIM, FD, {{FN + "final_layer.linear.weight", LDIM}});
   L.total = cur;
   return L;
 }

@@ -20,7 +20,26 @@ class TensorSource {
   virtual ~TensorSource() = default;
   // Tensor `name` (TTSModel state-dict key) as fp32, checked against `shape`.
   virtual std::vector<float> get(const std::string& name, const std::vector<int64_t>& shape) = 0;
+  // Quantization scope applied by this source (QuantMode) and the per-tensor scale it used for
+  // `name` (0 = tensor kept in full precision). Plain sources quantize nothing.
+  virtual int quant_mode() const { return 0; }
+  virtual float quant_scale(const std::string&) const { return 0.f; }
 };
+
+// ---------------------------------------------------------------------------------------------
+// Weight quantization of the reference (crates/pocket-tts/src/quantize.rs), restated:
+// symmetric per-tensor int8 levels with QuantizeConfig::default() (skip names containing
+// "embed", "lut", "out_proj", "eos_head"; tensors under 1024 elements stay f32; 256 levels).
+// QUANT_FLOW_LM applies quantize_weights() to the flow_lm.* tensors (BASELINE configs[4],
+// "int8-quantised FlowLM"), QUANT_ALL to the whole state dict.
+enum QuantMode : int { QUANT_NONE = 0, QUANT_FLOW_LM = 1, QUANT_ALL = 2 };
+// should_skip_layer / min_size test of quantize_weights (quantize.rs:120-150) plus the scope
+bool quant_applies(const std::string& name, size_t numel, int mode);
+// QuantizedTensor::quantize (quantize.rs:66-90) in place: v <- clamp(round(v/s), +-127) * s,
+// s = max|v| / 127 (1 for an all-zero tensor). Returns s.
+float quantize_inplace(std::vector<float>& v, int num_levels = 256);
+// `base` with quantize_inplace applied to every tensor quant_applies() selects.
+std::unique_ptr<TensorSource> make_quant_source(std::unique_ptr<TensorSource> base, int mode);
 
 // Counter-based synthetic weights, bit-identical to tests/golden/synth.py.
 std::unique_ptr<TensorSource> make_synth_source(uint64_t seed);
@@ -44,6 +63,16 @@ struct Layout {
   TL mdec[MNL], menc[MNL];
   size_t dc0_w, dc0_b, dtr_w[3], dtr_b[3], dra_w[3], dra_b[3], drb_w[3], drb_b[3], dfin_w, dfin_b;
   size_t ec0_w, ec0_b, era_w[3], era_b[3], erb_w[3], erb_b[3], edn_w[3], edn_b[3], efin_w, efin_b, down_w;
+  // Quantized storage. `qmode` is one float holding the QuantMode the blob was packed with.
+  // Every FlowLM step GEMM weight whose source tensors were all quantized gets an int8 code
+  // matrix at engine finalize: codes q[n][k] = W[n][k] / s[n] with the row scales s packed in
+  // the blob (the per-tensor scale of the source tensor each row came from; 0 = not quantized).
+  struct Q8 {
+    size_t w, s;  // f32 weights [N][K], row scales [N]
+    int N, K;
+  };
+  size_t qmode;
+  std::vector<Q8> q8;
   size_t total;
 };
 

@@ -16,6 +16,7 @@ FRAME = 1920
 LDIM = 32
 DIM = 1024
 SAMPLE_RATE = 24000
+QUANT_NONE, QUANT_FLOW_LM, QUANT_ALL = 0, 1, 2
 
 F32P = C.POINTER(C.c_float)
 U8P = C.POINTER(C.c_uint8)
@@ -33,6 +34,7 @@ class EngineConfig(C.Structure):
         ("weight_blob", C.c_void_p),
         ("defer_weights", C.c_int),
         ("pipeline", C.c_int),
+        ("weight_quant", C.c_int),
     ]
 
 
@@ -51,6 +53,10 @@ class GenParams(C.Structure):
 SIGNATURES = [
     ("ptts_weight_blob_bytes", C.c_size_t, []),
     ("ptts_pack_weights", C.c_int, [C.c_uint64, C.c_char_p, F32P, C.c_size_t]),
+    ("ptts_pack_weights_ex", C.c_int, [C.c_uint64, C.c_char_p, C.c_int, F32P, C.c_size_t]),
+    ("ptts_quantize_tensor", C.c_int, [F32P, C.c_size_t, C.c_int, F32P, F32P]),
+    ("ptts_quant_applies", C.c_int, [C.c_char_p, C.c_size_t, C.c_int]),
+    ("ptts_engine_int8_matrices", C.c_int, [C.c_void_p]),
     ("ptts_engine_create", C.c_int, [C.POINTER(EngineConfig), C.POINTER(C.c_void_p)]),
     ("ptts_engine_finalize", C.c_int, [C.c_void_p]),
     ("ptts_engine_destroy", None, [C.c_void_p]),

@@ -67,15 +67,18 @@ class StepResult:
 class Engine:
     def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
                  seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
-                 defer_weights: bool = False, pipeline: bool = False):
+                 defer_weights: bool = False, pipeline: bool = False, weight_quant: int = 0):
         """pipeline=True: overlapped stepping, each step() returns the frame produced by the
-        previous call (see ptts_engine_config.pipeline)."""
+        previous call (see ptts_engine_config.pipeline). weight_quant: QUANT_NONE / QUANT_FLOW_LM /
+        QUANT_ALL, the reference's simulated int8 weight quantization (quantize.rs), with the
+        FlowLM step GEMMs streaming int8 codes."""
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
-                           weight_blob or None, int(defer_weights), int(pipeline))
+                           weight_blob or None, int(defer_weights), int(pipeline), int(weight_quant))
         h = C.c_void_p()
         check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
         self.handle = h
+        self.weight_quant = int(weight_quant)
         self.max_slots = max_slots
         self.max_ctx = max_ctx
         self.lsd_decode_steps = lsd_decode_steps
@@ -86,12 +89,18 @@ class Engine:
         return int(lib().ptts_weight_blob_bytes())
 
     @staticmethod
-    def pack_weights(seed: int = 0x5EED, weights_path: str | None = None) -> np.ndarray:
-        """Packed weight blob (engine device layout) built on the host; no GPU needed."""
+    def pack_weights(seed: int = 0x5EED, weights_path: str | None = None, weight_quant: int = 0) -> np.ndarray:
+        """Packed weight blob (engine device layout) built on the host; no GPU needed.
+        weight_quant applies the reference's quantize_weights (quantize.rs) while packing."""
         out = np.empty(Engine.weight_blob_bytes() // 4, np.float32)
-        check(lib().ptts_pack_weights(seed, weights_path.encode() if weights_path else None,
-                                      out.ctypes.data_as(F32P), out.nbytes))
+        check(lib().ptts_pack_weights_ex(seed, weights_path.encode() if weights_path else None, int(weight_quant),
+                                         out.ctypes.data_as(F32P), out.nbytes))
         return out
+
+    @property
+    def int8_matrices(self) -> int:
+        """FlowLM GEMM weight matrices streamed as int8 codes (0 unless weight_quant)."""
+        return int(lib().ptts_engine_int8_matrices(self.handle))
 
     def weight_blob(self) -> int:
         return int(lib().ptts_engine_weight_blob(self.handle) or 0)

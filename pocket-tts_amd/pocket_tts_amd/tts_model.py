@@ -23,7 +23,7 @@ from typing import Callable, Iterator, Sequence
 
 import numpy as np
 
-from ._lib import FRAME, SAMPLE_RATE
+from ._lib import FRAME, QUANT_ALL, QUANT_FLOW_LM, QUANT_NONE, SAMPLE_RATE
 from .audio import read_wav, read_wav_from_bytes
 from .engine import Engine, GenerationParams, Voice
 from .text import (estimate_frames_after_eos, load_tokenizer, long_text_segments, max_gen_len,
@@ -63,7 +63,8 @@ class TTSModel:
     def load_with_params(cls, variant: str = DEFAULT_VARIANT, temp: float = 0.7, lsd_decode_steps: int = 1,
                          eos_threshold: float = -4.0, noise_clamp: float | None = None, *,
                          weights_path: str | None = None, tokenizer_path: str | None = None, seed: int = 0x5EED,
-                         device: int = 0, max_ctx: int = 1024, tokenizer=None) -> "TTSModel":
+                         device: int = 0, max_ctx: int = 1024, tokenizer=None,
+                         weight_quant: int = QUANT_NONE) -> "TTSModel":
         """weights_path: local safetensors with the TTSModel state-dict names (synthetic weights
         from `seed` when None); tokenizer_path: tokenizer.model (SentencePiece) or tokenizer.json."""
         if variant != DEFAULT_VARIANT:
@@ -71,8 +72,29 @@ class TTSModel:
         if tokenizer is None and tokenizer_path:
             tokenizer = load_tokenizer(tokenizer_path)
         eng = Engine(device=device, max_slots=1, max_ctx=max_ctx, lsd_decode_steps=lsd_decode_steps, seed=seed,
-                     weights_path=weights_path)
+                     weights_path=weights_path, weight_quant=weight_quant)
         return cls(eng, temp, lsd_decode_steps, eos_threshold, noise_clamp, tokenizer)
+
+    # ---- quantized loading (tts_model.rs:108-181, feature "quantized"). The reference's version
+    # is a placeholder that returns the f32 model (is_quantized() == false); here the weights get
+    # quantize_weights() with QuantizeConfig::default() (quantize.rs) and the FlowLM step GEMMs
+    # stream the int8 codes. scope: QUANT_FLOW_LM (default) or QUANT_ALL.
+    @classmethod
+    def load_quantized(cls, variant: str = DEFAULT_VARIANT, **kw) -> "TTSModel":
+        return cls.load_quantized_with_params(variant, **kw)
+
+    @classmethod
+    def load_quantized_with_params(cls, variant: str = DEFAULT_VARIANT, temp: float = 0.7,
+                                   lsd_decode_steps: int = 1, eos_threshold: float = -4.0,
+                                   noise_clamp: float | None = None, *, scope: int = QUANT_FLOW_LM,
+                                   **kw) -> "TTSModel":
+        if scope not in (QUANT_FLOW_LM, QUANT_ALL):
+            raise ValueError("scope must be QUANT_FLOW_LM or QUANT_ALL")
+        return cls.load_with_params(variant, temp, lsd_decode_steps, eos_threshold, noise_clamp,
+                                    weight_quant=scope, **kw)
+
+    def is_quantized(self) -> bool:
+        return self.engine.weight_quant != QUANT_NONE
 
     # ---- voice states
     def get_voice_state_from_prompt_tensor(self, prompt: np.ndarray) -> Voice:

@@ -21,6 +21,11 @@ def lib() -> C.CDLL:
         L = C.CDLL(str(path))
         L.orc_model_create.restype = C.c_void_p
         L.orc_model_create.argtypes = [C.c_uint64]
+        L.orc_model_create_ex.restype = C.c_void_p
+        L.orc_model_create_ex.argtypes = [C.c_uint64, C.c_int]
+        L.orc_quantize.restype = C.c_float
+        L.orc_quantize.argtypes = [F32P, C.c_int64, C.c_int, F32P]
+        L.orc_quant_applies.argtypes = [C.c_char_p, C.c_int64, C.c_int]
         L.orc_model_destroy.argtypes = [C.c_void_p]
         L.orc_synth_head.argtypes = [C.c_uint64, C.c_char_p, C.POINTER(C.c_int64), C.c_int, F32P, C.c_int64]
         L.orc_state_create.restype = C.c_void_p
@@ -51,11 +56,12 @@ def fp(a: np.ndarray | None):
 
 
 class Oracle:
-    """One synthetic-weight model (seed) on the CPU."""
+    """One synthetic-weight model (seed) on the CPU; quant = weight quantization scope
+    (0 none, 1 flow_lm.*, 2 all: the oracle's quantize.rs restatement)."""
 
-    def __init__(self, seed: int = 0x5EED):
+    def __init__(self, seed: int = 0x5EED, quant: int = 0):
         self.L = lib()
-        self.m = self.L.orc_model_create(seed)
+        self.m = self.L.orc_model_create_ex(seed, quant)
 
     def __del__(self):
         if getattr(self, "m", None):
@@ -91,6 +97,18 @@ class Oracle:
 
     def bench(self, n_utt, F, S, n_frames, threads):
         return self.L.orc_bench(self.m, n_utt, F, S, n_frames, threads)
+
+
+def quantize(x: np.ndarray, num_levels: int = 256):
+    """The oracle's QuantizedTensor::quantize restatement: (simulated values, scale)."""
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    sc = lib().orc_quantize(fp(x), x.size, num_levels, fp(out))
+    return out, float(sc)
+
+
+def quant_applies(name: str, numel: int, mode: int) -> bool:
+    return bool(lib().orc_quant_applies(name.encode(), numel, mode))
 
 
 def resample(x: np.ndarray, sr_from: int, sr_to: int = 24000) -> np.ndarray:
