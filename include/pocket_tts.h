@@ -105,6 +105,9 @@ int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out);
 /* Second half of create when cfg->defer_weights = 1 (derived tables, time embeddings). */
 int ptts_engine_finalize(ptts_engine* e);
 void ptts_engine_destroy(ptts_engine* e);
+/* Copy a host blob from ptts_pack_weights[_ex] into a deferred engine's weight buffer (the
+ * single-process alternative to a device-side fill); call ptts_engine_finalize() after it. */
+int ptts_engine_load_blob(ptts_engine* e, const float* host_blob, size_t n_bytes);
 /* Device pointer of the packed weight blob (for the caller's RCCL broadcast). */
 void* ptts_engine_weight_blob(ptts_engine* e);
 

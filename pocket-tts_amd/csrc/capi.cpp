@@ -90,6 +90,13 @@ int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out) {
   });
 }
 
+int ptts_engine_load_blob(ptts_engine* e, const float* host_blob, size_t n_bytes) {
+  return guard([&] {
+    if (!host_blob) throw ptts::Error(PTTS_ERR_INVALID, "null blob");
+    eng(e).load_blob(host_blob, n_bytes);
+  });
+}
+
 int ptts_engine_finalize(ptts_engine* e) { return guard([&] { eng(e).finalize(); }); }
 
 void ptts_engine_destroy(ptts_engine* e) {

@@ -180,6 +180,13 @@ void Engine::upload_weights(TensorSource* src) {
   PTTS_HIP(hipMemcpy(blob_, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
 }
 
+void Engine::load_blob(const float* host, size_t n_bytes) {
+  PTTS_REQUIRE(n_bytes == L_.total * sizeof(float), "blob size differs from ptts_weight_blob_bytes()");
+  PTTS_REQUIRE(!ready_, "engine already finalized");
+  PTTS_HIP(hipSetDevice(dev_));
+  PTTS_HIP(hipMemcpy(blob_, host, n_bytes, hipMemcpyHostToDevice));
+}
+
 void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
@@ -260,16 +267,18 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
     layout = 12;
     S = 1;
   }
-  // quantized FlowLM weights on the step path: stream int8 codes (k_gemm_w8, 32x64 tiles, enough
-  // z-slices for ~384 workgroups, >= 4 K chunks per slice). Prefill passes (M >= 256) keep the
-  // f32 copy of the same values: they are MFMA-bound.
+  // quantized FlowLM weights on the step path: stream int8 codes (k_gemm_w8, 32x64 tiles, the
+  // smallest power-of-two split reaching 256 workgroups with >= 4 K chunks per slice). Only the
+  // large matrices (qkv, ff1, ff2, adaLN; >= 2M weights): below that the launch is latency-bound
+  // and the f32 copy of the same values is as fast (tools/w8_probe.py). Prefill passes
+  // (M >= 256) keep the f32 copy too: they are MFMA-bound.
   auto q8 = q8map_.find(Wt);
-  const bool w8 = q8 != q8map_.end() && M <= 64;
+  const bool w8 = q8 != q8map_.end() && M <= 64 && (long)N * K >= (2L << 20) && !getenv("PTTS_W8_OFF");
   if (w8) {
-    const int tn = getenv("PTTS_W8_TN1") ? 1 : 2;
-    layout = tn == 1 ? 1 : 0;
-    const int tiles = ((N + 32 * tn - 1) / (32 * tn)) * ((M + 31) / 32);
-    S = std::max(1, std::min({16, std::max(1, (K / 32) / 4), (384 + tiles - 1) / tiles}));
+    layout = 0;
+    const int tiles = ((N + 63) / 64) * ((M + 31) / 32);
+    S = 1;
+    while (S < 16 && tiles * S < 256 && (K / 32) / (2 * S) >= 4) S *= 2;
   }
   while (S > 1 && (size_t)S * M * N > pcap_) --S;
   PTTS_REQUIRE((size_t)S * M * N <= pcap_, "split-K partial buffer too small");

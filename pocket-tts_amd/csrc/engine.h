@@ -34,6 +34,7 @@ class Engine {
   Engine& operator=(const Engine&) = delete;
 
   void finalize();
+  void load_blob(const float* host, size_t n_bytes);
   float* blob() { return blob_; }
   int max_slots() const { return max_slots_; }
   bool pipelined() const { return pipeline_; }

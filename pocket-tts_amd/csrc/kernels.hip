@@ -894,11 +894,8 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
 }
 
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s) {
-  if (a.Wq) {  // int8 weights: layout 1 = 32x32 tiles, else 32x64
-    if (a.layout == 1)
-      hipLaunchKernelGGL((k_gemm_w8<1>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((k_gemm_w8<2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+  if (a.Wq) {  // int8 weights: 32x64 tiles
+    hipLaunchKernelGGL((k_gemm_w8<2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
     return;
   }
   if (a.mode == 0) gemm_launch<0>(a, grid_z, s);

@@ -59,6 +59,7 @@ SIGNATURES = [
     ("ptts_engine_int8_matrices", C.c_int, [C.c_void_p]),
     ("ptts_engine_create", C.c_int, [C.POINTER(EngineConfig), C.POINTER(C.c_void_p)]),
     ("ptts_engine_finalize", C.c_int, [C.c_void_p]),
+    ("ptts_engine_load_blob", C.c_int, [C.c_void_p, F32P, C.c_size_t]),
     ("ptts_engine_destroy", None, [C.c_void_p]),
     ("ptts_engine_weight_blob", C.c_void_p, [C.c_void_p]),
     ("ptts_voice_from_prompt", C.c_int, [C.c_void_p, F32P, C.c_int, C.POINTER(C.c_void_p)]),

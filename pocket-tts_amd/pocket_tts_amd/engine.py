@@ -105,6 +105,11 @@ class Engine:
     def weight_blob(self) -> int:
         return int(lib().ptts_engine_weight_blob(self.handle) or 0)
 
+    def load_blob(self, blob: np.ndarray):
+        """Fill a deferred engine's weights from a host blob (Engine.pack_weights)."""
+        blob = np.ascontiguousarray(blob, np.float32)
+        check(lib().ptts_engine_load_blob(self.handle, blob.ctypes.data_as(F32P), blob.nbytes))
+
     def finalize(self):
         check(lib().ptts_engine_finalize(self.handle))
 

@@ -241,25 +241,22 @@ def test_gpu_int8_batched_pipelined_matches_quantized_oracle():
 
 @pytest.mark.gpu
 def test_gpu_quant_mode_mismatch_is_an_error():
-    """A deferred blob packed without quantization cannot back a weight_quant engine."""
-    import torch
-
+    """A deferred blob packed without quantization cannot back a weight_quant engine; one
+    packed with the same mode can (the multi-GPU path: rank 0 packs, the others receive)."""
     import pocket_tts_amd as pt
 
-    blob = pt.Engine.pack_weights(0x5EED, None, 0)
-    dev = torch.from_numpy(blob).to("cuda:0")
-    eng = pt.Engine(device=0, max_slots=1, max_ctx=64, weight_blob=dev.data_ptr(), defer_weights=True,
-                    weight_quant=1)
+    eng = pt.Engine(device=0, max_slots=1, max_ctx=64, defer_weights=True, weight_quant=1)
     try:
+        eng.load_blob(pt.Engine.pack_weights(0x5EED, None, 0))
         with pytest.raises(pt.PocketTTSError, match="weight_quant"):
             eng.finalize()
     finally:
         eng.close()
-    blob1 = pt.Engine.pack_weights(0x5EED, None, 1)
-    dev1 = torch.from_numpy(blob1).to("cuda:0")
-    eng = pt.Engine(device=0, max_slots=1, max_ctx=64, weight_blob=dev1.data_ptr(), defer_weights=True,
-                    weight_quant=1)
+    eng = pt.Engine(device=0, max_slots=1, max_ctx=64, defer_weights=True, weight_quant=1)
     try:
+        with pytest.raises(pt.PocketTTSError):
+            eng.load_blob(np.zeros(10, np.float32))
+        eng.load_blob(pt.Engine.pack_weights(0x5EED, None, 1))
         eng.finalize()
         assert eng.int8_matrices == 34
     finally:
