@@ -126,8 +126,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
     T *= RATIOS[i];
     ch /= 2;
     cb_[i] = dalloc((size_t)B * T * ch);
+    ce_[i] = dalloc((size_t)B * T * ch);
     cv_[i] = dalloc((size_t)B * T * (ch / 2));
     ca_[i] = dalloc((size_t)B * T * ch);
+    trb_[i] = dalloc((size_t)RATIOS[i] * ch);
   }
   temb_ = dalloc((size_t)lsd_ * FD);
   temb_tmp_ = dalloc((size_t)2 * lsd_ * FD);
@@ -199,6 +201,10 @@ void Engine::finalize() {
     tw.alpha[i] = W(L_.te_alpha[i]);
   }
   time_embeddings(tw, lsd_, temb_tmp_, temb_, stream_);
+  for (int i = 0, ch = MD / 2; i < 3; ++i, ch /= 2)  // bias of the phase-merged transposed convs
+    for (int p = 0; p < RATIOS[i]; ++p)
+      PTTS_HIP(hipMemcpyAsync(trb_[i] + (size_t)p * ch, W(L_.dtr_b[i]), sizeof(float) * ch, hipMemcpyDeviceToDevice,
+                              stream_));
   PTTS_HIP(hipGetLastError());
   PTTS_HIP(hipStreamSynchronize(stream_));
   ready_ = true;
@@ -358,7 +364,8 @@ void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float
 
 void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float* X, int B, int T_in, int cin,
                      const float* H, int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases,
-                     const float* bias, const float* R, float* Y, int T_out, int tstride, int layout) {
+                     const float* bias, const float* R, float* Y, int T_out, int tstride, int layout, int elu_out,
+                     float* Y2) {
   PTTS_REQUIRE(cin % 32 == 0, "conv cin must be a multiple of 32");
   GemmArgs a{};
   a.mode = 1;
@@ -386,9 +393,11 @@ void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float*
   a.ldy = cout;
   a.T_out = T_out;
   a.out_tstride = tstride;
+  a.elu_out = elu_out;
+  a.Y2 = Y2;
   ops.push_back({name, [a, phases](hipStream_t s) { gemm(a, phases, s); }, 2.0 * a.M * a.N * a.K * phases,
                  4.0 * ((double)phases * a.N * a.K + (double)B * T_in * cin +
-                        (double)B * T_out * cout * (R ? 2 : 1))});
+                        (double)B * T_out * cout * ((R ? 2 : 1) + (Y2 ? 1 : 0)))});
 }
 
 // FlowLM transformer layers over M rows (x_ holds the residual stream, h_ = norm1_0(x_)).
@@ -534,8 +543,8 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
     }
     for (int i = 0; i < FDEPTH; ++i) {
       const std::string pb = p + ".rb" + std::to_string(i);
-      linear_split(ops, pb + ".mlp0_gemm", hf_, FD, B, W(L_.rb_w0[i]), FD, FD, &S);
       {
+        linear_split(ops, pb + ".mlp0_gemm", hf_, FD, B, W(L_.rb_w0[i]), FD, FD, &S);
         RowReduceArgs a{};
         a.P = partial_;
         a.S = S;
@@ -673,39 +682,44 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
       ops.push_back({p + ".ln1_next", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
     }
   }
-  // SEANetDecoder (seanet.rs:396-402): conv0 -> [ELU, convtr(r), resblock] x3 -> ELU, conv(64->1)
+  // SEANetDecoder (seanet.rs:396-402): conv0 -> [ELU, convtr(r), resblock] x3 -> ELU, conv(64->1).
+  // Every ELU is applied once, by the producer of the activation (elu_out / the dual store Y2),
+  // so the consumers' operand loads are plain: a0, ce, cv and ca hold ELU'd activations (and so
+  // do the histories of the convs that read them; elu(0) = 0 keeps the zero reset valid), cb
+  // stays raw for the resblock skip. Transposed convs run with their r phases merged into N: one
+  // 2-tap conv over rows (x[q-1], x[q]) whose output row q is the r time rows q*r .. q*r+r-1 of
+  // the channels-last output, N = r * Cout (packed [r][Cout][2][Cin] = [r*Cout][2*Cin]).
+  const bool big = B >= 16;
   conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, W(L_.dc0_b), nullptr, a0_,
-          16, 1);
+          16, 1, 0, 1);
   const float* cin_buf = a0_;
   int T = 16, ch = 512;
   for (int i = 0; i < 3; ++i) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
-    // per-stage tile choice (tools/gemm_bench.hip at B=32): the short-K, many-row late stages
-    // run the LDS-DMA kernels; the first stage keeps the K-split register kernel
-    const bool big = B >= 16;
-    const int l_tr = big ? (i == 1 ? 20 : (i == 2 ? 6 : 0)) : 0;
-    const int l_r3 = big && i == 0 ? 18 : 0;
-    const int l_r1 = big && i == 2 ? 6 : 0;
-    conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 1, W(L_.dtr_w[i]), ch / 2, 2, r,
-            W(L_.dtr_b[i]), nullptr, cb_[i], T * r, r, l_tr);
+    // per-stage tiles (tools/gemm_bench.hip, rb.* cases, B = 32)
+    const int l_tr = big ? (i == 0 ? 20 : 6) : 0;
+    const int l_r3 = big ? (i == 0 ? 18 : (i == 1 ? 20 : 6)) : 0;
+    const int l_r1 = big ? 6 : 0;
+    conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 0, W(L_.dtr_w[i]), r * (ch / 2), 2, 1,
+            trb_[i], nullptr, cb_[i], T, 1, l_tr, 0, ce_[i]);
     T *= r;
     ch /= 2;
-    conv_op(ops, p + ".res_conv3", cb_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 1, W(L_.dra_w[i]), ch / 2, 3, 1,
-            W(L_.dra_b[i]), nullptr, cv_[i], T, 1, l_r3);
-    conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 1, W(L_.drb_w[i]), ch, 1, 1, W(L_.drb_b[i]),
-            cb_[i], ca_[i], T, 1, l_r1);
+    conv_op(ops, p + ".res_conv3", ce_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 0, W(L_.dra_w[i]), ch / 2, 3, 1,
+            W(L_.dra_b[i]), nullptr, cv_[i], T, 1, l_r3, 1);
+    conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 0, W(L_.drb_w[i]), ch, 1, 1, W(L_.drb_b[i]),
+            cb_[i], ca_[i], T, 1, l_r1, 1);
     cin_buf = ca_[i];
   }
   {
     const float *X = ca_[2], *H = hist_[7], *w = W(L_.dfin_w), *b = W(L_.dfin_b);
     float* Y = pcm_[par];
-    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, FRAME, 64, 3, w, b, Y, s); }});
+    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, FRAME, 64, 3, w, b, Y, 0, s); }});
   }
   // ---- commit of the back part: conv histories and Mimi positions of rows with a frame
   {
     CommitArgs c{};
-    const float* srcs[8] = {mx_, a0_, cb_[0], ca_[0], cb_[1], ca_[1], cb_[2], ca_[2]};
+    const float* srcs[8] = {mx_, a0_, ce_[0], ca_[0], ce_[1], ca_[1], ce_[2], ca_[2]};
     for (int i = 0; i < 8; ++i) c.h[i] = HistDesc{srcs[i], hist_[i], hist_T_[i], hist_C_[i], hist_P_[i]};
     c.nh = 8;
     c.B = B;

@@ -75,7 +75,8 @@ class Engine {
                     int N, int K, int* S_out);
   void conv_op(std::vector<Op>& ops, const std::string& name, const float* X, int B, int T_in, int cin, const float* H,
                int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases, const float* bias,
-               const float* R, float* Y, int T_out, int tstride, int layout = 0);
+               const float* R, float* Y, int T_out, int tstride, int layout = 0, int elu_out = 0,
+               float* Y2 = nullptr);
   void dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N, int K,
                 const float* bias, int act, const float* rscale, const float* R, float* Y,
                 int layout = 0);
@@ -117,7 +118,8 @@ class Engine {
   float *ysilu_ = nullptr, *mods_ = nullptr, *xf_ = nullptr, *hf_ = nullptr, *uf_ = nullptr;
   float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;
   float* a0_ = nullptr;
-  float *cb_[3] = {}, *cv_[3] = {}, *ca_[3] = {};
+  float *cb_[3] = {}, *cv_[3] = {}, *ca_[3] = {}, *ce_[3] = {};
+  float* trb_[3] = {};  // transposed-conv biases replicated over the r output phases [r][Cout]
   // front -> back hand-off per step parity, and the back part's own split-K slabs
   float* lat_out_[2] = {};
   float* eos_out_[2] = {};

@@ -76,6 +76,10 @@ struct GemmArgs {
   float* Y;
   long ldy;
   int T_out, out_tstride;  // mode 1 output row = b*T_out + q*out_tstride + phase
+  // ELU on the way out (SEANet: the consumer's ELU applied once by the producer, seanet.rs:298-305):
+  // elu_out: Y = elu(v) (after the residual); Y2 != null: Y = v and Y2 = elu(v) (same indexing)
+  int elu_out;
+  float* Y2;
   // In-launch split-K combine (layouts 0 and 13, mode 0): every workgroup stores its slab into
   // `partial`, then draws a ticket on its output tile; the last arriver sums the S slabs and runs
   // the row-reduce epilogue `rr` on the tile (fuse 1). With fuse 2 the tile finishers also draw a
@@ -230,7 +234,7 @@ void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols
 // out[m] = sum_k x[m*ldx + k] * w[k] + b  (tiny GEMV column, e.g. the N=1 final conv)
 // Streaming conv with Cout == 1: pcm[b][t] = bias + sum_{j,ci} elu(xin)[...] * w[j][ci].
 void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, const float* w, const float* bias,
-                float* Y, hipStream_t s);
+                float* Y, int elu_in, hipStream_t s);
 
 // Encoder first conv (Cin == 1): Y[b][t][co] = bias[co] + sum_j w[co][j] * xpad[t + j], with
 // the 6-sample zero history (constant padding, conv.py:90-108).

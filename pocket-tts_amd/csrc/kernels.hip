@@ -53,6 +53,33 @@ __device__ void splitk_combine(const GemmArgs& g, int m0, int n0, int ncols, flo
 //   (each wave runs the whole K chain of its z-slice; neighbours share A rows / W rows in L1/L2)
 //   K-split variants of LAYOUT 0: LAYOUT 9 = 8 waves (2 per SIMD at one workgroup per CU),
 //   LAYOUT 10 = 4 waves with two chunks in flight, LAYOUT 17 = 8 waves, two chunks in flight.
+// Epilogue of one output element v of GEMM row `row`, column `col` (S == 1 path): bias,
+// activation, per-column scale, residual, ELU-out / dual store. Mode 1 maps row (b, q) to the
+// output time row b*T_out + q*out_tstride + phase; `ident` (wave-uniform) marks the identity map
+// (mode 0, or stride-1 single-phase convs) and skips the per-element division.
+__device__ __forceinline__ void gemm_store(const GemmArgs& a, int row, int col, int phase, bool ident, float v) {
+  if (a.bias) v += a.bias[col];
+  if (a.act == ACT_GELU) v = gelu_tanh(v);
+  else if (a.act == ACT_SILU) v = silu(v);
+  long yrow = row;
+  if (!ident) {
+    const int b2 = row / a.Tq;
+    const int q2 = row - b2 * a.Tq;
+    yrow = (long)b2 * a.T_out + (long)q2 * a.out_tstride + phase;
+  }
+  if (a.rscale) v *= a.rscale[col];
+  if (a.R) v += a.R[yrow * a.ldr + col];
+  if (a.Y2) {
+    a.Y[yrow * a.ldy + col] = v;
+    a.Y2[yrow * a.ldy + col] = elu1(v);
+  } else {
+    a.Y[yrow * a.ldy + col] = a.elu_out ? elu1(v) : v;
+  }
+}
+__device__ __forceinline__ bool gemm_ident(const GemmArgs& a, int mode, int phase) {
+  return mode == 0 || (phase == 0 && a.out_tstride == 1 && a.T_out == a.Tq);
+}
+
 template <int LAYOUT>
 struct Lay {
   static constexpr bool KSPLIT = LAYOUT == 0 || LAYOUT == 9 || LAYOUT == 10 || LAYOUT == 17;
@@ -188,6 +215,7 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
     }
   }
 
+  const bool ident = gemm_ident(a, MODE, phase);
   auto store = [&](int g, float v) {
     const int row = m0 + (g & 3) + 8 * (g >> 2) + 4 * h;
     const int col = n0 + r;
@@ -196,18 +224,7 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
       a.partial[((long)z * a.M + row) * a.N + col] = v;
       return;
     }
-    if (a.bias) v += a.bias[col];
-    if (a.act == ACT_GELU) v = gelu_tanh(v);
-    else if (a.act == ACT_SILU) v = silu(v);
-    long yrow = row;
-    if (MODE == 1) {
-      const int b2 = row / a.Tq;
-      const int q2 = row - b2 * a.Tq;
-      yrow = (long)b2 * a.T_out + (long)q2 * a.out_tstride + phase;
-    }
-    if (a.rscale) v *= a.rscale[col];
-    if (a.R) v += a.R[yrow * a.ldr + col];
-    a.Y[yrow * a.ldy + col] = v;
+    gemm_store(a, row, col, phase, ident, v);
   };
   if (KS) {
 #pragma unroll
@@ -352,18 +369,7 @@ __global__ __launch_bounds__(256) void k_gemm_lds(GemmArgs a) {
       a.partial[((long)z * a.M + row) * a.N + col] = v;
       return;
     }
-    if (a.bias) v += a.bias[col];
-    if (a.act == ACT_GELU) v = gelu_tanh(v);
-    else if (a.act == ACT_SILU) v = silu(v);
-    long yrow = row;
-    if (MODE == 1) {
-      const int b2 = row / a.Tq;
-      const int q2 = row - b2 * a.Tq;
-      yrow = (long)b2 * a.T_out + (long)q2 * a.out_tstride + phase;
-    }
-    if (a.rscale) v *= a.rscale[col];
-    if (a.R) v += a.R[yrow * a.ldr + col];
-    a.Y[yrow * a.ldy + col] = v;
+    gemm_store(a, row, col, phase, gemm_ident(a, MODE, phase), v);
   };
   if (!SHARED) {
 #pragma unroll
@@ -422,9 +428,12 @@ __device__ __forceinline__ unsigned lds_addr(const float* p) {
 // s_waitcnt with only vmcnt = n (expcnt/lgkmcnt left at "no wait"), gfx9 simm16 encoding
 #define PTTS_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
 
-template <int MODE, int WM, int WN, int BK, int NBUF>
+// TMW x TNW: 32x32 accumulators per wave (register blocking: one A fragment feeds TNW MFMAs,
+// one B fragment TMW), WG tile (32*WM*TMW) x (32*WN*TNW).
+// MODE 1 with S > 1 (single-phase convs): z is a K slice and the tile goes to partial slab z.
+template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1>
 __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
-  constexpr int TM = 32 * WM, TN = 32 * WN, ROWS = TM + TN;
+  constexpr int TM = 32 * WM * TMW, TN = 32 * WN * TNW, ROWS = TM + TN;
   constexpr int CPR = BK / 4;        // 16-byte columns per LDS row
   constexpr int RPI = 64 / CPR;      // rows per 1-KiB wave instruction
   constexpr int NINS = ROWS / RPI;   // DMA instructions per chunk (whole workgroup)
@@ -440,7 +449,7 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
   const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM, z = blockIdx.z;
   const int nchunks = a.K / BK;
   int cb = 0, ce = nchunks, phase = 0;
-  if (MODE == 0) {
+  if (MODE == 0 || a.S > 1) {
     cb = (int)((long)nchunks * z / a.S);
     ce = (int)((long)nchunks * (z + 1) / a.S);
   } else {
@@ -496,10 +505,14 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
     }
   };
   const bool elu = MODE == 1 && a.elu_in;
-  floatx16 acc;
+  floatx16 acc[TMW][TNW];
 #pragma unroll
-  for (int g = 0; g < 16; ++g) acc[g] = 0.f;
-  const int arow = 32 * wm + r, brow = TM + 32 * wn + r;
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < TNW; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.f;
+  const int arow = 32 * TMW * wm + r, brow = TM + 32 * TNW * wn + r;
   for (int d = 0; d < DIST; ++d)
     if (cb + d < ce) issue(cb + d, d);
   for (int c = cb; c < ce; ++c) {
@@ -515,53 +528,65 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
     if (c + DIST < ce) issue(c + DIST, (c + DIST - cb) % NBUF);
     {
       const int buf = (c - cb) % NBUF;
-      const float* la = lds + buf * ROWS * BK + arow * BK;
-      const float* lb = lds + buf * ROWS * BK + brow * BK;
 #pragma unroll
       for (int half = 0; half < BK / 32; ++half) {
-        float af[16], bf[16];
+        float af[TMW][16], bf[TNW][16];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int lc = 8 * half + 4 * h + i;
-          const float4 x = *reinterpret_cast<const float4*>(la + 4 * (lc ^ swz<BK>(arow)));
-          const float4 y = *reinterpret_cast<const float4*>(lb + 4 * (lc ^ swz<BK>(brow)));
-          af[4 * i + 0] = x.x; af[4 * i + 1] = x.y; af[4 * i + 2] = x.z; af[4 * i + 3] = x.w;
-          bf[4 * i + 0] = y.x; bf[4 * i + 1] = y.y; bf[4 * i + 2] = y.z; bf[4 * i + 3] = y.w;
+        for (int ii = 0; ii < TMW; ++ii) {
+          const int row = arow + 32 * ii;
+          const float* la = lds + buf * ROWS * BK + row * BK;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int lc = 8 * half + 4 * h + i;
+            const float4 x = *reinterpret_cast<const float4*>(la + 4 * (lc ^ swz<BK>(row)));
+            af[ii][4 * i + 0] = x.x; af[ii][4 * i + 1] = x.y; af[ii][4 * i + 2] = x.z; af[ii][4 * i + 3] = x.w;
+          }
+          if (elu) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) af[ii][j] = elu1(af[ii][j]);
+          }
         }
-        if (elu) {
 #pragma unroll
-          for (int j = 0; j < 16; ++j) af[j] = elu1(af[j]);
+        for (int jj = 0; jj < TNW; ++jj) {
+          const int row = brow + 32 * jj;
+          const float* lb = lds + buf * ROWS * BK + row * BK;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int lc = 8 * half + 4 * h + i;
+            const float4 y = *reinterpret_cast<const float4*>(lb + 4 * (lc ^ swz<BK>(row)));
+            bf[jj][4 * i + 0] = y.x; bf[jj][4 * i + 1] = y.y; bf[jj][4 * i + 2] = y.z; bf[jj][4 * i + 3] = y.w;
+          }
         }
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+          for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+            for (int jj = 0; jj < TNW; ++jj)
+              acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[ii][j], bf[jj][j], acc[ii][jj], 0, 0, 0);
       }
     }
   }
-  const int tm0 = m0 + 32 * wm, tn0 = n0 + 32 * wn;
+  const bool ident = gemm_ident(a, MODE, phase);
 #pragma unroll
-  for (int g = 0; g < 16; ++g) {
-    const int row = tm0 + (g & 3) + 8 * (g >> 2) + 4 * h;
-    const int col = tn0 + r;
-    if (row >= a.M || col >= a.N) continue;
-    float v = acc[g];
-    if (a.partial) {
-      a.partial[((long)z * a.M + row) * a.N + col] = v;
-      continue;
+  for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < TNW; ++jj) {
+      const int tm0 = m0 + 32 * TMW * wm + 32 * ii, tn0 = n0 + 32 * TNW * wn + 32 * jj;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int row = tm0 + (g & 3) + 8 * (g >> 2) + 4 * h;
+        const int col = tn0 + r;
+        if (row >= a.M || col >= a.N) continue;
+        float v = acc[ii][jj][g];
+        if (a.partial) {
+          a.partial[((long)z * a.M + row) * a.N + col] = v;
+          continue;
+        }
+        gemm_store(a, row, col, phase, ident, v);
+      }
     }
-    if (a.bias) v += a.bias[col];
-    if (a.act == ACT_GELU) v = gelu_tanh(v);
-    else if (a.act == ACT_SILU) v = silu(v);
-    long yrow = row;
-    if (MODE == 1) {
-      const int b2 = row / a.Tq;
-      const int q2 = row - b2 * a.Tq;
-      yrow = (long)b2 * a.T_out + (long)q2 * a.out_tstride + phase;
-    }
-    if (a.rscale) v *= a.rscale[col];
-    if (a.R) v += a.R[yrow * a.ldr + col];
-    a.Y[yrow * a.ldy + col] = v;
-  }
-  if (MODE == 0 && WM == 1 && a.fuse) splitk_combine(a, m0, n0, TN, lds);
+  if (MODE == 0 && WM == 1 && TMW == 1 && TNW == 1 && a.fuse) splitk_combine(a, m0, n0, TN, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -682,6 +707,7 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
     }
   }
   // K-split sum over the 4 waves, one 32x32 accumulator at a time through LDS
+  const bool ident = gemm_ident(a, MODE, phase);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -703,18 +729,7 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
           a.partial[((long)z * a.M + row) * a.N + col] = v;
           continue;
         }
-        if (a.bias) v += a.bias[col];
-        if (a.act == ACT_GELU) v = gelu_tanh(v);
-        else if (a.act == ACT_SILU) v = silu(v);
-        long yrow = row;
-        if (MODE == 1) {
-          const int b2 = row / a.Tq;
-          const int q2 = row - b2 * a.Tq;
-          yrow = (long)b2 * a.T_out + (long)q2 * a.out_tstride + phase;
-        }
-        if (a.rscale) v *= a.rscale[col];
-        if (a.R) v += a.R[yrow * a.ldr + col];
-        a.Y[yrow * a.ldy + col] = v;
+        gemm_store(a, row, col, phase, ident, v);
       }
     }
 }
@@ -849,6 +864,22 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     PTTS_GLDS(15, 2, 2, 64, 3)
     PTTS_GLDS(16, 1, 4, 64, 3)
 #undef PTTS_GLDS
+#define PTTS_GLRB(L, WM_, WN_, NB_, TMW_, TNW_)                                                       \
+  case L:                                                                                             \
+    hipLaunchKernelGGL((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_>),                             \
+                       dim3((a.N + 32 * WN_ * TNW_ - 1) / (32 * WN_ * TNW_),                          \
+                            (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z),                  \
+                       dim3(256), 0, s, a);                                                          \
+    return;
+    // register-blocked LDS-DMA tiles (per-wave TMW x TNW accumulators)
+    PTTS_GLRB(21, 2, 2, 3, 2, 2)  // 128 x 128
+    PTTS_GLRB(22, 2, 2, 3, 1, 2)  //  64 x 128
+    PTTS_GLRB(23, 2, 2, 3, 2, 1)  // 128 x  64
+    PTTS_GLRB(24, 4, 1, 3, 2, 1)  // 256 x  32
+    PTTS_GLRB(25, 4, 1, 3, 1, 2)  // 128 x  64 (waves stacked in M)
+    PTTS_GLRB(26, 2, 2, 4, 2, 2)  // 128 x 128, 4 buffers
+    PTTS_GLRB(27, 1, 4, 3, 2, 1)  //  64 x 128 (waves side by side in N)
+#undef PTTS_GLRB
     default:
       break;
   }
@@ -1511,16 +1542,32 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
   int slot, qp;
   row_slot_pos(mp, row, slot, qp);
   const int d = nh * 64, ld = 3 * d;
+  float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
+  float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
+  // The cached keys 0 .. qp-1 do not depend on this step's token: each wave issues the loads of
+  // its first 64-key block before the slab sum / RoPE / append below, so that HBM round trip
+  // overlaps them (one memory latency per wave instead of two in series).
+  const int last = qp - 1;
+  float4 k[16];
+  float v[64];
+  auto load_block = [&](int base) {
+    const int j = min(base + lane, last);
+    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)j * 64);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) k[i] = kr[i];
+#pragma unroll
+    for (int jj = 0; jj < 64; ++jj) v[jj] = vbase[(long)min(base + jj, last) * 64 + lane];
+  };
+  int base = 64 * wave;
+  if (base < qp) load_block(base);
   if (tid < 192) {  // q | k | v column of this head, summed over the slabs in z order
     const int part = tid >> 6;
     const float* pr = P + (long)row * ld + part * d + head * 64 + lane;
-    float v = 0.f;
-    for (int z = 0; z < S; ++z) v += pr[(long)z * M * ld];
-    s_qkv[part][lane] = v;
+    float acc = 0.f;
+    for (int z = 0; z < S; ++z) acc += pr[(long)z * M * ld];
+    s_qkv[part][lane] = acc;
   }
   __syncthreads();
-  float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
-  float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
   if (tid < 64) {  // rotate the (2i, 2i+1) pairs of q (tid < 32) and k (tid >= 32)
     const int i = tid & 31, part = tid >> 5;
     const float freq = expf((float)i * (-logf(10000.0f) * 2.0f / 64.0f));
@@ -1542,17 +1589,8 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
 #pragma unroll
   for (int i = 0; i < 16; ++i) q[i] = reinterpret_cast<const float4*>(s_qkv[0])[i];
   float m = -INFINITY, l = 0.f, o = 0.f;
-  for (int base = 64 * wave; base < qp; base += 256) {  // cached keys 0 .. qp-1
-    const int j = base + lane;
-    const int last = qp - 1;
-    const bool valid = j <= last;
-    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)(valid ? j : last) * 64);
-    float4 k[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) k[i] = kr[i];
-    float v[64];
-#pragma unroll
-    for (int jj = 0; jj < 64; ++jj) v[jj] = vbase[(long)min(base + jj, last) * 64 + lane];
+  for (; base < qp; base += 256) {  // cached keys 0 .. qp-1, block `base` already in registers
+    const bool valid = base + lane <= last;
     float sc = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) sc += q[i].x * k[i].x + q[i].y * k[i].y + q[i].z * k[i].z + q[i].w * k[i].w;
@@ -1566,6 +1604,7 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
 #pragma unroll
     for (int jj = 0; jj < 64; ++jj) o += __builtin_bit_cast(float, __builtin_amdgcn_readlane(pb, jj)) * v[jj];
     m = mn;
+    if (base + 256 < qp) load_block(base + 256);
   }
   if (wave == 0) {  // the new key (position qp) from LDS
     const float sc = wave_sum(s_qkv[0][lane] * s_qkv[1][lane]) * 0.125f;
@@ -1897,7 +1936,7 @@ void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols
 // t as a plain k x cin dot product (weights broadcast from LDS).
 template <int KT>
 __global__ __launch_bounds__(256) void k_conv_cout1(const float* X, const float* H, int B, int T, int cin,
-                                                    const float* w, const float* bias, float* Y) {
+                                                    const float* w, const float* bias, float* Y, int elu_in) {
   constexpr int P = KT - 1, ROWS = 64 + P;
   __shared__ float tile[4][ROWS][65];
   __shared__ float sw[KT * 64];
@@ -1916,7 +1955,7 @@ __global__ __launch_bounds__(256) void k_conv_cout1(const float* X, const float*
     e[i] = tt >= 0 ? xb[(long)tt * cin] : hb[(long)tt * cin];
   }
 #pragma unroll
-  for (int i = 0; i < ROWS; ++i) tile[wave][i][lane] = elu1(e[i]);
+  for (int i = 0; i < ROWS; ++i) tile[wave][i][lane] = elu_in ? elu1(e[i]) : e[i];
   __syncthreads();
   float acc = 0.f;
 #pragma unroll 8
@@ -1927,11 +1966,11 @@ __global__ __launch_bounds__(256) void k_conv_cout1(const float* X, const float*
 }
 
 void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, const float* w, const float* bias,
-                float* Y, hipStream_t s) {
+                float* Y, int elu_in, hipStream_t s) {
   const long waves = (long)B * ((T + 63) / 64);  // one lane per input channel: cin == 64, k == 3
   (void)k;
   hipLaunchKernelGGL(k_conv_cout1<3>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, X, H, B, T, cin, w, bias,
-                     Y);
+                     Y, elu_in);
 }
 
 // Encoder first conv (1 -> cout, k taps, zero history of k-1 samples): one thread per output.

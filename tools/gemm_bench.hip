@@ -106,7 +106,7 @@ int main(int argc, char** argv) {
     a.X = drand((size_t)B * T_in * cin, 3, 1.f);
     a.ldx = cin;
     a.H = drand((size_t)B * (P_ ? P_ : 1) * cin, 4, 1.f);
-    a.P = P_; a.T_in = T_in; a.stride_in = 1; a.cin = cin; a.elu_in = 1;
+    a.P = P_; a.T_in = T_in; a.stride_in = 1; a.cin = cin; a.elu_in = getenv("NOELU") ? 0 : 1;
     a.W = drand((size_t)phases * a.Nw * a.K, 5, 0.05f);
     a.w_phase_stride = (long)N * a.K;
     a.S = 1;
@@ -136,6 +136,26 @@ int main(int argc, char** argv) {
   conv("sea.convtr3 T480 c128 N64 x4", 480, 128, 1, 2, 64, 4, 4, fat);
   conv("sea.res3a T1920 c64 k3 N32", 1920, 64, 2, 3, 32, 1, 1, fat);
   conv("sea.res3b T1920 c32 k1 N64", 1920, 32, 0, 1, 64, 1, 1, fat);
+  // register-blocked LDS-DMA tiles; transposed convs with the r phases merged into N (one
+  // 2-tap conv whose output row q holds the r output rows q*r .. q*r+r-1)
+  std::vector<std::pair<int, int>> rb = {{6, 1}, {12, 1}, {20, 1}, {21, 1}, {22, 1}, {23, 1}, {24, 1},
+                                         {25, 1}, {26, 1}, {27, 1}};
+  std::vector<std::pair<int, int>> rbk = {{0, 1}, {21, 1}, {21, 2}, {21, 4}, {22, 1}, {22, 2}, {22, 4},
+                                          {23, 2}, {23, 4}, {25, 2}, {25, 4}, {27, 2}, {27, 4}};
+  conv("rb.conv0 T16 c512 k7 N512", 16, 512, 6, 7, 512, 1, 1, rbk);
+  conv("rb.convtr1m T16 c512 N1536", 16, 512, 1, 2, 1536, 1, 1, rb);
+  conv("rb.res1a T96 c256 k3 N128", 96, 256, 2, 3, 128, 1, 1, rbk);
+  conv("rb.res1b T96 c128 k1 N256", 96, 128, 0, 1, 256, 1, 1, rb);
+  conv("rb.convtr2m T96 c256 N640", 96, 256, 1, 2, 640, 1, 1, rb);
+  conv("rb.res2a T480 c128 k3 N64", 480, 128, 2, 3, 64, 1, 1, rb);
+  conv("rb.res2b T480 c64 k1 N128", 480, 64, 0, 1, 128, 1, 1, rb);
+  conv("rb.convtr3m T480 c128 N256", 480, 128, 1, 2, 256, 1, 1, rb);
+  conv("rb.res3a T1920 c64 k3 N32", 1920, 64, 2, 3, 32, 1, 1, rb);
+  conv("rb.res3b T1920 c32 k1 N64", 1920, 32, 0, 1, 64, 1, 1, rb);
+  dense("rb.mimi.qkv M512 N1536 K512", 16 * B, 1536, 512, rbk);
+  dense("rb.mimi.ff1 M512 N2048 K512", 16 * B, 2048, 512, rbk);
+  dense("rb.mimi.ff2 M512 N512 K2048", 16 * B, 512, 2048, rbk);
+  dense("rb.mimi.out M512 N512 K512", 16 * B, 512, 512, rbk);
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -159,8 +179,8 @@ int main(int argc, char** argv) {
       const int bk = (layout == 8 || layout == 15 || layout == 16) ? 64 : 32;
       if (layout >= 6 && (a.K % bk != 0 || (a.mode == 1 && a.cin % bk != 0))) continue;
       int gz = c.phases;
-      if (S > 1 && a.mode == 1) continue;
-      if (a.mode == 0 && S > 1) {
+      if (S > 1 && a.mode == 1 && (c.phases > 1 || layout < 21)) continue;
+      if (S > 1) {  // dense split-K, or K-sliced single-phase conv (register-blocked LDS-DMA)
         if (a.K / bk < S) continue;
         v.S = S;
         v.partial = P;
