@@ -236,6 +236,7 @@ def main():
     # quantization of the FlowLM (quantize.rs); its step GEMMs stream int8 codes. Reported beside
     # `value`, never as it (different weights from the f32 model).
     quant = None
+    eng.close()  # one engine on the GPU at a time
     if not args.no_quant_variant and world == 1:
         eq = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                        pipeline=pipeline, weight_quant=pt.QUANT_FLOW_LM)
@@ -290,7 +291,6 @@ def main():
         "sum_op_ms": sum_ops_ms,
     }
     print(json.dumps(out))
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 

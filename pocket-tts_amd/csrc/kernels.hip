@@ -80,6 +80,19 @@ __device__ __forceinline__ bool gemm_ident(const GemmArgs& a, int mode, int phas
   return mode == 0 || (phase == 0 && a.out_tstride == 1 && a.T_out == a.Tq);
 }
 
+// XCD-aware tile order. Workgroups are dealt round-robin to the 8 XCDs by linear id, so
+// consecutive ids land on different L2s and the N-tiles that share one A row block would each
+// miss in their own L2. Id L -> tile (L % 8) * (T / 8) + L / 8 gives every XCD a contiguous run
+// of tiles (x fastest), so those N-tiles meet in one L2. Identity when T % 8 != 0 or when the
+// in-launch split-K combine keys its tickets on blockIdx.
+__device__ __forceinline__ void xcd_tile(bool on, int& bx, int& by) {
+  const int gx = gridDim.x, T = gx * gridDim.y;
+  const int L = blockIdx.x + blockIdx.y * gx;
+  const int t = (on && (T & 7) == 0) ? (L & 7) * (T >> 3) + (L >> 3) : L;
+  bx = t % gx;
+  by = t / gx;
+}
+
 template <int LAYOUT>
 struct Lay {
   static constexpr bool KSPLIT = LAYOUT == 0 || LAYOUT == 9 || LAYOUT == 10 || LAYOUT == 17;
@@ -101,7 +114,9 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
   const int r = lane & 31, h = lane >> 5;
   constexpr int WM = Lay<LAYOUT>::WM, WN = Lay<LAYOUT>::WN;
   const int wm = KS ? 0 : wave / WN, wn = KS ? 0 : wave % WN;
-  const int n0 = (blockIdx.x * WN + wn) * 32, m0 = (blockIdx.y * WM + wm) * 32, z = blockIdx.z;
+  int bx, by;
+  xcd_tile(!a.fuse, bx, by);
+  const int n0 = (bx * WN + wn) * 32, m0 = (by * WM + wm) * 32, z = blockIdx.z;
   const int nchunks = a.K >> 5;
   int cb = 0, ce = nchunks, phase = 0;
   if (MODE == 0) {
@@ -446,7 +461,9 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int r = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM, z = blockIdx.z;
+  int bx, by;
+  xcd_tile(!a.fuse, bx, by);
+  const int n0 = bx * TN, m0 = by * TM, z = blockIdx.z;
   const int nchunks = a.K / BK;
   int cb = 0, ce = nchunks, phase = 0;
   if (MODE == 0 || a.S > 1) {
@@ -602,7 +619,9 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.x * 32 * TN, m0 = blockIdx.y * 32 * TM, z = blockIdx.z;
+  int bx, by;
+  xcd_tile(true, bx, by);
+  const int n0 = bx * 32 * TN, m0 = by * 32 * TM, z = blockIdx.z;
   const int nchunks = a.K >> 5;
   int cb = 0, ce = nchunks, phase = 0;
   if (MODE == 0) {
@@ -1532,31 +1551,48 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
 // sums its 192 q|k|v columns over the S slabs, rotates q and k (rope.rs:18-60), appends k, v at
 // the row's position and attends over the cached keys 0..pos-1 plus the new key from LDS.
 // ---------------------------------------------------------------------------------------------
+// Sum over each 16-lane row of the wave with DPP (quad_perm xor 1, xor 2, row_half_mirror,
+// row_mirror); every lane of the row ends with the row's sum.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true));
+  return v;
+}
+
+// Decode attention of the FlowLM step fused with the QKV slab sum, RoPE and KV append
+// (attention.rs:104-283 with the single-query mask skip of sdpa.rs:3-18). One 256-thread
+// workgroup per (row, head); the cached keys are dealt to the 4 waves 64 at a time.
+// A 64-key block of K (and of V) is 16 KB contiguous, read with 16 fully coalesced 1-KB wave
+// loads: load i gives lane l the 4 dims 4(l%16).. of key 4i + l/16. Scores: a 4-term dot with
+// the matching q dims, summed over the 16-lane row with DPP, so lane l holds the score of key
+// 4i + l/16 - exactly the key whose V dims it holds from V load i, so P.V needs no broadcast.
+// The rows (l/16) are combined once per wave at the end. Each wave issues its first block's
+// loads before the QKV/RoPE phase: the cached keys do not depend on this step's token.
 __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict__ P, int S, int M, int nh, RowMap mp,
                                                          KvStore kv, float* __restrict__ O) {
-  __shared__ float s_m[4], s_l[4], s_o[4][64];
-  __shared__ float s_qkv[3][64];
+  __shared__ float s_m[4], s_l[4];
+  __shared__ __attribute__((aligned(16))) float s_o[4][64];
+  __shared__ __attribute__((aligned(16))) float s_qkv[3][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c4 = (lane & 15) * 4;  // key row within a load, first of my 4 dims
   const int row = blockIdx.x, head = blockIdx.y;
   int slot, qp;
   row_slot_pos(mp, row, slot, qp);
   const int d = nh * 64, ld = 3 * d;
   float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
   float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
-  // The cached keys 0 .. qp-1 do not depend on this step's token: each wave issues the loads of
-  // its first 64-key block before the slab sum / RoPE / append below, so that HBM round trip
-  // overlaps them (one memory latency per wave instead of two in series).
   const int last = qp - 1;
-  float4 k[16];
-  float v[64];
+  float4 k[16], v[16];
   auto load_block = [&](int base) {
-    const int j = min(base + lane, last);
-    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)j * 64);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) k[i] = kr[i];
-#pragma unroll
-    for (int jj = 0; jj < 64; ++jj) v[jj] = vbase[(long)min(base + jj, last) * 64 + lane];
+    for (int i = 0; i < 16; ++i) {
+      const long off = (long)min(base + 4 * i + g, last) * 64 + c4;
+      k[i] = *reinterpret_cast<const float4*>(kbase + off);
+      v[i] = *reinterpret_cast<const float4*>(vbase + off);
+    }
   };
   int base = 64 * wave;
   if (base < qp) load_block(base);
@@ -1585,41 +1621,58 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
     vbase[(long)qp * 64 + lane] = s_qkv[2][lane];
   }
   __syncthreads();
-  float4 q[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) q[i] = reinterpret_cast<const float4*>(s_qkv[0])[i];
-  float m = -INFINITY, l = 0.f, o = 0.f;
+  const float4 q = *reinterpret_cast<const float4*>(&s_qkv[0][c4]);
+  float m = -INFINITY, l = 0.f;
+  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
   for (; base < qp; base += 256) {  // cached keys 0 .. qp-1, block `base` already in registers
-    const bool valid = base + lane <= last;
-    float sc = 0.f;
+    float sc[16];
+    float bm = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sc += q[i].x * k[i].x + q[i].y * k[i].y + q[i].z * k[i].z + q[i].w * k[i].w;
-    sc = valid ? sc * 0.125f : -INFINITY;  // 1/sqrt(64) (attention.rs:191,229)
-    const float mn = fmaxf(m, wave_max(sc));
+    for (int i = 0; i < 16; ++i) {
+      const float part = q.x * k[i].x + q.y * k[i].y + q.z * k[i].z + q.w * k[i].w;
+      const float t = row16_sum(part) * 0.125f;  // 1/sqrt(64) (attention.rs:191,229)
+      sc[i] = base + 4 * i + g <= last ? t : -INFINITY;
+      bm = fmaxf(bm, sc[i]);
+    }
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
     const float alpha = expf(m - mn);
-    const float p = valid ? expf(sc - mn) : 0.f;
-    l = l * alpha + wave_sum(p);
-    o *= alpha;
-    const int pb = __builtin_bit_cast(int, p);
+    float ps = 0.f;
+    o.x *= alpha; o.y *= alpha; o.z *= alpha; o.w *= alpha;
 #pragma unroll
-    for (int jj = 0; jj < 64; ++jj) o += __builtin_bit_cast(float, __builtin_amdgcn_readlane(pb, jj)) * v[jj];
+    for (int i = 0; i < 16; ++i) {
+      const float p = expf(sc[i] - mn);  // 0 for masked keys
+      ps += p;
+      o.x += p * v[i].x; o.y += p * v[i].y; o.z += p * v[i].z; o.w += p * v[i].w;
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
     m = mn;
     if (base + 256 < qp) load_block(base + 256);
   }
+  // combine the 4 key rows (lanes l, l^16, l^32, l^48 hold the same dims)
+  o.x += __shfl_xor(o.x, 16, 64); o.y += __shfl_xor(o.y, 16, 64);
+  o.z += __shfl_xor(o.z, 16, 64); o.w += __shfl_xor(o.w, 16, 64);
+  o.x += __shfl_xor(o.x, 32, 64); o.y += __shfl_xor(o.y, 32, 64);
+  o.z += __shfl_xor(o.z, 32, 64); o.w += __shfl_xor(o.w, 32, 64);
   if (wave == 0) {  // the new key (position qp) from LDS
     const float sc = wave_sum(s_qkv[0][lane] * s_qkv[1][lane]) * 0.125f;
     const float mn = fmaxf(m, sc);
     const float alpha = expf(m - mn);
     const float p = expf(sc - mn);
     l = l * alpha + p;
-    o = o * alpha + p * s_qkv[2][lane];
+    const float4 vn = *reinterpret_cast<const float4*>(&s_qkv[2][c4]);
+    o.x = o.x * alpha + p * vn.x; o.y = o.y * alpha + p * vn.y;
+    o.z = o.z * alpha + p * vn.z; o.w = o.w * alpha + p * vn.w;
     m = mn;
   }
   if (lane == 0) {
     s_m[wave] = m;
     s_l[wave] = l;
   }
-  s_o[wave][lane] = o;
+  if (lane < 16) *reinterpret_cast<float4*>(&s_o[wave][c4]) = o;
   __syncthreads();
   if (wave == 0) {
     const float Mx = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
