@@ -80,6 +80,65 @@ __device__ __forceinline__ bool gemm_ident(const GemmArgs& a, int mode, int phas
   return mode == 0 || (phase == 0 && a.out_tstride == 1 && a.T_out == a.Tq);
 }
 
+// Fast epilogue of NG accumulator values g = g0 .. g0+NG-1 of one in-bounds 32x32 tile
+// (identity row map, no split-K; row of g = tm0 + (g&3) + 8(g>>2) + 4h, column tn0 + r). The
+// column is fixed per lane, so bias / scale load once, row offsets are compile-time multiples of
+// the leading dimensions, and the uniform options branch once per call instead of per element
+// (the generic per-element path costs ~150 VALU per output, which dominated short-K tiles).
+template <int NG>
+__device__ __forceinline__ void gemm_store_fast(const GemmArgs& a, const float* acc, int g0, int tm0, int tn0, int h,
+                                                int r) {
+  const int col = tn0 + r;
+  const long rb = (long)(tm0 + 4 * h);
+  auto roff = [&](int k) { const int g = g0 + k; return (long)((g & 3) + 8 * (g >> 2)); };
+  const float bcol = a.bias ? a.bias[col] : 0.f;
+  float v[NG];
+#pragma unroll
+  for (int k = 0; k < NG; ++k) v[k] = acc[k] + bcol;
+  if (a.act == ACT_GELU) {
+#pragma unroll
+    for (int k = 0; k < NG; ++k) v[k] = gelu_tanh(v[k]);
+  } else if (a.act == ACT_SILU) {
+#pragma unroll
+    for (int k = 0; k < NG; ++k) v[k] = silu(v[k]);
+  }
+  if (a.rscale) {
+    const float sc = a.rscale[col];
+#pragma unroll
+    for (int k = 0; k < NG; ++k) v[k] *= sc;
+  }
+  if (a.R) {
+    const float* rp = a.R + rb * a.ldr + col;
+    float rv[NG];
+#pragma unroll
+    for (int k = 0; k < NG; ++k) rv[k] = rp[roff(k) * a.ldr];
+#pragma unroll
+    for (int k = 0; k < NG; ++k) v[k] += rv[k];
+  }
+  float* yp = a.Y + rb * a.ldy + col;
+  if (a.Y2) {
+    float* y2 = a.Y2 + rb * a.ldy + col;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      yp[roff(k) * a.ldy] = v[k];
+      y2[roff(k) * a.ldy] = elu1(v[k]);
+    }
+  } else if (a.elu_out) {
+#pragma unroll
+    for (int k = 0; k < NG; ++k) yp[roff(k) * a.ldy] = elu1(v[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NG; ++k) yp[roff(k) * a.ldy] = v[k];
+  }
+}
+__device__ __forceinline__ void gemm_store_tile(const GemmArgs& a, const floatx16& acc, int tm0, int tn0, int h,
+                                                int r) {
+  float v[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) v[g] = acc[g];
+  gemm_store_fast<16>(a, v, 0, tm0, tn0, h, r);
+}
+
 // XCD-aware tile order. Workgroups are dealt round-robin to the 8 XCDs by linear id, so
 // consecutive ids land on different L2s and the N-tiles that share one A row block would each
 // miss in their own L2. Id L -> tile (L % 8) * (T / 8) + L / 8 gives every XCD a contiguous run
@@ -162,7 +221,7 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
   // Rows >= M were clamped to a valid row above: their garbage only reaches output rows that
   // are never stored, so the loads are unconditional (no exec-masked branches around them).
   (void)mvalid;
-  const bool elu = MODE == 1 && a.elu_in;
+  constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
   auto load = [&](int cc, float4 (&A)[4], float4 (&Bv)[4]) {
     const float* ap = a_ptr(cc << 5);
 #pragma unroll
@@ -246,18 +305,29 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
     for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[g];
     __syncthreads();
     constexpr int GPW = 16 / NW;  // output registers finished per wave
+    float vs[GPW];
 #pragma unroll
     for (int gg = 0; gg < GPW; ++gg) {
       const int g = wave * GPW + gg;
       float v = red[(0 * 16 + g) * 64 + lane];
 #pragma unroll
       for (int w = 1; w < NW; ++w) v += red[(w * 16 + g) * 64 + lane];
-      store(g, v);
+      vs[gg] = v;
+    }
+    if (ident && !a.partial && m0 + 32 <= a.M && n0 + 32 <= a.N) {
+      gemm_store_fast<GPW>(a, vs, wave * GPW, m0, n0, h, r);
+    } else {
+#pragma unroll
+      for (int gg = 0; gg < GPW; ++gg) store(wave * GPW + gg, vs[gg]);
     }
     if (MODE == 0 && a.fuse) splitk_combine(a, m0, n0, 32, red);
   } else if (wave_live) {
+    if (ident && !a.partial && m0 + 32 <= a.M && n0 + 32 <= a.N) {
+      gemm_store_tile(a, acc, m0, n0, h, r);
+    } else {
 #pragma unroll
-    for (int g = 0; g < 16; ++g) store(g, acc[g]);
+      for (int g = 0; g < 16; ++g) store(g, acc[g]);
+    }
   }
 }
 
@@ -334,7 +404,7 @@ __global__ __launch_bounds__(256) void k_gemm_lds(GemmArgs a) {
     for (int i = 0; i < NLD; ++i) {
       ra[i] = av_ok[i] ? *reinterpret_cast<const float4*>(a_src(i, k0)) : zero4;
       rb[i] = wv[i] ? *reinterpret_cast<const float4*>(wp[i] + k0) : zero4;
-      if (MODE == 1 && a.elu_in)
+      if (MODE == 2)
         ra[i] = make_float4(elu1(ra[i].x), elu1(ra[i].y), elu1(ra[i].z), elu1(ra[i].w));
     }
   };
@@ -474,54 +544,61 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
   }
   const float* Wp = a.W + (long)phase * a.w_phase_stride;
   const unsigned lds_base = lds_addr(lds);
-  // this lane's DMA sources: instruction j = wave + 4*ins covers rows j*RPI .. +RPI-1
+  // this lane's DMA sources: instruction j = wave + 4*ins covers rows j*RPI .. +RPI-1, all of
+  // them A rows or all of them W rows (TM % RPI == 0), so the A/W choice is wave-uniform.
+  // Conv A rows keep two base pointers (activation X and history H, both at time index 0 and
+  // this lane's column); a chunk picks one per lane with a select, never a branch.
   const float* src_base[IPW];
-  int src_row[IPW], src_bq[IPW], src_qq[IPW], src_col[IPW];
-  bool src_is_a[IPW];
+  const float* src_hist[IPW];
+  int src_qs[IPW];
 #pragma unroll
   for (int ins = 0; ins < IPW; ++ins) {
     const int j = wave + 4 * ins;
     const int row = (j < NINS ? j : 0) * RPI + lane / CPR;
     const int lcol = (lane % CPR) ^ swz<BK>(row);
-    src_col[ins] = 4 * lcol;
-    src_row[ins] = row;
-    src_is_a[ins] = row < TM;
-    if (row < TM) {
+    if ((j < NINS ? j : 0) * RPI < TM) {
       const int m = min(m0 + row, a.M - 1);  // rows >= M only feed output rows that are never stored
       if (MODE == 0) {
-        src_base[ins] = a.X + (long)m * a.ldx;
+        src_base[ins] = a.X + (long)m * a.ldx + 4 * lcol;
       } else {
-        src_bq[ins] = m / a.Tq;
-        src_qq[ins] = m - src_bq[ins] * a.Tq;
-        src_base[ins] = nullptr;
+        const int bq = m / a.Tq;
+        const int qq = m - bq * a.Tq;
+        src_qs[ins] = qq * a.stride_in - a.P;
+        src_base[ins] = a.X + (long)bq * a.T_in * a.ldx + 4 * lcol;
+        src_hist[ins] = a.H + ((long)bq * a.P + a.P) * a.cin + 4 * lcol;
       }
     } else {
       const int n = min(n0 + row - TM, a.Nw - 1);
-      src_base[ins] = Wp + (long)n * a.K;
+      src_base[ins] = Wp + (long)n * a.K + 4 * lcol;
     }
   }
+  const long ldx = a.ldx, hld = a.cin;
   auto issue = [&](int c, int buf) {
     const int k0 = c * BK;
+    int tap = 0, ci = 0;
+    if (MODE != 0) {  // scalar, once per chunk
+      tap = k0 / a.cin;
+      ci = k0 - tap * a.cin;
+    }
 #pragma unroll
     for (int ins = 0; ins < IPW; ++ins) {
       const int j = wave + 4 * ins;
       if (j >= NINS) break;  // wave-uniform
       const float* src;
-      if (MODE == 1 && src_is_a[ins]) {
-        const int tap = k0 / a.cin;
-        const int ci = k0 - tap * a.cin + src_col[ins];
-        const int t = src_qq[ins] * a.stride_in + tap - a.P;
-        src = t >= 0 ? a.X + ((long)src_bq[ins] * a.T_in + t) * a.ldx + ci
-                     : a.H + ((long)src_bq[ins] * a.P + (a.P + t)) * a.cin + ci;
+      if (MODE != 0 && j * RPI < TM) {
+        const int t = src_qs[ins] + tap;
+        const float* px = src_base[ins] + t * ldx + ci;
+        const float* ph = src_hist[ins] + t * hld + ci;
+        src = t >= 0 ? px : ph;
       } else {
-        src = src_base[ins] + k0 + src_col[ins];
+        src = src_base[ins] + k0;
       }
       // wave-uniform LDS base of this instruction; lane l -> + 16*l bytes
       const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)((buf * ROWS * BK + j * RPI * BK) * 4));
       glds16(src, dst);
     }
   };
-  const bool elu = MODE == 1 && a.elu_in;
+  constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
   floatx16 acc[TMW][TNW];
 #pragma unroll
   for (int i = 0; i < TMW; ++i)
@@ -590,6 +667,10 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
 #pragma unroll
     for (int jj = 0; jj < TNW; ++jj) {
       const int tm0 = m0 + 32 * TMW * wm + 32 * ii, tn0 = n0 + 32 * TNW * wn + 32 * jj;
+      if (ident && !a.partial && tm0 + 32 <= a.M && tn0 + 32 <= a.N) {
+        gemm_store_tile(a, acc[ii][jj], tm0, tn0, h, r);
+        continue;
+      }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int row = tm0 + (g & 3) + 8 * (g >> 2) + 4 * h;
@@ -667,7 +748,7 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.f;
-  const bool elu = MODE == 1 && a.elu_in;
+  constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
   auto load = [&](int cc, float4 (&A)[TM][4], float4 (&Bv)[TN][4]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -735,20 +816,30 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
 #pragma unroll
       for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[i][j][g];
       __syncthreads();
+      float vs[4];
 #pragma unroll
       for (int gg = 0; gg < 4; ++gg) {
         const int g = wave * 4 + gg;
         float v = red[(0 * 16 + g) * 64 + lane] + red[(1 * 16 + g) * 64 + lane];
         v += red[(2 * 16 + g) * 64 + lane];
         v += red[(3 * 16 + g) * 64 + lane];
+        vs[gg] = v;
+      }
+      if (ident && !a.partial && m0 + 32 * i + 32 <= a.M && n0 + 32 * j + 32 <= a.N) {
+        gemm_store_fast<4>(a, vs, wave * 4, m0 + 32 * i, n0 + 32 * j, h, r);
+        continue;
+      }
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int g = wave * 4 + gg;
         const int row = m0 + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
         const int col = n0 + 32 * j + r;
         if (row >= a.M || col >= a.N) continue;
         if (a.partial) {
-          a.partial[((long)z * a.M + row) * a.N + col] = v;
+          a.partial[((long)z * a.M + row) * a.N + col] = vs[gg];
           continue;
         }
-        gemm_store(a, row, col, phase, ident, v);
+        gemm_store(a, row, col, phase, ident, vs[gg]);
       }
     }
 }
@@ -948,7 +1039,9 @@ void gemm(const GemmArgs& a, int grid_z, hipStream_t s) {
     hipLaunchKernelGGL((k_gemm_w8<2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
     return;
   }
+  // MODE 1 = implicit-GEMM conv, MODE 2 = the same with ELU applied to A on load
   if (a.mode == 0) gemm_launch<0>(a, grid_z, s);
+  else if (a.elu_in) gemm_launch<2>(a, grid_z, s);
   else gemm_launch<1>(a, grid_z, s);
 }
 

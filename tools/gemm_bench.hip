@@ -152,6 +152,19 @@ int main(int argc, char** argv) {
   conv("rb.convtr3m T480 c128 N256", 480, 128, 1, 2, 256, 1, 1, rb);
   conv("rb.res3a T1920 c64 k3 N32", 1920, 64, 2, 3, 32, 1, 1, rb);
   conv("rb.res3b T1920 c32 k1 N64", 1920, 32, 0, 1, 64, 1, 1, rb);
+  // shape study: the convtr3m GEMM as a dense GEMM, and the same flops at long K
+  dense("study.dense M15360 N256 K256", 15360, 256, 256, rb);
+  dense("study.dense M3840 N256 K1024", 3840, 256, 1024, rb);
+  dense("study.dense M1920 N256 K2048", 1920, 256, 2048, rb);
+  dense("study.dense M30720 N256 K128", 30720, 256, 128, rb);
+  std::vector<std::pair<int, int>> lk = {{6, 1}, {21, 1}, {22, 1}};
+  dense("kstudy M3840 N256 K32", 3840, 256, 32, lk);
+  dense("kstudy M3840 N256 K64", 3840, 256, 64, lk);
+  dense("kstudy M3840 N256 K128", 3840, 256, 128, lk);
+  dense("kstudy M3840 N256 K256", 3840, 256, 256, lk);
+  dense("kstudy M3840 N256 K512", 3840, 256, 512, lk);
+  dense("kstudy M256 N256 K32", 256, 256, 32, lk);
+  dense("kstudy M256 N256 K1024", 256, 256, 1024, lk);
   dense("rb.mimi.qkv M512 N1536 K512", 16 * B, 1536, 512, rbk);
   dense("rb.mimi.ff1 M512 N2048 K512", 16 * B, 2048, 512, rbk);
   dense("rb.mimi.ff2 M512 N512 K2048", 16 * B, 512, 2048, rbk);
