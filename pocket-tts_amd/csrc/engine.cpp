@@ -132,6 +132,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
     trb_[i] = dalloc((size_t)RATIOS[i] * ch);
   }
   temb_ = dalloc((size_t)lsd_ * FD);
+  rope_ = dalloc((size_t)max_ctx_ * 64);
   temb_tmp_ = dalloc((size_t)2 * lsd_ * FD);
 
   PTTS_HIP(hipHostMalloc((void**)&h_pcm_, sizeof(float) * B * FRAME, hipHostMallocDefault));
@@ -201,6 +202,7 @@ void Engine::finalize() {
     tw.alpha[i] = W(L_.te_alpha[i]);
   }
   time_embeddings(tw, lsd_, temb_tmp_, temb_, stream_);
+  rope_table(rope_, max_ctx_, stream_);
   for (int i = 0, ch = MD / 2; i < 3; ++i, ch /= 2)  // bias of the phase-merged transposed convs
     for (int p = 0; p < RATIOS[i]; ++p)
       PTTS_HIP(hipMemcpyAsync(trb_[i] + (size_t)p * ch, W(L_.dtr_b[i]), sizeof(float) * ch, hipMemcpyDeviceToDevice,
@@ -412,7 +414,8 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
     if (qg == 1) {  // step: slab sum + RoPE + KV append fused into the attention kernel
       const float* P = partial_;
       float* O = o_;
-      ops.push_back({p + ".attention", [=](hipStream_t s) { attention_step_qkv(P, S, M, NH, map, kv, O, s); }});
+      const float* rope = rope_;
+      ops.push_back({p + ".attention", [=](hipStream_t s) { attention_step_qkv(P, S, M, NH, map, kv, rope, O, s); }});
     } else {
       {
         const float* P = partial_;

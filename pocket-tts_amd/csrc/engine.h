@@ -142,6 +142,7 @@ class Engine {
   int out_rows_ = 0;         // rows that frame covers
   int front_rows_ = 0;       // rows of the last front part
   float *temb_ = nullptr, *temb_tmp_ = nullptr;
+  float* rope_ = nullptr;  // FlowLM RoPE cos/sin table [max_ctx][32][2]
 
   // pinned host staging
   float* h_pcm_ = nullptr;

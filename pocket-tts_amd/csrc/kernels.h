@@ -128,7 +128,11 @@ void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window
                hipStream_t s);
 // One-query-per-row step attention fused with the QKV slab sum, RoPE and KV append (positions
 // must not wrap: FlowLM cache).
-void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStore kv, float* O, hipStream_t s);
+void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStore kv, const float* rope, float* O,
+                        hipStream_t s);
+// RoPE table (rope.rs:9-60): tab[pos][2i] = cos(pos * f_i), tab[pos][2i+1] = sin(pos * f_i),
+// f_i = exp(-ln(1e4) * 2i / 64), i < 32, pos < npos - the values the step kernels would compute.
+void rope_table(float* tab, int npos, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // Per-slot generation bookkeeping (device resident so the step can be replayed as a graph).

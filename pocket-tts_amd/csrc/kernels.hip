@@ -1664,7 +1664,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 // The rows (l/16) are combined once per wave at the end. Each wave issues its first block's
 // loads before the QKV/RoPE phase: the cached keys do not depend on this step's token.
 __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict__ P, int S, int M, int nh, RowMap mp,
-                                                         KvStore kv, float* __restrict__ O) {
+                                                         KvStore kv, const float* __restrict__ rope,
+                                                         float* __restrict__ O) {
   __shared__ float s_m[4], s_l[4];
   __shared__ __attribute__((aligned(16))) float s_o[4][64];
   __shared__ __attribute__((aligned(16))) float s_qkv[3][64];
@@ -1699,9 +1700,8 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
   __syncthreads();
   if (tid < 64) {  // rotate the (2i, 2i+1) pairs of q (tid < 32) and k (tid >= 32)
     const int i = tid & 31, part = tid >> 5;
-    const float freq = expf((float)i * (-logf(10000.0f) * 2.0f / 64.0f));
-    const float ang = (float)qp * freq;
-    const float cs = cosf(ang), sn = sinf(ang);
+    const float2 cssn = *reinterpret_cast<const float2*>(rope + (long)qp * 64 + 2 * i);  // table of rope_table()
+    const float cs = cssn.x, sn = cssn.y;
     const float x0 = s_qkv[part][2 * i], x1 = s_qkv[part][2 * i + 1];
     const float y0 = x0 * cs - x1 * sn, y1 = x0 * sn + x1 * cs;  // one wave: all reads precede the writes
     s_qkv[part][2 * i] = y0;
@@ -1780,8 +1780,23 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
   }
 }
 
-void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStore kv, float* O, hipStream_t s) {
-  hipLaunchKernelGGL(k_attn_decode_qkv, dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, O);
+void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStore kv, const float* rope, float* O,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_attn_decode_qkv, dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
+}
+
+__global__ __launch_bounds__(256) void k_rope_table(float* tab, int npos) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)npos * 32) return;
+  const int pos = (int)(idx >> 5), i = (int)(idx & 31);
+  const float freq = expf((float)i * (-logf(10000.0f) * 2.0f / 64.0f));
+  const float ang = (float)pos * freq;
+  tab[(long)pos * 64 + 2 * i] = cosf(ang);
+  tab[(long)pos * 64 + 2 * i + 1] = sinf(ang);
+}
+
+void rope_table(float* tab, int npos, hipStream_t s) {
+  hipLaunchKernelGGL(k_rope_table, dim3((unsigned)((npos * 32L + 255) / 256)), dim3(256), 0, s, tab, npos);
 }
 
 void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O, hipStream_t s) {
