@@ -77,7 +77,9 @@ Engine::Engine(const ptts_engine_config& cfg) {
     flags_[q] = (FrameFlags*)dalloc((size_t)2 * B);
     pcm_[q] = dalloc((size_t)B * FRAME);
   }
-  mpartial_ = dalloc((size_t)2 * B * UP * 3 * MD);  // back part's own split-K slabs (Mimi QKV)
+  // back part's own split-K slabs: Mimi QKV (2 slabs), Mimi ff2 (4), SEANet conv0 (8), convtr0 (4)
+  mpcap_ = std::max({(size_t)2 * B * UP * 3 * MD, (size_t)8 * B * UP * MD, (size_t)4 * B * UP * RATIOS[0] * (MD / 2)});
+  mpartial_ = dalloc(mpcap_);
 
   // streaming conv histories (SEANetDecoder, seanet.rs:307-402): source T, channels, rows kept
   const int hT[8] = {16, 16, 96, 96, 480, 480, 1920, 1920};
@@ -367,8 +369,12 @@ void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float
 void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float* X, int B, int T_in, int cin,
                      const float* H, int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases,
                      const float* bias, const float* R, float* Y, int T_out, int tstride, int layout, int elu_out,
-                     float* Y2) {
+                     float* Y2, int ksplit) {
   PTTS_REQUIRE(cin % 32 == 0, "conv cin must be a multiple of 32");
+  // ksplit > 1: single-phase conv on an LDS-DMA tile, K split into ksplit partial slabs in the
+  // back part's slab buffer; the caller adds the row-reduce epilogue
+  PTTS_REQUIRE(ksplit == 1 || (phases == 1 && layout >= 6 && layout != 9 && layout != 10 && layout < 17),
+               "K-split convs need a single-phase LDS-DMA tile");
   GemmArgs a{};
   a.mode = 1;
   a.layout = layout;
@@ -397,8 +403,15 @@ void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float*
   a.out_tstride = tstride;
   a.elu_out = elu_out;
   a.Y2 = Y2;
-  ops.push_back({name, [a, phases](hipStream_t s) { gemm(a, phases, s); }, 2.0 * a.M * a.N * a.K * phases,
-                 4.0 * ((double)phases * a.N * a.K + (double)B * T_in * cin +
+  const int nph = phases;
+  if (ksplit > 1) {
+    PTTS_REQUIRE((size_t)ksplit * a.M * a.N <= mpcap_, "back split-K slab buffer too small");
+    a.S = ksplit;
+    a.partial = mpartial_;
+    phases = ksplit;  // grid z
+  }
+  ops.push_back({name, [a, phases](hipStream_t s) { gemm(a, phases, s); }, 2.0 * a.M * a.N * a.K * nph,
+                 4.0 * ((double)nph * a.N * a.K + (double)B * T_in * cin +
                         (double)B * T_out * cout * ((R ? 2 : 1) + (Y2 ? 1 : 0)))});
 }
 
@@ -678,7 +691,38 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
     }
     dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
              fat ? 15 : 0);
-    dense_op(ops, p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, nullptr, ACT_NONE, W(t.ls2), mx_, mx_);
+    if (fat) {  // K = 2048: 64x64 LDS-DMA tiles, 4-way split-K; LayerScale + residual in the reduce
+      const int S = 4;
+      GemmArgs a{};
+      a.mode = 0;
+      a.layout = 6;
+      a.M = MR;
+      a.N = MD;
+      a.K = MFF;
+      a.Nw = MD;
+      a.X = mu_;
+      a.ldx = MFF;
+      a.W = W(t.l2);
+      a.S = S;
+      a.partial = mpartial_;
+      PTTS_REQUIRE((size_t)S * MR * MD <= mpcap_, "back split-K slab buffer too small");
+      ops.push_back({p + ".ff2_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * MD * MFF,
+                     4.0 * ((double)MD * MFF + (double)MR * MFF + 2.0 * MR * MD)});
+      RowReduceArgs r{};
+      r.P = mpartial_;
+      r.S = S;
+      r.M = MR;
+      r.N = MD;
+      r.gate = W(t.ls2);  // per-column LayerScale: gate row stride 0
+      r.ldg = 0;
+      r.R = mx_;
+      r.ldr = MD;
+      r.Y = mx_;
+      r.ldy = MD;
+      ops.push_back({p + ".ff2_reduce", [r](hipStream_t s) { row_reduce(r, s); }});
+    } else {
+      dense_op(ops, p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, nullptr, ACT_NONE, W(t.ls2), mx_, mx_);
+    }
     if (l + 1 < MNL) {
       const float *x = mx_, *w = W(L_.mdec[l + 1].n1w), *b = W(L_.mdec[l + 1].n1b);
       float* h = mh_;
@@ -693,8 +737,23 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
   // 2-tap conv over rows (x[q-1], x[q]) whose output row q is the r time rows q*r .. q*r+r-1 of
   // the channels-last output, N = r * Cout (packed [r][Cout][2][Cin] = [r*Cout][2*Cin]).
   const bool big = B >= 16;
-  conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, W(L_.dc0_b), nullptr, a0_,
-          16, 1, 0, 1);
+  if (big) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the reduce
+    conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
+            nullptr, 16, 1, 6, 0, nullptr, 8);
+    RowReduceArgs r{};
+    r.P = mpartial_;
+    r.S = 8;
+    r.M = B * 16;
+    r.N = 512;
+    r.bias = W(L_.dc0_b);
+    r.act = ACT_ELU;
+    r.Y = a0_;
+    r.ldy = 512;
+    ops.push_back({"seanet.conv0_reduce", [r](hipStream_t s) { row_reduce(r, s); }});
+  } else {
+    conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, W(L_.dc0_b), nullptr,
+            a0_, 16, 1, 0, 1);
+  }
   const float* cin_buf = a0_;
   int T = 16, ch = 512;
   for (int i = 0; i < 3; ++i) {
@@ -702,10 +761,25 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
     const std::string p = "seanet.up" + std::to_string(i);
     // per-stage tiles (tools/gemm_bench.hip, rb.* cases, B = 32)
     const int l_tr = big ? (i == 0 ? 20 : 6) : 0;
-    const int l_r3 = big ? (i == 0 ? 18 : (i == 1 ? 20 : 6)) : 0;
+    const int l_r3 = big ? (i == 0 ? 18 : (i == 1 ? 20 : 14)) : 0;
     const int l_r1 = big ? 6 : 0;
-    conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 0, W(L_.dtr_w[i]), r * (ch / 2), 2, 1,
-            trb_[i], nullptr, cb_[i], T, 1, l_tr, 0, ce_[i]);
+    if (big && i == 0) {  // M = 16 B rows only: 4-way split-K fills the chip; bias + dual store in the reduce
+      conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1], 1, 1, 0, W(L_.dtr_w[0]), r * (ch / 2), 2, 1, nullptr,
+              nullptr, nullptr, T, 1, 6, 0, nullptr, 4);
+      RowReduceArgs rr{};
+      rr.P = mpartial_;
+      rr.S = 4;
+      rr.M = B * T;
+      rr.N = r * (ch / 2);
+      rr.bias = trb_[0];
+      rr.Y = cb_[0];
+      rr.Y2 = ce_[0];
+      rr.ldy = r * (ch / 2);
+      ops.push_back({p + ".convtr_reduce", [rr](hipStream_t s) { row_reduce(rr, s); }});
+    } else {
+      conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 0, W(L_.dtr_w[i]), r * (ch / 2), 2, 1,
+              trb_[i], nullptr, cb_[i], T, 1, l_tr, 0, ce_[i]);
+    }
     T *= r;
     ch /= 2;
     conv_op(ops, p + ".res_conv3", ce_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 0, W(L_.dra_w[i]), ch / 2, 3, 1,

@@ -76,7 +76,7 @@ class Engine {
   void conv_op(std::vector<Op>& ops, const std::string& name, const float* X, int B, int T_in, int cin, const float* H,
                int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases, const float* bias,
                const float* R, float* Y, int T_out, int tstride, int layout = 0, int elu_out = 0,
-               float* Y2 = nullptr);
+               float* Y2 = nullptr, int ksplit = 1);
   void dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N, int K,
                 const float* bias, int act, const float* rscale, const float* R, float* Y,
                 int layout = 0);
@@ -126,6 +126,7 @@ class Engine {
   FrameFlags* flags_[2] = {};
   float* pcm_[2] = {};
   float* mpartial_ = nullptr;
+  size_t mpcap_ = 0;
   // in-launch split-K combine (front part only; the back part never uses it)
   static constexpr int TICKETS = 4096, ROW_TICKETS = 256;
   int* tickets_ = nullptr;

@@ -16,7 +16,7 @@ namespace ptts {
 // W rows are padded to a multiple of 32; K must be a multiple of 32 (and cin % 32 == 0).
 // grid = (ceil(N/32), ceil(M/32), S) ; S > 1 = split-K partial slabs (mode 0 only),
 // or the transposed-conv phase index (mode 1).
-enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2 };
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_ELU = 3 };
 
 // ---------------------------------------------------------------------------------------------
 // Row reduce / epilogue of a split-K GEMM, fused with residual, gate, LayerNorm and modulate:
@@ -34,6 +34,7 @@ struct RowReduceArgs {
   long ldr;
   float* Y;  // [M][ldy] or nullptr
   long ldy;
+  float* Y2;  // also store elu(v) here ([M][ldy]), or nullptr (SEANet dual raw / ELU'd output)
   float* euler;  // cur [M][32]: cur += v * euler_scale (N must be 32)
   float euler_scale;
   // LayerNorm of the final row (N <= 1024)

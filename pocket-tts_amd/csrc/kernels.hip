@@ -1066,7 +1066,7 @@ __device__ __forceinline__ float4 f4mul(float4 a, float4 b) {
   return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
 }
 __device__ __forceinline__ float act1(float x, int act) {
-  return act == ACT_GELU ? gelu_tanh(x) : (act == ACT_SILU ? silu(x) : x);
+  return act == ACT_GELU ? gelu_tanh(x) : (act == ACT_SILU ? silu(x) : (act == ACT_ELU ? elu1(x) : x));
 }
 
 // Every load of a thread (its S slab float4s and the bias / gate / residual operands) is issued
@@ -1095,6 +1095,7 @@ __device__ __forceinline__ float4 rr_value(const RowReduceArgs& a, int m, int n)
 }
 __device__ __forceinline__ void rr_store(const RowReduceArgs& a, int m, int n, float4 v) {
   if (a.Y) *reinterpret_cast<float4*>(a.Y + (long)m * a.ldy + n) = v;
+  if (a.Y2) *reinterpret_cast<float4*>(a.Y2 + (long)m * a.ldy + n) = make_float4(elu1(v.x), elu1(v.y), elu1(v.z), elu1(v.w));
   if (a.euler) {
     float4* e = reinterpret_cast<float4*>(a.euler + (long)m * 32 + n);
     const float sc = a.euler_scale;

@@ -157,6 +157,18 @@ int main(int argc, char** argv) {
   dense("study.dense M3840 N256 K1024", 3840, 256, 1024, rb);
   dense("study.dense M1920 N256 K2048", 1920, 256, 2048, rb);
   dense("study.dense M30720 N256 K128", 30720, 256, 128, rb);
+  std::vector<std::pair<int, int>> kv = {{0, 1}, {9, 1}, {10, 1}, {17, 1}, {18, 1}, {6, 2}, {6, 4}, {6, 8},
+                                         {12, 4}, {22, 4}, {22, 8}, {23, 8}, {25, 8}, {27, 8}};
+  conv("c0.conv0 T16 c512 k7 N512", 16, 512, 6, 7, 512, 1, 1, kv);
+  std::vector<std::pair<int, int>> kv2 = {{6, 1}, {6, 2}, {6, 4}, {20, 1}, {22, 1}, {22, 2}, {22, 4}, {12, 2},
+                                          {27, 2}, {25, 2}, {23, 2}};
+  conv("c1.convtr1m T16 c512 N1536", 16, 512, 1, 2, 1536, 1, 1, kv2);
+  std::vector<std::pair<int, int>> kv3 = {{6, 1}, {14, 1}, {3, 1}, {0, 1}, {24, 1}, {25, 1}, {12, 1}, {11, 1}};
+  conv("c1.res3a T1920 c64 k3 N32", 1920, 64, 2, 3, 32, 1, 1, kv3);
+  conv("c1.res3b T1920 c32 k1 N64", 1920, 32, 0, 1, 64, 1, 1, kv3);
+  conv("c1.res2a T480 c128 k3 N64", 480, 128, 2, 3, 64, 1, 1, kv3);
+  conv("c0.res1a T96 c256 k3 N128", 96, 256, 2, 3, 128, 1, 1, kv);
+  dense("c0.mimi.ff2 M512 N512 K2048", 16 * B, 512, 2048, kv);
   std::vector<std::pair<int, int>> lk = {{6, 1}, {21, 1}, {22, 1}};
   dense("kstudy M3840 N256 K32", 3840, 256, 32, lk);
   dense("kstudy M3840 N256 K64", 3840, 256, 64, lk);
@@ -192,7 +204,8 @@ int main(int argc, char** argv) {
       const int bk = (layout == 8 || layout == 15 || layout == 16) ? 64 : 32;
       if (layout >= 6 && (a.K % bk != 0 || (a.mode == 1 && a.cin % bk != 0))) continue;
       int gz = c.phases;
-      if (S > 1 && a.mode == 1 && (c.phases > 1 || layout < 21)) continue;
+      if (S > 1 && a.mode == 1 && (c.phases > 1 || layout < 6 || (layout >= 9 && layout <= 10) ||
+                                   (layout >= 17 && layout <= 20))) continue;
       if (S > 1) {  // dense split-K, or K-sliced single-phase conv (register-blocked LDS-DMA)
         if (a.K / bk < S) continue;
         v.S = S;
