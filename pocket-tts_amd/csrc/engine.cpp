@@ -650,30 +650,11 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
     const Layout::TL& t = L_.mdec[l];
     const std::string p = "mimi.l" + std::to_string(l);
     KvStore kv{ring_ + (long)l * ring_layer_, ring_slot_, RING};
-    // fat GEMMs (B*16 rows): 64x64 LDS-DMA tiles once there are enough rows to fill the chip;
-    // QKV runs 2-way split-K and the RoPE/append kernel sums the two slabs
+    // fat GEMMs (B*16 rows): LDS-DMA tiles once there are enough rows to fill the chip
     const bool fat = MR >= 256;
-    if (fat) {
-      int S = 2;
-      GemmArgs a{};
-      a.mode = 0;
-      a.layout = 12;
-      a.M = MR;
-      a.N = 3 * MD;
-      a.K = MD;
-      a.Nw = 3 * MD;
-      a.X = mh_;
-      a.ldx = MD;
-      a.W = W(t.in_proj);
-      a.S = S;
-      a.partial = mpartial_;
-      ops.push_back({p + ".qkv_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * 3 * MD * MD,
-                     4.0 * (3.0 * MD * MD + (double)MR * MD + (double)S * MR * 3 * MD)});
-      const float* P = mpartial_;
-      float* Q = mq_;
-      ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(P, S, nullptr, MR, MNH, mmap, kv, Q, s); }});
-    } else {
-      dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_);
+    {  // QKV: one pass, 64x64 LDS-DMA BK 64 tiles once there are enough rows (tools/gemm_bench.hip c2.mimi.qkv)
+      dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_,
+               fat ? 15 : 0);
       const float* qkv = mqkv_;
       float* Q = mq_;
       ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(nullptr, 0, qkv, MR, MNH, mmap, kv, Q, s); }});
@@ -760,7 +741,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
     // per-stage tiles (tools/gemm_bench.hip, rb.* cases, B = 32)
-    const int l_tr = big ? (i == 0 ? 20 : 6) : 0;
+    const int l_tr = big ? (i == 0 ? 20 : (i == 1 ? 13 : 22)) : 0;
     const int l_r3 = big ? (i == 0 ? 18 : (i == 1 ? 20 : 14)) : 0;
     const int l_r1 = big ? 6 : 0;
     if (big && i == 0) {  // M = 16 B rows only: 4-way split-K fills the chip; bias + dual store in the reduce

@@ -167,6 +167,14 @@ int main(int argc, char** argv) {
   conv("c1.res3a T1920 c64 k3 N32", 1920, 64, 2, 3, 32, 1, 1, kv3);
   conv("c1.res3b T1920 c32 k1 N64", 1920, 32, 0, 1, 64, 1, 1, kv3);
   conv("c1.res2a T480 c128 k3 N64", 480, 128, 2, 3, 64, 1, 1, kv3);
+  std::vector<std::pair<int, int>> kv4 = {{6, 1}, {6, 2}, {22, 1}, {22, 2}, {12, 1}, {12, 2}, {11, 1}, {27, 1},
+                                          {13, 1}, {16, 1}, {15, 1}};
+  conv("c2.convtr2m T96 c256 N640", 96, 256, 1, 2, 640, 1, 1, kv4);
+  conv("c2.convtr3m T480 c128 N256", 480, 128, 1, 2, 256, 1, 1, kv4);
+  conv("c2.res1a T96 c256 k3 N128", 96, 256, 2, 3, 128, 1, 1, kv4);
+  conv("c2.res1b T96 c128 k1 N256", 96, 128, 0, 1, 256, 1, 1, kv4);
+  dense("c2.mimi.qkv M512 N1536 K512", 16 * B, 1536, 512, kv4);
+  dense("c2.mimi.ff1 M512 N2048 K512", 16 * B, 2048, 512, kv4);
   conv("c0.res1a T96 c256 k3 N128", 96, 256, 2, 3, 128, 1, 1, kv);
   dense("c0.mimi.ff2 M512 N512 K2048", 16 * B, 512, 2048, kv);
   std::vector<std::pair<int, int>> lk = {{6, 1}, {21, 1}, {22, 1}};
