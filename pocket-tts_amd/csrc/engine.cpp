@@ -276,6 +276,11 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   } else if (M >= 256) {  // prefill passes: MFMA-bound, 64x64 LDS-DMA tiles, no split
     layout = 12;
     S = 1;
+  } else if (M <= 64 && K >= 4096) {  // FlowLM ff2: 8 slabs (tools/gemm_bench.hip flow.ff2: 8.5 -> 7.3 us)
+    S = 8;
+  } else if (M <= 64 && N <= 512 && K == 512) {  // flow-head MLPs: 8 waves, 8 slabs (head.mlp: 3.9 -> 3.4 us)
+    layout = 9;
+    S = 8;
   }
   // quantized FlowLM weights on the step path: stream int8 codes (k_gemm_w8, 32x64 tiles, the
   // smallest power-of-two split reaching 256 workgroups with >= 4 K chunks per slice). Only the

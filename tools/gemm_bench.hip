@@ -115,7 +115,8 @@ int main(int argc, char** argv) {
     a.T_out = T_in * tstride; a.out_tstride = tstride;
     cases.push_back({nm, a, phases, v});
   };
-  std::vector<std::pair<int, int>> skinny = {{0, 8}, {13, 8}, {0, 1}, {0, 2}, {13, 1}, {13, 2}, {9, 1}, {9, 2}};
+  std::vector<std::pair<int, int>> skinny = {{0, 8}, {0, 16}, {7, 8}, {7, 16}, {13, 8}, {13, 16}, {9, 8}, {9, 16},
+                                             {10, 8}, {10, 16}, {17, 8}, {17, 16}, {0, 4}, {9, 4}};
   std::vector<std::pair<int, int>> fat = {{0, 1}, {18, 1}, {19, 1}, {20, 1}, {20, 2}, {6, 1}, {12, 1}, {12, 2},
                                           {13, 1}, {14, 1}};
   dense("flow.qkv M32 N3072 K1024", B, 3072, 1024, skinny);
