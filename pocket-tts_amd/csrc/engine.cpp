@@ -705,11 +705,19 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
       r.ldr = MD;
       r.Y = mx_;
       r.ldy = MD;
+      if (l + 1 < MNL) {  // the next layer's norm1 on the reduced rows (no separate LayerNorm launch)
+        r.ln = 1;
+        r.ln_w = W(L_.mdec[l + 1].n1w);
+        r.ln_b = W(L_.mdec[l + 1].n1b);
+        r.eps = 1e-5f;
+        r.Hout = mh_;
+        r.ldh = MD;
+      }
       ops.push_back({p + ".ff2_reduce", [r](hipStream_t s) { row_reduce(r, s); }});
     } else {
       dense_op(ops, p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, nullptr, ACT_NONE, W(t.ls2), mx_, mx_);
     }
-    if (l + 1 < MNL) {
+    if (l + 1 < MNL && !fat) {
       const float *x = mx_, *w = W(L_.mdec[l + 1].n1w), *b = W(L_.mdec[l + 1].n1b);
       float* h = mh_;
       ops.push_back({p + ".ln1_next", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
