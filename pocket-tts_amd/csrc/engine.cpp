@@ -141,6 +141,11 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_HIP(hipHostMalloc((void**)&h_eos_, sizeof(float) * B, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_lat_, sizeof(float) * B * LDIM, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_fl_, sizeof(FrameFlags) * B, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_slots_, sizeof(int) * B, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_st_, sizeof(SlotState) * B, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_fp_, sizeof(int) * B, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_ids_, sizeof(int) * PREFILL, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_tab_, sizeof(int) * PREFILL, hipHostMallocDefault));
   PTTS_HIP(hipStreamCreateWithFlags(&stream_be_, hipStreamNonBlocking));
   for (int q = 0; q < 2; ++q) {
     PTTS_HIP(hipEventCreateWithFlags(&ev_front_[q], hipEventDisableTiming));
@@ -176,6 +181,8 @@ Engine::~Engine() {
   if (h_eos_) (void)hipHostFree(h_eos_);
   if (h_lat_) (void)hipHostFree(h_lat_);
   if (h_fl_) (void)hipHostFree(h_fl_);
+  for (void* hp : {(void*)h_slots_, (void*)h_st_, (void*)h_fp_, (void*)h_ids_, (void*)h_tab_})
+    if (hp) (void)hipHostFree(hp);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -1269,9 +1276,15 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     s.seed = p.seed;
     fp[i] = voices[i]->F + n_ids[i];
   }
-  PTTS_HIP(hipMemcpyAsync(admit_slots_, slots, sizeof(int) * n, hipMemcpyHostToDevice, stream_));
-  PTTS_HIP(hipMemcpyAsync(admit_st_, st.data(), sizeof(SlotState) * n, hipMemcpyHostToDevice, stream_));
-  PTTS_HIP(hipMemcpyAsync(admit_fpos_, fp.data(), sizeof(int) * n, hipMemcpyHostToDevice, stream_));
+  // staged through pinned buffers so the copies are truly asynchronous: admission returns with
+  // the prefill still running and the caller's first step queued right behind it (no host
+  // round trip in between); the sync() above guarantees the staging is free again
+  memcpy(h_slots_, slots, sizeof(int) * n);
+  memcpy(h_st_, st.data(), sizeof(SlotState) * n);
+  memcpy(h_fp_, fp.data(), sizeof(int) * n);
+  PTTS_HIP(hipMemcpyAsync(admit_slots_, h_slots_, sizeof(int) * n, hipMemcpyHostToDevice, stream_));
+  PTTS_HIP(hipMemcpyAsync(admit_st_, h_st_, sizeof(SlotState) * n, hipMemcpyHostToDevice, stream_));
+  PTTS_HIP(hipMemcpyAsync(admit_fpos_, h_fp_, sizeof(int) * n, hipMemcpyHostToDevice, stream_));
   {
     ResetArgs r{};
     for (int i = 0; i < 8; ++i) {
@@ -1311,8 +1324,11 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
   }
   for (size_t c0 = 0; c0 < tab.size(); c0 += PREFILL) {
     const int T = (int)std::min<size_t>(PREFILL, tab.size() - c0);  // PREFILL % 16 == 0
-    PTTS_HIP(hipMemcpyAsync(ids_dev_, rid.data() + c0, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
-    PTTS_HIP(hipMemcpyAsync(rowtab_dev_, tab.data() + c0, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    if (c0 > 0) PTTS_HIP(hipStreamSynchronize(stream_));  // ids / row table / staging reused by this pass
+    memcpy(h_ids_, rid.data() + c0, sizeof(int) * T);
+    memcpy(h_tab_, tab.data() + c0, sizeof(int) * T);
+    PTTS_HIP(hipMemcpyAsync(ids_dev_, h_ids_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(rowtab_dev_, h_tab_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
     std::vector<Op> ops;
     {
       const int* idp = ids_dev_;
@@ -1330,9 +1346,7 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     RowMap map{0, 1, 0, nullptr, rowtab_dev_};
     flow_layers(ops, T, map, 16, false, "prefill");
     run_ops(ops);
-    PTTS_HIP(hipStreamSynchronize(stream_));  // ids / row table are reused by the next pass
   }
-  PTTS_HIP(hipStreamSynchronize(stream_));
 }
 
 void Engine::slot_close(int slot) {

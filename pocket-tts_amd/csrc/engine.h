@@ -150,6 +150,8 @@ class Engine {
   float* h_eos_ = nullptr;
   float* h_lat_ = nullptr;
   FrameFlags* h_fl_ = nullptr;
+  int *h_slots_ = nullptr, *h_fp_ = nullptr, *h_ids_ = nullptr, *h_tab_ = nullptr;  // admission staging
+  SlotState* h_st_ = nullptr;
 
   std::map<int, hipGraphExec_t> graphs_;
   std::map<int, hipGraph_t> graph_defs_;
