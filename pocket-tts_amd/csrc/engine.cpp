@@ -69,7 +69,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   st_ = (SlotState*)dalloc((sizeof(SlotState) * B + 3) / 4);
   lat_in_ = dalloc((size_t)B * LDIM);
   cur_ = dalloc((size_t)B * LDIM);
-  qprev_ = dalloc((size_t)B * MD);
+  qprev_ = dalloc((size_t)2 * B * MD);  // [parity][slot][512], see quant_upsample
   eos_ = dalloc(B);
   for (int q = 0; q < 2; ++q) {  // front -> back hand-off, one set per step parity
     lat_out_[q] = dalloc((size_t)B * LDIM);
@@ -651,10 +651,12 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
     const float *lat = lat_out_[par], *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w),
                 *wu = W(L_.up_w);
     const float *lw = W(L_.mdec[0].n1w), *lb = W(L_.mdec[0].n1b);
-    float *qp = qprev_, *x = mx_, *h = mh_;
+    const float* qin = qprev_ + (size_t)(par ^ 1) * max_slots_ * MD;
+    float* qout = qprev_ + (size_t)par * max_slots_ * MD;
+    float *x = mx_, *h = mh_;
     const FrameFlags* fl = flags_[par];
     ops.push_back({"mimi.quant_upsample",
-                   [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qp, fl, x, h, lw, lb, s); }});
+                   [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qin, qout, fl, x, h, lw, lb, s); }});
   }
   const int MR = B * UP;
   RowMap mmap{0, UP, 0, mpos_};
@@ -1291,9 +1293,11 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
       r.buf[i] = hist_[i];
       r.per_slot[i] = (long)hist_P_[i] * hist_C_[i];
     }
-    r.buf[8] = qprev_;
+    r.buf[8] = qprev_;  // both parity halves of the overlap-add history
     r.per_slot[8] = MD;
-    r.nb = 9;
+    r.buf[9] = qprev_ + (size_t)max_slots_ * MD;
+    r.per_slot[9] = MD;
+    r.nb = 10;
     r.slots = admit_slots_;
     r.n = n;
     r.lat_in = lat_in_;

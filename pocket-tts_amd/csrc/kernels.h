@@ -176,11 +176,11 @@ struct FrontCommitArgs {
 void front_commit(const FrontCommitArgs& a, hipStream_t s);
 
 // Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0.
-// latent [B][32] -> x [B*16][512], h = LN(x); qprev [B][512] carries the overlap-add history
-// (advanced only for rows whose frame is valid).
+// latent [B][32] -> x [B*16][512], h = LN(x); the overlap-add history [B][512] is read from
+// qprev_in and written to qprev_out (frame-parity double buffer; carried over for invalid rows).
 void quant_upsample(const float* latent, int B, const float* emb_std, const float* emb_mean,
-                    const float* wq, const float* wup, float* qprev, const FrameFlags* fl, float* x, float* h,
-                    const float* ln_w, const float* ln_b, hipStream_t s);
+                    const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
+                    const FrameFlags* fl, float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s);
 
 // End of the back part, for rows with a valid frame: copy the last P rows of each conv input
 // into its history, advance the Mimi position.

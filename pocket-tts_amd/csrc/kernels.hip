@@ -1877,25 +1877,31 @@ void flow_cond(const float* P, int S, int B, const float* bias, const float* tem
 // The transposed conv's overlap-add `partial` (conv.rs:202-267) equals qprev * W[:, 16 + r],
 // so the kernel keeps the previous frame's quantized vector instead.
 // =============================================================================================
+// Denorm + quantizer 1x1 conv (mimi.rs:8-37) + depthwise ConvTrUpsample1d k32 s16
+// (conv.rs:315-346: frame row r = q*w[r] + qprev*w[16+r], the overlap-add of the previous frame's
+// tail) + norm1 of Mimi layer 0. One workgroup per (row b, 4 of the 16 output rows): 4x the
+// workgroups of a per-row kernel, each loading only its rows' upsample taps, one LayerNorm row
+// per wave. The overlap-add history is double-buffered by frame parity (read qprev_in, write
+// qprev_out), so the four workgroups of a row never race on it; a row without a valid frame
+// carries its history over unchanged.
 __global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, const float* emb_std,
                                                         const float* emb_mean, const float* wq, const float* wup,
-                                                        float* qprev, const FrameFlags* fl, float* x, float* h,
-                                                        const float* ln_w, const float* ln_b) {
+                                                        const float* qprev_in, float* qprev_out, const FrameFlags* fl,
+                                                        float* x, float* h, const float* ln_w, const float* ln_b) {
   __shared__ float sz[32];
-  __shared__ float sx[16 * 512];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ float sx[4 * 512];
+  const int b = blockIdx.x, r0 = blockIdx.y * 4, tid = threadIdx.x;
   // every operand load of the thread's two channels is issued before the arithmetic
-  float4 wqr[2][8], wur[2][8];
+  float4 wqr[2][8], wur[2][2];
   float qpv[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = tid + 256 * u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      wqr[u][i] = *reinterpret_cast<const float4*>(wq + c * 32 + 4 * i);
-      wur[u][i] = *reinterpret_cast<const float4*>(wup + c * 32 + 4 * i);
-    }
-    qpv[u] = qprev[(long)b * 512 + c];
+    for (int i = 0; i < 8; ++i) wqr[u][i] = *reinterpret_cast<const float4*>(wq + c * 32 + 4 * i);
+    wur[u][0] = *reinterpret_cast<const float4*>(wup + c * 32 + r0);
+    wur[u][1] = *reinterpret_cast<const float4*>(wup + c * 32 + 16 + r0);
+    qpv[u] = qprev_in[(long)b * 512 + c];
   }
   if (tid < 32) sz[tid] = latent[b * 32 + tid] * emb_std[tid] + emb_mean[tid];
   __syncthreads();
@@ -1904,45 +1910,44 @@ __global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, con
   for (int u = 0; u < 2; ++u) {
     const int c = tid + 256 * u;
     const float* wqf = reinterpret_cast<const float*>(wqr[u]);
-    const float* wuf = reinterpret_cast<const float*>(wur[u]);
+    const float* w0 = reinterpret_cast<const float*>(&wur[u][0]);
+    const float* w1 = reinterpret_cast<const float*>(&wur[u][1]);
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < 32; ++k) q += wqf[k] * sz[k];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v = q * wuf[r] + qpv[u] * wuf[16 + r];
+    for (int r = 0; r < 4; ++r) {
+      const float v = q * w0[r] + qpv[u] * w1[r];
       sx[r * 512 + c] = v;
-      x[((long)b * 16 + r) * 512 + c] = v;
+      x[((long)b * 16 + r0 + r) * 512 + c] = v;
     }
-    if (upd) qprev[(long)b * 512 + c] = q;
+    if (blockIdx.y == 0) qprev_out[(long)b * 512 + c] = upd ? q : qpv[u];
   }
   __syncthreads();
-  const int lane = tid & 63, wave = tid >> 6;
-  for (int r = wave; r < 16; r += 4) {
-    float v[8], s = 0.f;
+  const int lane = tid & 63, r = tid >> 6;  // one row per wave
+  float v[8], sm = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      v[i] = sx[r * 512 + lane + 64 * i];
-      s += v[i];
-    }
-    const float mean = wave_sum(s) / 512.f;
-    float q = 0.f;
+  for (int i = 0; i < 8; ++i) {
+    v[i] = sx[r * 512 + lane + 64 * i];
+    sm += v[i];
+  }
+  const float mean = wave_sum(sm) / 512.f;
+  float qq = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) q += (v[i] - mean) * (v[i] - mean);
-    const float den = sqrtf(wave_sum(q) / 512.f + 1e-5f);
+  for (int i = 0; i < 8; ++i) qq += (v[i] - mean) * (v[i] - mean);
+  const float den = sqrtf(wave_sum(qq) / 512.f + 1e-5f);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int n = lane + 64 * i;
-      h[((long)b * 16 + r) * 512 + n] = (v[i] - mean) / den * ln_w[n] + ln_b[n];
-    }
+  for (int i = 0; i < 8; ++i) {
+    const int n = lane + 64 * i;
+    h[((long)b * 16 + r0 + r) * 512 + n] = (v[i] - mean) / den * ln_w[n] + ln_b[n];
   }
 }
 
 void quant_upsample(const float* latent, int B, const float* emb_std, const float* emb_mean, const float* wq,
-                    const float* wup, float* qprev, const FrameFlags* fl, float* x, float* h, const float* ln_w,
-                    const float* ln_b, hipStream_t s) {
-  hipLaunchKernelGGL(k_quant_upsample, dim3(B), dim3(256), 0, s, latent, emb_std, emb_mean, wq, wup, qprev, fl, x,
-                     h, ln_w, ln_b);
+                    const float* wup, const float* qprev_in, float* qprev_out, const FrameFlags* fl, float* x,
+                    float* h, const float* ln_w, const float* ln_b, hipStream_t s) {
+  hipLaunchKernelGGL(k_quant_upsample, dim3(B, 4), dim3(256), 0, s, latent, emb_std, emb_mean, wq, wup, qprev_in,
+                     qprev_out, fl, x, h, ln_w, ln_b);
 }
 
 // =============================================================================================
