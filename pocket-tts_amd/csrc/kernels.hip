@@ -35,6 +35,19 @@ __device__ __forceinline__ float wave_max(float v) {
 
 __device__ void splitk_combine(const GemmArgs& g, int m0, int n0, int ncols, float* flag);
 
+// Sum over S (<= 16) split-K slabs p[z * stride] in z order, every load issued before the first
+// add (a runtime-bounded loop waited on each load in turn: one L2 round trip per slab).
+__device__ __forceinline__ float slab_sum(const float* p, long stride, int S) {
+  float v[16];
+#pragma unroll
+  for (int z = 0; z < 16; ++z) v[z] = z < S ? p[(long)z * stride] : 0.f;
+  float acc = 0.f;
+#pragma unroll
+  for (int z = 0; z < 16; ++z)
+    if (z < S) acc += v[z];
+  return acc;
+}
+
 // =============================================================================================
 // GEMM (see kernels.h). One 256-thread workgroup = 4 waves owns a 32x32 output tile; the
 // tile's K chunks (32 wide) are dealt round-robin to the 4 waves, each wave accumulates with
@@ -1694,9 +1707,7 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
   if (tid < 192) {  // q | k | v column of this head, summed over the slabs in z order
     const int part = tid >> 6;
     const float* pr = P + (long)row * ld + part * d + head * 64 + lane;
-    float acc = 0.f;
-    for (int z = 0; z < S; ++z) acc += pr[(long)z * M * ld];
-    s_qkv[part][lane] = acc;
+    s_qkv[part][lane] = slab_sum(pr, (long)M * ld, S);
   }
   __syncthreads();
   if (tid < 64) {  // rotate the (2i, 2i+1) pairs of q (tid < 32) and k (tid >= 32)
@@ -1841,14 +1852,14 @@ __global__ __launch_bounds__(256) void k_flow_cond(const float* P, int S, int B,
   const int NC = 513;  // cond_embed (512) | out_eos (1)
   for (int n = tid; n < 512; n += 256) {
     float c = 0.f;
-    for (int z = 0; z < S; ++z) c += P[((long)z * B + b) * NC + n];
+    c = slab_sum(P + (long)b * NC + n, (long)B * NC, S);
     c += bias[n];
     for (int s = 0; s < lsd; ++s) ysilu[((long)s * B + b) * 512 + n] = silu(temb[s * 512 + n] + c);
   }
   const SlotState& ss = st[b];
   if (tid == 0) {  // out_eos logit (flow_lm.rs:139-145); the EOS rule runs in front_commit
     float e = 0.f;
-    for (int z = 0; z < S; ++z) e += P[((long)z * B + b) * NC + 512];
+    e = slab_sum(P + (long)b * NC + 512, (long)B * NC, S);
     eos_out[b] = e + bias[512];
   }
   if (tid < 32) {
