@@ -116,6 +116,11 @@ Engine::Engine(const ptts_engine_config& cfg) {
   xf_ = dalloc((size_t)B * FD);
   hf_ = dalloc((size_t)B * FD);
   uf_ = dalloc((size_t)B * FD);
+  head_chain_ = !getenv("PTTS_HEAD_CHAIN_OFF");
+  hxp_ = dalloc((size_t)B * FD);
+  hup_ = dalloc((size_t)B * FD);
+  hctr_ = (int*)dalloc(4 * ((B + 15) / 16) + 4);
+  herr_ = (int*)dalloc(4);
   mx_ = dalloc((size_t)B * UP * MD);
   mh_ = dalloc((size_t)B * UP * MD);
   mq_ = dalloc((size_t)B * UP * MD);
@@ -544,8 +549,38 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
     a.ldy = NADA;
     push_rr(ops, "head.ada_reduce", a);
   }
-  // lsd_decode Euler steps (flow_lm.rs:7-22) over ResBlocks (mlp.rs:146-213)
-  for (int st = 0; st < lsd_; ++st) {
+  // lsd_decode Euler steps (flow_lm.rs:7-22) over ResBlocks (mlp.rs:146-213): one persistent
+  // launch (k_flow_head) for the whole chain, or 28 GEMM + row-reduce launches per step
+  if (head_chain_ && flow_head_fits(B)) {
+    FlowHeadArgs f{};
+    f.B = B;
+    f.lsd = lsd_;
+    f.euler_scale = 1.0f / (float)lsd_;
+    f.cur = cur_;
+    f.mods = mods_;
+    f.ldm = NADA;
+    f.in_w = W(L_.inproj_w);
+    f.in_b = W(L_.inproj_b);
+    for (int i = 0; i < FDEPTH; ++i) {
+      f.lnw[i] = W(L_.rb_lnw[i]);
+      f.lnb[i] = W(L_.rb_lnb[i]);
+      f.w0[i] = W(L_.rb_w0[i]);
+      f.b0[i] = W(L_.rb_b0[i]);
+      f.w2[i] = W(L_.rb_w2[i]);
+      f.b2[i] = W(L_.rb_b2[i]);
+    }
+    f.fin_w = W(L_.fin_w);
+    f.fin_b = W(L_.fin_b);
+    f.xp = hxp_;
+    f.up = hup_;
+    f.ctr = hctr_;
+    f.err = herr_;
+    const double fl = 2.0 * lsd_ * B * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD);
+    const double by = 4.0 * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD) +
+                      4.0 * lsd_ * B * ((double)FDEPTH * 3 * FD + 2 * FD);
+    ops.push_back({"head.chain", [f](hipStream_t s) { flow_head(f, s); }, fl, by});
+  }
+  for (int st = 0; st < lsd_ && !(head_chain_ && flow_head_fits(B)); ++st) {
     const float* mods = mods_ + (size_t)st * B * NADA;
     const std::string p = "head.s" + std::to_string(st);
     linear_split(ops, p + ".inproj_gemm", cur_, LDIM, B, W(L_.inproj_w), FD, LDIM, &S);

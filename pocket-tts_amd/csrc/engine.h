@@ -116,6 +116,10 @@ class Engine {
   SlotState* admit_st_ = nullptr;
   int* admit_fpos_ = nullptr;
   float *ysilu_ = nullptr, *mods_ = nullptr, *xf_ = nullptr, *hf_ = nullptr, *uf_ = nullptr;
+  // persistent flow-head chain (k_flow_head): hand-off rows, counters, timeout word
+  bool head_chain_ = true;
+  float *hxp_ = nullptr, *hup_ = nullptr;
+  int *hctr_ = nullptr, *herr_ = nullptr;
   float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;
   float* a0_ = nullptr;
   float *cb_[3] = {}, *cv_[3] = {}, *ca_[3] = {}, *ce_[3] = {};

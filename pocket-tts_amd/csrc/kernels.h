@@ -160,6 +160,31 @@ struct FrameFlags {
 void flow_cond(const float* P, int S, int B, const float* bias, const float* temb, int lsd_steps,
                const SlotState* st, float* ysilu, float* cur, float* eos_out, hipStream_t s);
 
+// ---------------------------------------------------------------------------------------------
+// Flow-head chain (mlp.rs:146-213,370-383; flow_lm.rs:7-22) in one persistent launch: per lsd
+// step, x = cur W_in^T + b_in; 6 ResBlocks x += gate * (silu(mod(LN(x)) W0^T + b0) W2^T + b2);
+// cur += (mod(LN_noaffine(x)) W_f^T + b_f) / lsd. mods [lsd][B][ldm] holds the adaLN shift |
+// scale | gate of each block and the final shift | scale (mlp.rs:322-368). xp/up: [B][512]
+// hand-off buffers; ctr: 4*ceil(B/16)+1 ints, zero before the first launch (the kernel re-arms
+// them); err: set to 1 if a hand-off wait timed out. Requires 1 <= B <= 128 (flow_head_fits).
+constexpr int FH_D = 512, FH_L = 32, FH_DEPTH = 6;
+struct FlowHeadArgs {
+  int B, lsd;
+  float euler_scale;
+  float* cur;
+  const float* mods;
+  long ldm;
+  const float *in_w, *in_b;
+  const float *lnw[FH_DEPTH], *lnb[FH_DEPTH];
+  const float *w0[FH_DEPTH], *b0[FH_DEPTH], *w2[FH_DEPTH], *b2[FH_DEPTH];
+  const float *fin_w, *fin_b;
+  float *xp, *up;
+  int* ctr;
+  int* err;
+};
+bool flow_head_fits(int B);
+void flow_head(const FlowHeadArgs& a, hipStream_t s);
+
 // End of the front part: EOS state machine (tts_model.rs:1055-1063), frame flags, the frame's
 // latent / eos logit into the parity buffers, next backbone input, step / FlowLM position.
 struct FrontCommitArgs {

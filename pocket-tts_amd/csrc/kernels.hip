@@ -2255,4 +2255,270 @@ void resample(const float* x, int n_in, const float* taps, const ResamplePlan& p
                      p.down, p.half, n_out, n_pad, use_lds, y);
 }
 
+// =============================================================================================
+// Flow-head chain in ONE persistent launch (mlp.rs:146-213, 370-383; flow_lm.rs:7-22): for every
+// lsd Euler step, input projection -> 6 ResBlocks -> FinalLayer -> x += v / N. As separate
+// launches this is 28 GEMM + row-reduce kernels of M = B rows x 512 (each ~1 MB of weights), a
+// chain of launch gaps and HBM round trips. Here a grid of ceil(B/16) row groups x 32 column
+// groups (16 rows x 16 output columns per workgroup, 8 waves splitting K = 512) runs the chain
+// with in-launch hand-offs (cdna_hip_programming.md Guideline 16, sc1 form):
+//   producer: the storing wave writes its 16x16 tile with sc1 (write-through) buffer stores,
+//             s_waitcnt vmcnt(0), then lane 0 adds 1 to the row group's counter (agent scope);
+//   consumer: thread 0 polls the counter with sc1 loads (bounded spin), __syncthreads(), then
+//             every load of handed-off bytes is an sc1 buffer load.
+// Each workgroup keeps its 16x16 tile of the residual stream x in registers for the whole chain;
+// consumers rebuild the full rows (LayerNorm statistics need all 512 columns) from the published
+// copy. Weights, LayerNorm affines and adaLN modulations do not depend on the chain and are
+// loaded before each wait. Counters are zeroed at allocation and re-armed by the last workgroup
+// to finish, so the kernel can be replayed (graphs, timing loops) without a memset node.
+// v_mfma_f32_16x16x4_f32 fragments as in k_attn16: lane (c = l & 15, G = l >> 4) supplies
+// A[row c][k] and B[k][col c] for k = 64*wave + 16*G + s at step s; D reg g -> row 4G+g, col c.
+// =============================================================================================
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int FH_WAVES = 8;  // FH_D, FH_L, FH_DEPTH: kernels.h
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fh_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 fh_ld(__amdgpu_buffer_rsrc_t r, int byte_off) {  // sc1 load
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ void fh_st(__amdgpu_buffer_rsrc_t r, int byte_off, float4 f) {  // sc1 store
+  const u32x4 v = {__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
+}
+// storing wave: drain its sc1 stores, then one lane signals
+__device__ __forceinline__ void fh_publish(int* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// whole workgroup: thread 0 polls until ctr >= target (bounded: a timeout sets *err and stops
+// waiting for the rest of the launch), then the barrier releases every wave's sc1 loads
+__device__ __forceinline__ void fh_wait(int* ctr, int target, int* err, bool& dead) {
+  if (threadIdx.x == 0 && !dead) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 20)) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dead = true;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+}
+__device__ __forceinline__ float4 f4ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// LayerNorm (eps 1e-6, optional affine) + adaLN modulate (mlp.rs:29-58,135-137) of this lane's
+// 16 values of row c; row statistics combine the 4 lane groups and the 8 waves in a fixed order.
+__device__ __forceinline__ void fh_ln(float4 (&v)[4], float (*s_st)[FH_WAVES][16], int wave, int c, int G,
+                                      const float4 (&lw)[4], const float4 (&lb)[4], bool affine,
+                                      const float4 (&sc)[4], const float4 (&sf)[4]) {
+  float s1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s1 += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  if (G == 0) s_st[0][wave][c] = s1;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < FH_WAVES; ++w) tot += s_st[0][w][c];
+  const float mean = tot / (float)FH_D;
+  float s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = make_float4(v[j].x - mean, v[j].y - mean, v[j].z - mean, v[j].w - mean);
+    s2 += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+  }
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  if (G == 0) s_st[1][wave][c] = s2;
+  __syncthreads();
+  float q = 0.f;
+#pragma unroll
+  for (int w = 0; w < FH_WAVES; ++w) q += s_st[1][w][c];
+  const float den = sqrtf(q / (float)FH_D + 1e-6f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float4 h = make_float4(v[j].x / den, v[j].y / den, v[j].z / den, v[j].w / den);
+    if (affine) h = f4add(f4mul(h, lw[j]), lb[j]);
+    v[j] = make_float4(h.x * (1.0f + sc[j].x) + sf[j].x, h.y * (1.0f + sc[j].y) + sf[j].y,
+                       h.z * (1.0f + sc[j].z) + sf[j].z, h.w * (1.0f + sc[j].w) + sf[j].w);
+  }
+}
+// 16 MFMA steps over this lane's k range, then the 8 wave partials summed in wave order; wave 0
+// lane t returns the 16x16 tile's row t/4, columns 4(t%4)..+3
+__device__ __forceinline__ float4 fh_gemm(const float4 (&a)[4], const float4 (&b)[4], float (*s_red)[16][16],
+                                          int wave, int c, int G, int lane) {
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].x, b[j].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].y, b[j].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].z, b[j].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].w, b[j].w, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) s_red[wave][4 * G + g][c] = acc[g];
+  __syncthreads();
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (wave == 0) {
+#pragma unroll
+    for (int w = 0; w < FH_WAVES; ++w) r = f4add(r, f4ld(&s_red[w][lane >> 2][4 * (lane & 3)]));
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
+  __shared__ float s_st[2][FH_WAVES][16];
+  __shared__ __attribute__((aligned(16))) float s_red[FH_WAVES][16][16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, G = lane >> 4;
+  const int RG = (a.B + 15) / 16;
+  const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;
+  const int col0 = 16 * cg;
+  const int arow = min(16 * rg + c, a.B - 1);  // A-operand row of this lane (clamped; rows >= B unused)
+  const int k0 = 64 * wave + 16 * G;           // this lane's 16 k
+  const int orow = 16 * rg + (lane >> 2);      // epilogue (wave 0): row, columns ocol..ocol+3
+  const int ocol = col0 + 4 * (lane & 3);
+  const bool ostore = orow < a.B;
+  const __amdgpu_buffer_rsrc_t xr = fh_rsrc(a.xp), ur = fh_rsrc(a.up), cr = fh_rsrc(a.cur);
+  int* cx = a.ctr + 4 * rg;  // [0] x published, [1] u published, [2] cur published
+  int *cu = cx + 1, *cc = cx + 2;
+  int nx = 0, nu = 0;
+  bool dead = false;
+  float4 xo = make_float4(0.f, 0.f, 0.f, 0.f);  // wave 0: residual tile x[orow][ocol..+3]
+  const float4 zero4[4] = {};
+
+  for (int st = 0; st < a.lsd; ++st) {
+    const float* mods = a.mods + (long)st * a.B * a.ldm;
+    // ---- input projection x = cur W_in^T + b_in (K = 32), one wave
+    if (st > 0) fh_wait(cc, 2 * st, a.err, dead);
+    if (wave == 0) {
+      const int r = min(orow, a.B - 1);
+      float4 cv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cv[j] = fh_ld(cr, (r * FH_L + 4 * j) * 4);
+      float acc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float* w = a.in_w + (long)(ocol + q) * FH_L;
+        float t = a.in_b[ocol + q];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 wv = f4ld(w + 4 * j);
+          t += (cv[j].x * wv.x + cv[j].y * wv.y) + (cv[j].z * wv.z + cv[j].w * wv.w);
+        }
+        acc[q] = t;
+      }
+      xo = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      if (ostore) fh_st(xr, (orow * FH_D + ocol) * 4, xo);
+      fh_publish(cx);
+    }
+    ++nx;
+    for (int i = 0; i < FH_DEPTH; ++i) {
+      // ---- h = modulate(LN(x)), u = silu(h W0^T + b0)
+      float4 w[4], lw[4], lb[4], sc[4], sf[4], v[4];
+      {
+        const float* W0 = a.w0[i] + (long)(col0 + c) * FH_D + k0;
+        const float* mr = mods + (long)arow * a.ldm + (long)i * 3 * FH_D + k0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          w[j] = f4ld(W0 + 4 * j);
+          lw[j] = f4ld(a.lnw[i] + k0 + 4 * j);
+          lb[j] = f4ld(a.lnb[i] + k0 + 4 * j);
+          sf[j] = f4ld(mr + 4 * j);
+          sc[j] = f4ld(mr + FH_D + 4 * j);
+        }
+      }
+      fh_wait(cx, 32 * nx, a.err, dead);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fh_ld(xr, (arow * FH_D + k0 + 4 * j) * 4);
+      fh_ln(v, s_st, wave, c, G, lw, lb, true, sc, sf);
+      float4 r = fh_gemm(v, w, s_red, wave, c, G, lane);
+      if (wave == 0) {
+        const float4 bb = f4ld(a.b0[i] + ocol);
+        const float4 u = make_float4(silu(r.x + bb.x), silu(r.y + bb.y), silu(r.z + bb.z), silu(r.w + bb.w));
+        if (ostore) fh_st(ur, (orow * FH_D + ocol) * 4, u);
+        fh_publish(cu);
+      }
+      ++nu;
+      // ---- x += gate * (u W2^T + b2)
+      {
+        const float* W2 = a.w2[i] + (long)(col0 + c) * FH_D + k0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = f4ld(W2 + 4 * j);
+      }
+      float4 gt = make_float4(0.f, 0.f, 0.f, 0.f), b2 = gt;
+      if (wave == 0) {
+        gt = f4ld(mods + (long)min(orow, a.B - 1) * a.ldm + (long)i * 3 * FH_D + 2 * FH_D + ocol);
+        b2 = f4ld(a.b2[i] + ocol);
+      }
+      fh_wait(cu, 32 * nu, a.err, dead);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fh_ld(ur, (arow * FH_D + k0 + 4 * j) * 4);
+      r = fh_gemm(v, w, s_red, wave, c, G, lane);
+      if (wave == 0) {
+        xo = f4add(xo, f4mul(gt, f4add(r, b2)));
+        if (ostore) fh_st(xr, (orow * FH_D + ocol) * 4, xo);
+        fh_publish(cx);
+      }
+      ++nx;
+    }
+    // ---- FinalLayer (mlp.rs:182-213): modulate(LN_noaffine(x)) W_f^T + b_f, Euler x += v / N;
+    // column groups 0 and 1 own the 32 latent columns
+    const bool fin = cg < FH_L / 16;
+    float4 w[4], sc[4], sf[4], v[4];
+    float4 fb = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (fin) {
+      const float* Wf = a.fin_w + (long)(col0 + c) * FH_D + k0;
+      const float* mr = mods + (long)arow * a.ldm + (long)FH_DEPTH * 3 * FH_D + k0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w[j] = f4ld(Wf + 4 * j);
+        sf[j] = f4ld(mr + 4 * j);
+        sc[j] = f4ld(mr + FH_D + 4 * j);
+      }
+      if (wave == 0) fb = f4ld(a.fin_b + ocol);
+    }
+    fh_wait(cx, 32 * nx, a.err, dead);
+    if (fin) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fh_ld(xr, (arow * FH_D + k0 + 4 * j) * 4);
+      fh_ln(v, s_st, wave, c, G, zero4, zero4, false, sc, sf);
+      const float4 r = fh_gemm(v, w, s_red, wave, c, G, lane);
+      if (wave == 0) {
+        const int off = (min(orow, a.B - 1) * FH_L + ocol) * 4;
+        const float4 cv = fh_ld(cr, off);
+        const float e = a.euler_scale;
+        const float4 o = f4add(r, fb);
+        if (ostore) fh_st(cr, off, make_float4(cv.x + o.x * e, cv.y + o.y * e, cv.z + o.z * e, cv.w + o.w * e));
+        fh_publish(cc);
+      }
+    }
+  }
+  // re-arm: the last workgroup to finish zeroes every counter (all waits are behind it)
+  if (tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* done = a.ctr + 4 * RG;
+    if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      for (int g = 0; g < 4 * RG; ++g) __hip_atomic_store(a.ctr + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+bool flow_head_fits(int B) { return B >= 1 && B <= 128; }
+
+void flow_head(const FlowHeadArgs& a, hipStream_t s) {
+  if (!flow_head_fits(a.B)) throw std::runtime_error("flow_head: B out of range");
+  const int RG = (a.B + 15) / 16;
+  hipLaunchKernelGGL(k_flow_head, dim3(RG * (FH_D / 16)), dim3(64 * FH_WAVES), 0, s, a);
+}
+
 }  // namespace ptts
