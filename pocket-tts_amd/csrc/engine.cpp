@@ -503,6 +503,19 @@ void Engine::prefill_rows(std::vector<Op>& ops, int slot, int T, int p0) {
   flow_layers(ops, T, map, 16, false, "prefill");
 }
 
+// The persistent flow-head launch needs <= 128 rows and ResBlock tensors at one uniform stride
+// in the packed blob (pack_weights lays the six blocks out identically).
+bool Engine::use_head_chain(int B) const {
+  if (!head_chain_ || !flow_head_fits(B)) return false;
+  const long s = (long)(L_.rb_w0[1] - L_.rb_w0[0]);
+  for (int i = 1; i < FDEPTH; ++i)
+    if ((long)(L_.rb_lnw[i] - L_.rb_lnw[i - 1]) != s || (long)(L_.rb_lnb[i] - L_.rb_lnb[i - 1]) != s ||
+        (long)(L_.rb_w0[i] - L_.rb_w0[i - 1]) != s || (long)(L_.rb_b0[i] - L_.rb_b0[i - 1]) != s ||
+        (long)(L_.rb_w2[i] - L_.rb_w2[i - 1]) != s || (long)(L_.rb_b2[i] - L_.rb_b2[i - 1]) != s)
+      return false;
+  return true;
+}
+
 // FRONT part of a step (FlowLM + flow head) for rows [0, B), handing its frame to parity `par`.
 void Engine::build_front(std::vector<Op>& ops, int B, int par) {
   int S = 1;
@@ -551,7 +564,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
   }
   // lsd_decode Euler steps (flow_lm.rs:7-22) over ResBlocks (mlp.rs:146-213): one persistent
   // launch (k_flow_head) for the whole chain, or 28 GEMM + row-reduce launches per step
-  if (head_chain_ && flow_head_fits(B)) {
+  if (use_head_chain(B)) {
     FlowHeadArgs f{};
     f.B = B;
     f.lsd = lsd_;
@@ -561,26 +574,26 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
     f.ldm = NADA;
     f.in_w = W(L_.inproj_w);
     f.in_b = W(L_.inproj_b);
-    for (int i = 0; i < FDEPTH; ++i) {
-      f.lnw[i] = W(L_.rb_lnw[i]);
-      f.lnb[i] = W(L_.rb_lnb[i]);
-      f.w0[i] = W(L_.rb_w0[i]);
-      f.b0[i] = W(L_.rb_b0[i]);
-      f.w2[i] = W(L_.rb_w2[i]);
-      f.b2[i] = W(L_.rb_b2[i]);
-    }
+    f.lnw = W(L_.rb_lnw[0]);
+    f.lnb = W(L_.rb_lnb[0]);
+    f.w0 = W(L_.rb_w0[0]);
+    f.b0 = W(L_.rb_b0[0]);
+    f.w2 = W(L_.rb_w2[0]);
+    f.b2 = W(L_.rb_b2[0]);
+    f.blk = (long)(L_.rb_w0[1] - L_.rb_w0[0]);
     f.fin_w = W(L_.fin_w);
     f.fin_b = W(L_.fin_b);
     f.xp = hxp_;
     f.up = hup_;
     f.ctr = hctr_;
     f.err = herr_;
+    f.dbg = getenv("PTTS_HEAD_DBG") ? (unsigned long long*)strtoull(getenv("PTTS_HEAD_DBG"), nullptr, 0) : nullptr;
     const double fl = 2.0 * lsd_ * B * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD);
     const double by = 4.0 * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD) +
                       4.0 * lsd_ * B * ((double)FDEPTH * 3 * FD + 2 * FD);
     ops.push_back({"head.chain", [f](hipStream_t s) { flow_head(f, s); }, fl, by});
   }
-  for (int st = 0; st < lsd_ && !(head_chain_ && flow_head_fits(B)); ++st) {
+  for (int st = 0; st < lsd_ && !use_head_chain(B); ++st) {
     const float* mods = mods_ + (size_t)st * B * NADA;
     const std::string p = "head.s" + std::to_string(st);
     linear_split(ops, p + ".inproj_gemm", cur_, LDIM, B, W(L_.inproj_w), FD, LDIM, &S);

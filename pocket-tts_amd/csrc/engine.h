@@ -118,6 +118,7 @@ class Engine {
   float *ysilu_ = nullptr, *mods_ = nullptr, *xf_ = nullptr, *hf_ = nullptr, *uf_ = nullptr;
   // persistent flow-head chain (k_flow_head): hand-off rows, counters, timeout word
   bool head_chain_ = true;
+  bool use_head_chain(int B) const;
   float *hxp_ = nullptr, *hup_ = nullptr;
   int *hctr_ = nullptr, *herr_ = nullptr;
   float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;

@@ -175,12 +175,14 @@ struct FlowHeadArgs {
   const float* mods;
   long ldm;
   const float *in_w, *in_b;
-  const float *lnw[FH_DEPTH], *lnb[FH_DEPTH];
-  const float *w0[FH_DEPTH], *b0[FH_DEPTH], *w2[FH_DEPTH], *b2[FH_DEPTH];
+  // ResBlock 0's tensors; block i's are at + i * blk floats (the packed blob's uniform stride)
+  const float *lnw, *lnb, *w0, *b0, *w2, *b2;
+  long blk;
   const float *fin_w, *fin_b;
   float *xp, *up;
   int* ctr;
   int* err;
+  unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr
 };
 bool flow_head_fits(int B);
 void flow_head(const FlowHeadArgs& a, hipStream_t s);

@@ -2341,10 +2341,10 @@ __device__ __forceinline__ void fh_ln(float4 (&v)[4], float (*s_st)[FH_WAVES][16
   float q = 0.f;
 #pragma unroll
   for (int w = 0; w < FH_WAVES; ++w) q += s_st[1][w][c];
-  const float den = sqrtf(q / (float)FH_D + 1e-6f);
+  const float rden = 1.0f / sqrtf(q / (float)FH_D + 1e-6f);  // one divide, then multiplies (<= 1 ulp apart)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float4 h = make_float4(v[j].x / den, v[j].y / den, v[j].z / den, v[j].w / den);
+    float4 h = make_float4(v[j].x * rden, v[j].y * rden, v[j].z * rden, v[j].w * rden);
     if (affine) h = f4add(f4mul(h, lw[j]), lb[j]);
     v[j] = make_float4(h.x * (1.0f + sc[j].x) + sf[j].x, h.y * (1.0f + sc[j].y) + sf[j].y,
                        h.z * (1.0f + sc[j].z) + sf[j].z, h.w * (1.0f + sc[j].w) + sf[j].w);
@@ -2373,9 +2373,19 @@ __device__ __forceinline__ float4 fh_gemm(const float4 (&a)[4], const float4 (&b
   return r;
 }
 
+// Operands of one phase, loaded a phase ahead of their use (non-publishing waves right after the
+// current phase's payload loads, the publishing wave 0 right after its publish, so that neither
+// the payload wait nor the publish drain waits for them): the lane's 16-k slice of one weight
+// row, and for LayerNorm phases the adaLN scale / shift of the lane's row.
+struct FhOps {
+  float4 w[4], sc[4], sf[4];
+  float4 e0, e1;  // wave 0 epilogue: bias | gate, bias
+};
+
 __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   __shared__ float s_st[2][FH_WAVES][16];
   __shared__ __attribute__((aligned(16))) float s_red[FH_WAVES][16][16];
+  __shared__ __attribute__((aligned(16))) float s_ln[FH_DEPTH][2][FH_D];  // ResBlock LayerNorm affines
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, G = lane >> 4;
@@ -2386,7 +2396,9 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   const int k0 = 64 * wave + 16 * G;           // this lane's 16 k
   const int orow = 16 * rg + (lane >> 2);      // epilogue (wave 0): row, columns ocol..ocol+3
   const int ocol = col0 + 4 * (lane & 3);
+  const int crow = min(orow, a.B - 1);
   const bool ostore = orow < a.B;
+  const bool fin = cg < FH_L / 16;  // column groups 0 and 1 own the 32 latent columns
   const __amdgpu_buffer_rsrc_t xr = fh_rsrc(a.xp), ur = fh_rsrc(a.up), cr = fh_rsrc(a.cur);
   int* cx = a.ctr + 4 * rg;  // [0] x published, [1] u published, [2] cur published
   int *cu = cx + 1, *cc = cx + 2;
@@ -2394,16 +2406,51 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   bool dead = false;
   float4 xo = make_float4(0.f, 0.f, 0.f, 0.f);  // wave 0: residual tile x[orow][ocol..+3]
   const float4 zero4[4] = {};
+  int sk = 0;
+#define FH_STAMP()                                                                     \
+  if (a.dbg && tid == 0 && blockIdx.x < 4 && sk < 120) a.dbg[blockIdx.x * 128 + sk++] = __builtin_amdgcn_s_memrealtime()
+
+#pragma unroll
+  for (int i = 0; i < FH_DEPTH; ++i)
+    if (tid < FH_D / 2) {  // threads 0..255: float4 (tid & 127) of lnw (tid < 128) or lnb
+      const float* src = (tid < FH_D / 4 ? a.lnw : a.lnb) + (long)i * a.blk;
+      reinterpret_cast<float4*>(&s_ln[i][tid < FH_D / 4 ? 0 : 1][0])[tid & (FH_D / 4 - 1)] =
+          f4ld(src + 4 * (tid & (FH_D / 4 - 1)));
+    }
+  // operand loaders (i: ResBlock, or FH_DEPTH for the FinalLayer)
+  auto load_ln_ops = [&](FhOps& o, const float* mods, int i) {
+    if (i == FH_DEPTH && !fin) return;
+    const float* W = (i < FH_DEPTH ? a.w0 + (long)i * a.blk : a.fin_w) + (long)(col0 + c) * FH_D + k0;
+    const float* mr = mods + (long)arow * a.ldm + (long)i * 3 * FH_D + k0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o.w[j] = f4ld(W + 4 * j);
+      o.sf[j] = f4ld(mr + 4 * j);
+      o.sc[j] = f4ld(mr + FH_D + 4 * j);
+    }
+    if (wave == 0) o.e0 = f4ld((i < FH_DEPTH ? a.b0 + (long)i * a.blk : a.fin_b) + ocol);
+  };
+  auto load_mlp2_ops = [&](FhOps& o, const float* mods, int i) {
+    const float* W = a.w2 + (long)i * a.blk + (long)(col0 + c) * FH_D + k0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o.w[j] = f4ld(W + 4 * j);
+    if (wave == 0) {
+      o.e0 = f4ld(mods + (long)crow * a.ldm + (long)i * 3 * FH_D + 2 * FH_D + ocol);  // gate
+      o.e1 = f4ld(a.b2 + (long)i * a.blk + ocol);
+    }
+  };
+  FhOps p0, p2;  // operands of the next LayerNorm phase and the next mlp2 phase
+  load_ln_ops(p0, a.mods, 0);
+  load_mlp2_ops(p2, a.mods, 0);
 
   for (int st = 0; st < a.lsd; ++st) {
     const float* mods = a.mods + (long)st * a.B * a.ldm;
     // ---- input projection x = cur W_in^T + b_in (K = 32), one wave
     if (st > 0) fh_wait(cc, 2 * st, a.err, dead);
     if (wave == 0) {
-      const int r = min(orow, a.B - 1);
       float4 cv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) cv[j] = fh_ld(cr, (r * FH_L + 4 * j) * 4);
+      for (int j = 0; j < 8; ++j) cv[j] = fh_ld(cr, (crow * FH_L + 4 * j) * 4);
       float acc[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -2421,85 +2468,76 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       fh_publish(cx);
     }
     ++nx;
+#pragma unroll 1
     for (int i = 0; i < FH_DEPTH; ++i) {
       // ---- h = modulate(LN(x)), u = silu(h W0^T + b0)
-      float4 w[4], lw[4], lb[4], sc[4], sf[4], v[4];
-      {
-        const float* W0 = a.w0[i] + (long)(col0 + c) * FH_D + k0;
-        const float* mr = mods + (long)arow * a.ldm + (long)i * 3 * FH_D + k0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          w[j] = f4ld(W0 + 4 * j);
-          lw[j] = f4ld(a.lnw[i] + k0 + 4 * j);
-          lb[j] = f4ld(a.lnb[i] + k0 + 4 * j);
-          sf[j] = f4ld(mr + 4 * j);
-          sc[j] = f4ld(mr + FH_D + 4 * j);
-        }
-      }
+      float4 v[4];
+      FH_STAMP();
       fh_wait(cx, 32 * nx, a.err, dead);
+      FH_STAMP();
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = fh_ld(xr, (arow * FH_D + k0 + 4 * j) * 4);
-      fh_ln(v, s_st, wave, c, G, lw, lb, true, sc, sf);
-      float4 r = fh_gemm(v, w, s_red, wave, c, G, lane);
+      float4 lw[4], lb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lw[j] = f4ld(&s_ln[i][0][k0 + 4 * j]);
+        lb[j] = f4ld(&s_ln[i][1][k0 + 4 * j]);
+      }
+      fh_ln(v, s_st, wave, c, G, lw, lb, true, p0.sc, p0.sf);
+      FH_STAMP();
+      float4 r = fh_gemm(v, p0.w, s_red, wave, c, G, lane);
+      FH_STAMP();
+      if (wave != 0) load_ln_ops(p0, mods, i + 1);
       if (wave == 0) {
-        const float4 bb = f4ld(a.b0[i] + ocol);
+        const float4 bb = p0.e0;
         const float4 u = make_float4(silu(r.x + bb.x), silu(r.y + bb.y), silu(r.z + bb.z), silu(r.w + bb.w));
         if (ostore) fh_st(ur, (orow * FH_D + ocol) * 4, u);
         fh_publish(cu);
+        load_ln_ops(p0, mods, i + 1);
       }
+      FH_STAMP();
       ++nu;
       // ---- x += gate * (u W2^T + b2)
-      {
-        const float* W2 = a.w2[i] + (long)(col0 + c) * FH_D + k0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = f4ld(W2 + 4 * j);
-      }
-      float4 gt = make_float4(0.f, 0.f, 0.f, 0.f), b2 = gt;
-      if (wave == 0) {
-        gt = f4ld(mods + (long)min(orow, a.B - 1) * a.ldm + (long)i * 3 * FH_D + 2 * FH_D + ocol);
-        b2 = f4ld(a.b2[i] + ocol);
-      }
       fh_wait(cu, 32 * nu, a.err, dead);
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = fh_ld(ur, (arow * FH_D + k0 + 4 * j) * 4);
-      r = fh_gemm(v, w, s_red, wave, c, G, lane);
+      r = fh_gemm(v, p2.w, s_red, wave, c, G, lane);
+      if (wave != 0 && i + 1 < FH_DEPTH) load_mlp2_ops(p2, mods, i + 1);
       if (wave == 0) {
-        xo = f4add(xo, f4mul(gt, f4add(r, b2)));
+        xo = f4add(xo, f4mul(p2.e0, f4add(r, p2.e1)));
         if (ostore) fh_st(xr, (orow * FH_D + ocol) * 4, xo);
         fh_publish(cx);
+        if (i + 1 < FH_DEPTH) load_mlp2_ops(p2, mods, i + 1);
       }
       ++nx;
     }
-    // ---- FinalLayer (mlp.rs:182-213): modulate(LN_noaffine(x)) W_f^T + b_f, Euler x += v / N;
-    // column groups 0 and 1 own the 32 latent columns
-    const bool fin = cg < FH_L / 16;
-    float4 w[4], sc[4], sf[4], v[4];
-    float4 fb = make_float4(0.f, 0.f, 0.f, 0.f);
+    // ---- FinalLayer (mlp.rs:182-213): modulate(LN_noaffine(x)) W_f^T + b_f, Euler x += v / N
+    const float* nmods = mods + (long)a.B * a.ldm;  // next Euler step's modulations
+    const bool more = st + 1 < a.lsd;
     if (fin) {
-      const float* Wf = a.fin_w + (long)(col0 + c) * FH_D + k0;
-      const float* mr = mods + (long)arow * a.ldm + (long)FH_DEPTH * 3 * FH_D + k0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        w[j] = f4ld(Wf + 4 * j);
-        sf[j] = f4ld(mr + 4 * j);
-        sc[j] = f4ld(mr + FH_D + 4 * j);
-      }
-      if (wave == 0) fb = f4ld(a.fin_b + ocol);
-    }
-    fh_wait(cx, 32 * nx, a.err, dead);
-    if (fin) {
+      float4 v[4];
+      fh_wait(cx, 32 * nx, a.err, dead);
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = fh_ld(xr, (arow * FH_D + k0 + 4 * j) * 4);
-      fh_ln(v, s_st, wave, c, G, zero4, zero4, false, sc, sf);
-      const float4 r = fh_gemm(v, w, s_red, wave, c, G, lane);
+      if (wave != 0 && more) load_mlp2_ops(p2, nmods, 0);
+      fh_ln(v, s_st, wave, c, G, zero4, zero4, false, p0.sc, p0.sf);
+      const float4 r = fh_gemm(v, p0.w, s_red, wave, c, G, lane);
+      if (wave != 0 && more) load_ln_ops(p0, nmods, 0);
       if (wave == 0) {
-        const int off = (min(orow, a.B - 1) * FH_L + ocol) * 4;
+        const int off = (crow * FH_L + ocol) * 4;
         const float4 cv = fh_ld(cr, off);
         const float e = a.euler_scale;
-        const float4 o = f4add(r, fb);
+        const float4 o = f4add(r, p0.e0);
         if (ostore) fh_st(cr, off, make_float4(cv.x + o.x * e, cv.y + o.y * e, cv.z + o.z * e, cv.w + o.w * e));
         fh_publish(cc);
+        if (more) {
+          load_ln_ops(p0, nmods, 0);
+          load_mlp2_ops(p2, nmods, 0);
+        }
       }
+    } else if (more) {
+      load_ln_ops(p0, nmods, 0);
+      load_mlp2_ops(p2, nmods, 0);
     }
   }
   // re-arm: the last workgroup to finish zeroes every counter (all waits are behind it)
