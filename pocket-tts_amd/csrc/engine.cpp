@@ -952,6 +952,12 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
     if (lat) PTTS_HIP(hipMemcpy(h_lat_, lat_out_[q], sizeof(float) * n * LDIM, hipMemcpyDeviceToHost));
     PTTS_HIP(hipMemcpy(h_fl_, flags_[q], sizeof(FrameFlags) * n, hipMemcpyDeviceToHost));
   }
+  int herr = 0;  // k_flow_head's bounded hand-off waits: a timeout poisons the frame, fail loudly
+  PTTS_HIP(hipMemcpy(&herr, herr_, sizeof(int), hipMemcpyDeviceToHost));
+  if (herr) {
+    PTTS_HIP(hipMemset(herr_, 0, sizeof(int)));
+    throw Error(PTTS_ERR_HIP, "flow-head persistent launch: an in-launch hand-off wait timed out");
+  }
   for (int b = 0; b < B; ++b) {
     const bool ok = b < n && h_fl_[b].valid;
     if (valid) valid[b] = ok;

@@ -382,3 +382,40 @@ def test_flow_head_chain_two_row_groups(oracle, lsd):
                 assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
     finally:
         eng.close()
+
+
+def test_large_batch_uses_multi_launch_head(oracle):
+    """B = 136 exceeds the persistent flow-head launch's 128 rows: the head runs as split-K GEMM
+    + row-reduce launches. Sampled rows in the first, middle and last 16-row groups (with their
+    own prompts and texts) equal their oracle runs."""
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    rng = np.random.default_rng(5)
+    B, steps, probe = 136, 2, (0, 70, 135)
+    eng = pt.Engine(device=0, max_slots=B, max_ctx=32, lsd_decode_steps=1, seed=0x5EED)
+    try:
+        assert "head.chain" not in eng.plan_ops(B) and "head.chain" in eng.plan_ops(128)
+        base = eng.voice_from_prompt(d["prompt"][:3])
+        orc = {}
+        for b in range(B):
+            if b in probe:
+                prompt = (d["prompt"][:4] * (1.0 + 0.1 * probe.index(b))).astype(np.float32)
+                ids = rng.integers(0, 4000, size=3).astype(np.int32)
+                eng.open(b, eng.voice_from_prompt(prompt), ids, params(max_frames=steps))
+                s = oracle.new_state(32)
+                s.prefill(prompt)
+                s.prefill_tokens(ids)
+                orc[b] = s
+            else:
+                eng.open(b, base, np.array([260, 261], np.int32), params(max_frames=steps))
+        lat = {b: None for b in probe}
+        for _ in range(steps):
+            r = eng.step(B)
+            for b in probe:
+                o = orc[b].step(lat[b])
+                lat[b] = o["latent"]
+                np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
+                assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+    finally:
+        eng.close()
