@@ -185,6 +185,9 @@ struct FlowHeadArgs {
   unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr
 };
 bool flow_head_fits(int B);
+// FlowLM input_linear (32 -> 1024, no bias) + layer-0 norm1: x = lat W^T, h = LN(x) (eps 1e-5).
+void input_ln(const float* lat, const float* W, const float* lnw, const float* lnb, float* x, float* h, int M,
+              hipStream_t s);
 void flow_head(const FlowHeadArgs& a, hipStream_t s);
 
 // End of the front part: EOS state machine (tts_model.rs:1055-1063), frame flags, the frame's

@@ -2551,6 +2551,44 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   }
 }
 
+// FlowLM input projection + the first layer's norm1 in one launch (flow_lm.rs:117 input_linear,
+// transformer.rs:66-90 norm1): x[m] = lat[m] W^T (K = 32, no bias), h[m] = LN(x[m]) (eps 1e-5).
+// One workgroup per row, 4 output columns per thread; replaces a split-K GEMM + row reduce.
+__global__ __launch_bounds__(256) void k_input_ln(const float* __restrict__ lat, const float* __restrict__ W,
+                                                  const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                  float* __restrict__ x, float* __restrict__ h) {
+  __shared__ float sh[4];
+  const int m = blockIdx.x, n = 4 * threadIdx.x;  // N = 1024
+  float4 lv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lv[j] = *reinterpret_cast<const float4*>(lat + (long)m * 32 + 4 * j);
+  float acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float* w = W + (long)(n + q) * 32;
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 wv = *reinterpret_cast<const float4*>(w + 4 * j);
+      t += (lv[j].x * wv.x + lv[j].y * wv.y) + (lv[j].z * wv.z + lv[j].w * wv.w);
+    }
+    acc[q] = t;
+  }
+  const float4 v = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(x + (long)m * 1024 + n) = v;
+  const float mean = block_sum((v.x + v.y) + (v.z + v.w), sh) / 1024.f;
+  const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+  const float den = sqrtf(block_sum((d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w), sh) / 1024.f + 1e-5f);
+  const float4 w4 = *reinterpret_cast<const float4*>(lnw + n), b4 = *reinterpret_cast<const float4*>(lnb + n);
+  *reinterpret_cast<float4*>(h + (long)m * 1024 + n) =
+      make_float4(d.x / den * w4.x + b4.x, d.y / den * w4.y + b4.y, d.z / den * w4.z + b4.z, d.w / den * w4.w + b4.w);
+}
+
+void input_ln(const float* lat, const float* W, const float* lnw, const float* lnb, float* x, float* h, int M,
+              hipStream_t s) {
+  hipLaunchKernelGGL(k_input_ln, dim3(M), dim3(256), 0, s, lat, W, lnw, lnb, x, h);
+}
+
 bool flow_head_fits(int B) { return B >= 1 && B <= 128; }
 
 void flow_head(const FlowHeadArgs& a, hipStream_t s) {
