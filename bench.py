@@ -51,6 +51,31 @@ def measured_traffic(op):
     return t["ops"][op]["hbm_bytes_per_launch"], t.get("source")
 
 
+def phase_rooflines(per_op, plan, B, K):
+    """SURVEY §8(d) per-phase rooflines over one batched step, from the per-op HIP-event times
+    (each op timed alone; the plan lists every launch of the step, repeated ops counted per launch):
+    - front (FlowLM step + flow head): HBM-bound; algorithmic bytes = the FlowLM per-step weights
+      (84,527,137 f32) + per row the KV read of 49,152 B per cached position at the job's mean
+      context L = prompt + text + K/2, and the 49,152-B append;
+    - back (Mimi decode): MFMA-bound; algorithmic flops = 525.1 MFLOP per frame (GEMMs and convs)
+      + 65,536 per window key (W = 266) of window attention, per row."""
+    us = {n: u for u, n, _, _ in per_op}
+    front = sum(us[n] for n, _, _ in plan if n.startswith(("flow.", "head.", "front_commit")))
+    back = sum(us[n] for n, _, _ in plan if n.startswith(("mimi.", "seanet.")) or n == "commit")
+    L = PROMPT_FRAMES + TEXT_TOKENS + K / 2.0
+    f_bytes = 84_527_137 * 4 + B * (49_152 * L + 49_152)
+    b_flops = B * (525.1e6 + 65_536 * 266)
+    fa = f_bytes / (front * 1e-6) / 1e9
+    ba = b_flops / (back * 1e-6) / 1e12
+    return {
+        "front": {"bound": "hbm", "algorithmic_bytes": round(f_bytes), "sum_op_us": round(front, 1),
+                  "achieved": round(fa, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fa / HBM_PEAK_GBS, 4)},
+        "back": {"bound": "mfma", "algorithmic_flops": round(b_flops), "sum_op_us": round(back, 1),
+                 "achieved": round(ba, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(ba / F32_PEAK_TFLOPS, 4)},
+    }
+
+
 def slot_seed(round_id, rank, row):
     """Noise-stream seed of one utterance: distinct across jobs, ranks and rows."""
     return 100000 * round_id + 1000 * rank + row + 1
@@ -209,6 +234,7 @@ def main():
         roof["algorithmic_flops"] = fl
         top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
         sum_ops_ms = round(sum(u for u, _, _, _ in per_op) / 1000.0, 3)
+        roof["phases"] = phase_rooflines(per_op, plan, B, K)
     if args.ops_out:
         with open(args.ops_out, "w") as f:
             json.dump({"n_rows": B, "plan": [n for n, _, _ in plan],
