@@ -115,7 +115,7 @@ def main():
     ap.add_argument("--ops-out", default="", help="write per-op timings of the step plan (JSON)")
     ap.add_argument("--no-op-times", action="store_true", help="skip the per-op HIP-event pass (PMC runs)")
     ap.add_argument("--no-quant-variant", action="store_true",
-                    help="skip the second job on an int8-weight engine (weight_quant = QUANT_FLOW_LM)")
+                    help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM) and fp8_gemm engines")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sequential stepping (no FlowLM / Mimi overlap across consecutive frames)")
     args = ap.parse_args()
@@ -273,6 +273,21 @@ def main():
                  "weight_quant": "flow_lm int8 (quantize.rs QuantizeConfig::default, per-tensor symmetric)",
                  "int8_matrices": eq.int8_matrices}
         eq.close()
+    # ---- configs[4] "fp8 MFMA GEMM path": the same job with the large FlowLM step GEMMs as fp8
+    # W8A8 (fp8_gemm); accuracy-gated against the f32 oracle (tests/test_fp8.py), not a reference
+    # numeric. Reported beside `value`, never as it.
+    fp8 = None
+    if not args.no_quant_variant and world == 1:
+        ef = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
+                       pipeline=pipeline, fp8_gemm=True)
+        f_el, f_ad = timed_job(ef)
+        fp8 = {"value": round(B * K * 1920 / 24000.0 / f_el, 2), "unit": "audio-sec/wall-sec",
+               "ms_per_step": round(1000.0 * f_el / K, 4),
+               "steady_ms_per_step": round(1000.0 * (f_el - f_ad) / K, 4),
+               "gemm": "fp8 e4m3 W8A8 on v_mfma_f32_32x32x16_fp8_fp8 (row-scaled weights, per-slice "
+                       "activation scales), FlowLM qkv/linear1/linear2/adaLN",
+               "fp8_matrices": ef.fp8_matrices}
+        ef.close()
 
     # ---- CPU baseline: the oracle (C port of the reference algorithm) on the host cores
     cpu = None
@@ -311,6 +326,7 @@ def main():
                    else "sequential"},
         "p50_first_chunk_ms": None if p50 is None else round(p50, 3),
         "int8_flowlm_variant": quant,
+        "fp8_flowlm_variant": fp8,
         "roofline": roof,
         "cpu_baseline": cpu,
         "top_ops": top,

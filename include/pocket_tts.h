@@ -60,6 +60,12 @@ typedef struct ptts_engine_config {
                                tts_model.rs:108-171). The FlowLM step GEMMs then stream int8 codes
                                (float(q) * scale rebuilt in-kernel = the simulated f32 weight).
                                A deferred blob must have been packed with the same mode. */
+  int fp8_gemm;             /* 1: the large FlowLM step GEMMs (qkv, linear1, linear2, adaLN) run
+                               as fp8 W8A8 on v_mfma_f32_32x32x16_fp8_fp8: OCP e4m3 weight codes
+                               with one scale per output row, activations quantized in-kernel per
+                               (row, K slice). Not a reference numeric (the reference has no fp8;
+                               BASELINE configs[4]): gated on accuracy vs the f32 path. Requires
+                               weight_quant = PTTS_QUANT_NONE. 0 = f32 (default). */
 } ptts_engine_config;
 
 #define PTTS_QUANT_NONE 0
@@ -99,6 +105,8 @@ int ptts_quantize_tensor(const float* x, size_t n, int num_levels, float* out, f
 int ptts_quant_applies(const char* name, size_t numel, int weight_quant);
 /* Number of FlowLM GEMM weight matrices the engine streams as int8 codes (0 when not quantized). */
 int ptts_engine_int8_matrices(ptts_engine* e);
+/* Number of FlowLM GEMM weight matrices running on the fp8 path (fp8_gemm = 1), else 0. */
+int ptts_engine_fp8_matrices(ptts_engine* e);
 
 /* TTSModel::load / load_with_params_device (tts_model.rs:59-106,182-236). */
 int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out);

@@ -45,6 +45,9 @@ Engine::Engine(const ptts_engine_config& cfg) {
   lsd_ = cfg.lsd_decode_steps;
   PTTS_REQUIRE(cfg.weight_quant >= QUANT_NONE && cfg.weight_quant <= QUANT_ALL, "unknown weight_quant mode");
   wq_ = cfg.weight_quant;
+  PTTS_REQUIRE(cfg.fp8_gemm == 0 || cfg.fp8_gemm == 1, "fp8_gemm must be 0 or 1");
+  PTTS_REQUIRE(!(cfg.fp8_gemm && cfg.weight_quant != QUANT_NONE), "fp8_gemm and weight_quant are exclusive");
+  fp8_ = cfg.fp8_gemm;
   int ndev = 0;
   PTTS_HIP(hipGetDeviceCount(&ndev));
   PTTS_REQUIRE(dev_ >= 0 && dev_ < ndev, "HIP device ordinal out of range");
@@ -209,6 +212,7 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
 void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
+  if (fp8_ && f8map_.empty()) derive_fp8();
   TimeEmbedWeights tw;
   for (int i = 0; i < 2; ++i) {
     tw.l1w[i] = W(L_.te_l1w[i]);
@@ -276,6 +280,33 @@ void Engine::derive_int8() {
   }
 }
 
+// e4m3 codes + row scales of the large FlowLM step GEMM weights (the int8 path's set: qkv,
+// linear1, linear2, adaLN; >= 2M weights), derived on the device from the f32 blob.
+void Engine::derive_fp8() {
+  std::vector<const Layout::Q8*> use;
+  size_t bytes = 0, nsc = 0;
+  for (const Layout::Q8& q : L_.q8)
+    if ((long)q.N * q.K >= (2L << 20)) {
+      use.push_back(&q);
+      bytes += ((size_t)q.N * q.K + 255) / 256 * 256;
+      nsc += (size_t)q.N;
+    }
+  void* codes = nullptr;
+  PTTS_HIP(hipMalloc(&codes, std::max<size_t>(bytes, 1)));
+  allocs_.push_back(codes);
+  float* scales = dalloc(nsc);
+  size_t off = 0, so = 0;
+  for (const Layout::Q8* q : use) {
+    uint8_t* c = (uint8_t*)codes + off;
+    fp8_codes(W(q->w), q->N, q->K, c, scales + so, stream_);
+    f8map_[W(q->w)] = {c, scales + so};
+    off += ((size_t)q->N * q->K + 255) / 256 * 256;
+    so += (size_t)q->N;
+  }
+  PTTS_HIP(hipGetLastError());
+  PTTS_HIP(hipStreamSynchronize(stream_));
+}
+
 // ------------------------------------------------------------------ op builders
 void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M,
                           const float* Wt, int N, int K, int* S_out) {
@@ -301,6 +332,15 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   // large matrices (qkv, ff1, ff2, adaLN; >= 2M weights): below that the launch is latency-bound
   // and the f32 copy of the same values is as fast (tools/w8_probe.py). Prefill passes
   // (M >= 256) keep the f32 copy too: they are MFMA-bound.
+  auto f8 = f8map_.find(Wt);
+  const bool wf8 = f8 != f8map_.end() && M <= 64;
+  if (wf8) {  // fp8 W8A8 (k_gemm_fp8): 32x64 tiles, >= 256 workgroups, K slice <= FP8_KSLICE_MAX
+    layout = 0;
+    const int tiles = ((N + 63) / 64) * ((M + 31) / 32), nch = K / 32;
+    S = 1;
+    while (S < 16 && tiles * S < 256 && nch / (2 * S) >= 4) S *= 2;
+    while ((nch + S - 1) / S > FP8_KSLICE_MAX / 32) ++S;
+  }
   auto q8 = q8map_.find(Wt);
   const bool w8 = q8 != q8map_.end() && M <= 64 && (long)N * K >= (2L << 20) && !getenv("PTTS_W8_OFF");
   if (w8) {
@@ -316,6 +356,11 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
     a.Wq = q8->second.first;
     a.wscale = q8->second.second;
   }
+  if (wf8) {
+    PTTS_REQUIRE((K / 32 + S - 1) / S <= FP8_KSLICE_MAX / 32, "fp8 GEMM K slice too long");
+    a.Wf8 = f8->second.first;
+    a.wscale = f8->second.second;
+  }
   a.mode = 0;
   a.layout = layout;
   a.M = M;
@@ -328,7 +373,7 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   a.S = S;
   a.partial = partial_;
   ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
-                 (w8 ? (double)N * K + 4.0 * N : 4.0 * N * K) + 4.0 * ((double)M * K + (double)S * M * N)});
+                 (w8 || wf8 ? (double)N * K + 4.0 * N : 4.0 * N * K) + 4.0 * ((double)M * K + (double)S * M * N)});
   last_split_ = a;
   last_split_op_ = ops.size() - 1;
   *S_out = S;

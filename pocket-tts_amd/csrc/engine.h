@@ -57,12 +57,14 @@ class Engine {
   void overlap_probe(int B, int reps, double* us);
   std::vector<std::string> plan_names(int B);
   int int8_matrices() const { return (int)q8map_.size(); }
+  int fp8_matrices() const { return (int)f8map_.size(); }
 
  private:
   float* dalloc(size_t n);
   const float* W(size_t off) const { return blob_ + off; }
   void upload_weights(TensorSource* src);
   void derive_int8();
+  void derive_fp8();
   void prefill_rows(std::vector<Op>& ops, int slot, int T, int p0);
   void run_ops(const std::vector<Op>& ops);
   std::vector<Op> build_step(int B);
@@ -88,6 +90,9 @@ class Engine {
   int wq_ = 0;  // weight_quant mode (QuantMode)
   // int8 code matrices of the quantized FlowLM step GEMMs: f32 weight pointer -> (codes, row scales)
   std::map<const float*, std::pair<const int8_t*, const float*>> q8map_;
+  int fp8_ = 0;  // ptts_engine_config.fp8_gemm
+  // e4m3 code matrices of the large FlowLM step GEMMs: f32 weight pointer -> (codes, row scales)
+  std::map<const float*, std::pair<const uint8_t*, const float*>> f8map_;
   bool own_blob_ = true, ready_ = false;
   hipStream_t stream_ = nullptr;
   Layout L_{};

@@ -65,6 +65,10 @@ struct GemmArgs {
   // wscale[n], formed per element before the MFMA. Replaces W when non-null.
   const int8_t* Wq;
   const float* wscale;
+  // fp8 W8A8 (ptts_engine_config.fp8_gemm; mode 0, split-K slabs only): W[n][k] ~= e4m3(Wf8[n][k])
+  // * wscale[n]; the A rows are quantized to e4m3 in-kernel with one scale per (row, K slice)
+  // and the tile runs on v_mfma_f32_32x32x16_fp8_fp8. Replaces W when non-null.
+  const uint8_t* Wf8;
   // split-K
   int S;
   float* partial;  // [S][M][N] when S > 1
@@ -96,6 +100,9 @@ void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
 // [-127, 127] for a blob packed by the quantizer); rows with s[n] == 0 get code 0. Any element
 // with float(q) * s[n] != W[n][k] (bitwise) increments *bad.
 void quant_codes(const float* W, const float* s, int N, int K, int8_t* q, int* bad, hipStream_t st);
+// fp8 (OCP e4m3) codes of W [N][K] with one scale per row: s[n] = max|W[n][:]| / 448
+void fp8_codes(const float* W, int N, int K, uint8_t* q, float* s, hipStream_t st);
+constexpr int FP8_KSLICE_MAX = 512;  // K elements per split-K slice the fp8 GEMM stages in LDS
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s);
 

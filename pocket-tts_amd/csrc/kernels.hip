@@ -968,6 +968,151 @@ void quant_codes(const float* W, const float* s, int N, int K, int8_t* q, int* b
   hipLaunchKernelGGL(k_quant_codes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, s, N, K, q, bad);
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp8 W8A8 split-K GEMM for the FlowLM step (ptts_engine_config.fp8_gemm; BASELINE configs[4]
+// "fp8 MFMA GEMM path"). Not a reference numeric: the reference has no fp8 (quantize.rs is a
+// simulated int8 grid), so this path is gated on accuracy against the f32 oracle.
+//   W: OCP e4m3 codes [N][K], one scale per row (fp8_codes). A: the workgroup's K slice of its
+//   32 rows is loaded once, each row's max |a| over the slice sets its scale (max/448), and the
+//   e4m3 codes go to LDS. v_mfma_f32_32x32x16_fp8_fp8 then runs the slice: lane (r, h) supplies
+//   the 16 bytes at k 32c+16h..+15 of A row r and of W row n as two 8-byte operands (A and B see
+//   the same k permutation, so the dot products are unchanged). Products of two e4m3 values are
+//   exact in f32; the slab value is acc * sa[row] * sw[col]. 4 waves deal the slice's 32-wide
+//   chunks round-robin (W loads one chunk ahead) and are summed through LDS as in k_gemm_w8.
+// ---------------------------------------------------------------------------------------------
+constexpr int F8_LDA = FP8_KSLICE_MAX + 16;  // LDS row stride (bytes): 16-B skew between rows
+
+template <int TN>
+__global__ __launch_bounds__(256) void k_gemm_fp8(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char sa8[32 * F8_LDA];
+  __shared__ float sas[32];
+  __shared__ float red[4 * 16 * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.x * 32 * TN, m0 = blockIdx.y * 32, z = blockIdx.z;
+  const int nchunks = a.K >> 5;
+  const int cb = (int)((long)nchunks * z / a.S), ce = (int)((long)nchunks * (z + 1) / a.S);
+  const int ks = 32 * (ce - cb);  // slice length (<= FP8_KSLICE_MAX, host-checked)
+  // ---- A slice: 8 threads per row, float4 j*8 + part; row max over the slice; e4m3 codes to LDS
+  {
+    const int row = tid >> 3, part = tid & 7;
+    const bool live = m0 + row < a.M;
+    const float* xr = a.X + (long)min(m0 + row, a.M - 1) * a.ldx + 32 * cb;
+    constexpr int NJ = FP8_KSLICE_MAX / 32;
+    float4 v[NJ];
+    float mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (live && 32 * j < ks) v[j] = *reinterpret_cast<const float4*>(xr + 4 * (8 * j + part));
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[j].x), fabsf(v[j].y)), fmaxf(fabsf(v[j].z), fabsf(v[j].w))));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+    const float inv = mx > 0.f ? 448.f / mx : 0.f;
+    if (part == 0) sas[row] = mx / 448.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if (32 * j < ks) {
+        int q = __builtin_amdgcn_cvt_pk_fp8_f32(v[j].x * inv, v[j].y * inv, 0, false);
+        q = __builtin_amdgcn_cvt_pk_fp8_f32(v[j].z * inv, v[j].w * inv, q, true);
+        *reinterpret_cast<int*>(&sa8[row * F8_LDA + 4 * (8 * j + part)]) = q;
+      }
+    }
+  }
+  __syncthreads();
+  const uint8_t* wrow[TN];
+  float sc[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int n = min(n0 + 32 * t + r, a.N - 1);
+    wrow[t] = a.Wf8 + (long)n * a.K + 16 * h;
+    sc[t] = a.wscale[n];
+  }
+  floatx16 acc[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
+  auto load = [&](int cc, uint4 (&Q)[TN]) {
+#pragma unroll
+    for (int t = 0; t < TN; ++t) Q[t] = *reinterpret_cast<const uint4*>(wrow[t] + (cc << 5));
+  };
+  auto mma = [&](int cc, uint4 (&Q)[TN]) {
+    const uint4 A = *reinterpret_cast<const uint4*>(&sa8[r * F8_LDA + 32 * (cc - cb) + 16 * h]);
+    const long a0 = (long)(((unsigned long)A.y << 32) | A.x), a1 = (long)(((unsigned long)A.w << 32) | A.z);
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const long b0 = (long)(((unsigned long)Q[t].y << 32) | Q[t].x);
+      const long b1 = (long)(((unsigned long)Q[t].w << 32) | Q[t].z);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a0, b0, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a1, b1, acc[t], 0, 0, 0);
+    }
+  };
+  uint4 q0[TN], q1[TN];
+  const int c = cb + wave;
+  const int n = c < ce ? (ce - c + 3) / 4 : 0;
+  const int clast = c + (n - 1) * 4;
+  auto chunk = [&](int i) { return i < n ? c + i * 4 : clast; };
+  if (n > 0) {
+    load(c, q0);
+    int i = 0;
+    for (; i + 2 <= n; i += 2) {
+      load(chunk(i + 1), q1);
+      mma(chunk(i), q0);
+      load(chunk(i + 2), q0);
+      mma(chunk(i + 1), q1);
+    }
+    if (i < n) mma(chunk(i), q0);
+  }
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[t][g];
+    __syncthreads();
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int g = wave * 4 + gg;
+      const float v = red[g * 64 + lane] + red[(16 + g) * 64 + lane] + red[(32 + g) * 64 + lane] +
+                      red[(48 + g) * 64 + lane];
+      const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
+      const int col = n0 + 32 * t + r;
+      if (m0 + row < a.M && col < a.N) a.partial[((long)z * a.M + m0 + row) * a.N + col] = v * sas[row] * sc[t];
+    }
+    __syncthreads();
+  }
+}
+
+// One workgroup per weight row: s = max|W[n][:]| / 448 (1 for an all-zero row), codes e4m3(W / s)
+__global__ __launch_bounds__(256) void k_fp8_codes(const float* W, int K, uint8_t* q, float* s) {
+  __shared__ float sh[4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float* w = W + (long)n * K;
+  float mx = 0.f;
+  for (int k = 4 * tid; k < K; k += 1024) {
+    const float4 v = *reinterpret_cast<const float4*>(w + k);
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((tid & 63) == 0) sh[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  const float sc = mx > 0.f ? mx / 448.f : 1.f, inv = 1.f / sc;
+  if (tid == 0) s[n] = sc;
+  for (int k = 4 * tid; k < K; k += 1024) {
+    const float4 v = *reinterpret_cast<const float4*>(w + k);
+    int c = __builtin_amdgcn_cvt_pk_fp8_f32(v.x * inv, v.y * inv, 0, false);
+    c = __builtin_amdgcn_cvt_pk_fp8_f32(v.z * inv, v.w * inv, c, true);
+    *reinterpret_cast<int*>(q + (long)n * K + k) = c;
+  }
+}
+
+void fp8_codes(const float* W, int N, int K, uint8_t* q, float* s, hipStream_t st) {
+  hipLaunchKernelGGL(k_fp8_codes, dim3((unsigned)N), dim3(256), 0, st, W, K, q, s);
+}
+
 template <int MODE>
 static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
   switch (a.layout) {
@@ -1048,6 +1193,10 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
 }
 
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s) {
+  if (a.Wf8) {  // fp8 W8A8: 32x64 tiles
+    hipLaunchKernelGGL((k_gemm_fp8<2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+    return;
+  }
   if (a.Wq) {  // int8 weights: 32x64 tiles
     hipLaunchKernelGGL((k_gemm_w8<2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
     return;

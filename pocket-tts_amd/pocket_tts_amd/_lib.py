@@ -35,6 +35,7 @@ class EngineConfig(C.Structure):
         ("defer_weights", C.c_int),
         ("pipeline", C.c_int),
         ("weight_quant", C.c_int),
+        ("fp8_gemm", C.c_int),
     ]
 
 
@@ -57,6 +58,7 @@ SIGNATURES = [
     ("ptts_quantize_tensor", C.c_int, [F32P, C.c_size_t, C.c_int, F32P, F32P]),
     ("ptts_quant_applies", C.c_int, [C.c_char_p, C.c_size_t, C.c_int]),
     ("ptts_engine_int8_matrices", C.c_int, [C.c_void_p]),
+    ("ptts_engine_fp8_matrices", C.c_int, [C.c_void_p]),
     ("ptts_engine_create", C.c_int, [C.POINTER(EngineConfig), C.POINTER(C.c_void_p)]),
     ("ptts_engine_finalize", C.c_int, [C.c_void_p]),
     ("ptts_engine_load_blob", C.c_int, [C.c_void_p, F32P, C.c_size_t]),

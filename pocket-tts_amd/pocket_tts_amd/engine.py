@@ -67,14 +67,16 @@ class StepResult:
 class Engine:
     def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
                  seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
-                 defer_weights: bool = False, pipeline: bool = False, weight_quant: int = 0):
+                 defer_weights: bool = False, pipeline: bool = False, weight_quant: int = 0, fp8_gemm: bool = False):
         """pipeline=True: overlapped stepping, each step() returns the frame produced by the
         previous call (see ptts_engine_config.pipeline). weight_quant: QUANT_NONE / QUANT_FLOW_LM /
         QUANT_ALL, the reference's simulated int8 weight quantization (quantize.rs), with the
-        FlowLM step GEMMs streaming int8 codes."""
+        FlowLM step GEMMs streaming int8 codes. fp8_gemm=True: the large FlowLM step GEMMs run as
+        fp8 W8A8 MFMA (accuracy-gated; see ptts_engine_config.fp8_gemm)."""
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
-                           weight_blob or None, int(defer_weights), int(pipeline), int(weight_quant))
+                           weight_blob or None, int(defer_weights), int(pipeline), int(weight_quant),
+                           int(fp8_gemm))
         h = C.c_void_p()
         check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
         self.handle = h
@@ -96,6 +98,11 @@ class Engine:
         check(lib().ptts_pack_weights_ex(seed, weights_path.encode() if weights_path else None, int(weight_quant),
                                          out.ctypes.data_as(F32P), out.nbytes))
         return out
+
+    @property
+    def fp8_matrices(self) -> int:
+        """FlowLM GEMM weight matrices on the fp8 W8A8 path (0 unless fp8_gemm)."""
+        return int(lib().ptts_engine_fp8_matrices(self.handle))
 
     @property
     def int8_matrices(self) -> int:

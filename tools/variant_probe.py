@@ -1,4 +1,4 @@
-"""Engine-variant probe: for each environment variant (JSON list of dicts on argv[1]), run in a fresh
+"""Engine-variant probe (FP8=1 / WQ=<mode> select the fp8 / int8 engines): for each environment variant (JSON list of dicts on argv[1]), run in a fresh
 process the bench workload (B = 32 rows, 125 pipelined steps after batched admission), report the
 steady ms/step and the HIP-event time of selected ops, and the max |diff| of the first 8 frames'
 latents / PCM against the first variant (so a variant that changes numerics shows it)."""
@@ -18,7 +18,8 @@ if len(sys.argv) > 2 and sys.argv[1] == "child":
     import pocket_tts_amd as pt
 
     ops = sys.argv[3].split(",") if len(sys.argv) > 3 and sys.argv[3] else []
-    eng = pt.Engine(device=0, max_slots=B, max_ctx=320, seed=0x5EED, pipeline=True)
+    eng = pt.Engine(device=0, max_slots=B, max_ctx=320, seed=0x5EED, pipeline=True,
+                    fp8_gemm=bool(int(os.environ.get("FP8", "0"))), weight_quant=int(os.environ.get("WQ", "0")))
     rng = np.random.default_rng(0)
     v = eng.voice_from_prompt((0.11 * rng.standard_normal((125, 1024))).astype(np.float32))
     res = {}
