@@ -19,8 +19,9 @@ HTTP (`create_app`, FastAPI; routes of pocket-tts-cli/src/server/routes.rs:20-30
   GET  /health             {"status": "healthy", "version": ...}
   POST /generate           JSON {text | token_ids, voice?, temperature?, eos_threshold?,
                            noise_clamp?, lsd_steps?} -> audio/wav (handlers.rs:128-213)
-  POST /stream             same body -> chunked 16-bit PCM LE, one chunk per frame
-                           (handlers.rs:215-310)
+  POST /stream             same body -> chunked 16-bit PCM LE (handlers.rs:215-310): the first
+                           frame as soon as it exists, later frames coalesced to at most one
+                           chunk per 5 ms per stream
   POST /v1/audio/speech    OpenAI body {model, input, voice?, response_format?} -> wav / pcm
                            (handlers.rs:380-398)
 Wire formats follow crates/pocket-tts/src/audio.rs:110-185 (clamp to [-1, 1], x 32767,
@@ -29,9 +30,11 @@ truncate to i16; 16-bit mono RIFF/WAVE).
 
 from __future__ import annotations
 
+import os
 import queue
 import struct
 import threading
+import time
 from collections import deque
 from dataclasses import dataclass, field
 from typing import Callable, Iterator, Sequence
@@ -58,6 +61,15 @@ class Request:
     out: "queue.Queue" = field(default_factory=queue.Queue)  # np.ndarray frames, then None
     slot: int = -1
     frames: int = 0
+    waker: Callable[[], None] | None = None  # set by an async consumer (HTTP /stream)
+    times: dict = field(default_factory=dict)  # submit / admit / first / last (time.time())
+
+    def put(self, item):
+        """Driver side: hand over a frame (np.ndarray), the end marker (None) or an error."""
+        self.out.put(item)
+        w = self.waker
+        if w is not None:
+            w()
 
     def stream(self, timeout: float | None = None) -> Iterator[np.ndarray]:
         """Frames [1920] float32 as they are produced; raises the driver's error if any."""
@@ -68,6 +80,29 @@ class Request:
             if isinstance(item, BaseException):
                 raise item
             yield item
+
+    def stream_batches(self, timeout: float | None = None) -> Iterator[np.ndarray]:
+        """Like stream(), but each item is every frame available at that moment, concatenated
+        (at least one): a client that falls behind the engine gets one HTTP chunk per backlog
+        instead of one per frame, so per-chunk server overhead cannot throttle the stream."""
+        done = False
+        while not done:
+            frames = [self.out.get(timeout=timeout)]
+            while True:
+                try:
+                    frames.append(self.out.get_nowait())
+                except queue.Empty:
+                    break
+            batch = []
+            for item in frames:
+                if item is None:
+                    done = True
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                batch.append(item)
+            if batch:
+                yield batch[0] if len(batch) == 1 else np.concatenate(batch)
 
     def audio(self, timeout: float | None = None) -> np.ndarray:
         frames = list(self.stream(timeout))
@@ -85,12 +120,14 @@ class BatchScheduler:
         self.cv = threading.Condition()
         self.running = True
         self.steps = 0
+        self.trace = bool(os.environ.get("PTTS_SERVE_TRACE"))
         self.thread = threading.Thread(target=self._loop, name="ptts-scheduler", daemon=True)
         self.thread.start()
 
     # -- client side
     def submit(self, ids, voice: Voice, params: GenerationParams) -> Request:
         req = Request(np.asarray(ids, np.int32).reshape(-1), voice, params)
+        req.times["submit"] = time.time()
         if voice.n_frames + req.ids.size + params.max_frames > self.engine.max_ctx:
             raise ValueError("voice + text + max_frames exceeds the engine's max_ctx")
         with self.cv:
@@ -121,44 +158,68 @@ class BatchScheduler:
         if batch:
             self.engine.open_many([r.slot for r in batch], [r.voice for r in batch], [r.ids for r in batch],
                                   [r.params for r in batch])
+            now = time.time()
             for r in batch:
+                r.times["admit"] = now
                 self.active[r.slot] = r
 
+    def _deliver(self, res, rows) -> list[int]:
+        done = []
+        for slot, req in list(self.active.items()):
+            if slot < rows and res.valid[slot]:
+                req.frames += 1
+                if req.frames == 1:
+                    req.times["first"] = time.time()
+                req.put(res.pcm[slot].copy())
+                if res.last[slot]:
+                    req.times["last"] = time.time()
+                    if self.trace:
+                        t = req.times
+                        print(f"ptts-serve slot {slot} frames {req.frames} admit_wait_ms "
+                              f"{1e3 * (t['admit'] - t['submit']):.1f} first_ms {1e3 * (t['first'] - t['submit']):.1f} "
+                              f"last_ms {1e3 * (t['last'] - t['submit']):.1f} steps {self.steps}", flush=True)
+                    req.put(None)
+                    done.append(slot)
+        return done
+
     def _loop(self):
+        # step k is launched (step_async) before the frames of step k-1 are handed out, so the
+        # host-side delivery overlaps the GPU; a finished row is released one step later (its
+        # extra step is computed and discarded: frame_valid = 0)
+        pending = None
         try:
             while True:
                 with self.cv:
-                    while self.running and not self.waiting and not self.active:
+                    while self.running and not self.waiting and not self.active and pending is None:
                         self.cv.wait()
                     if not self.running:
                         break
                     self._admit()
-                    rows = max(self.active) + 1
-                res = self.engine.step(rows)
-                self.steps += 1
-                done = []
-                for slot, req in list(self.active.items()):
-                    if slot < rows and res.valid[slot]:
-                        req.frames += 1
-                        req.out.put(res.pcm[slot].copy())
-                        if res.last[slot]:
-                            req.out.put(None)
-                            done.append(slot)
-                with self.cv:
-                    for slot in done:
-                        del self.active[slot]
+                    rows = max(self.active) + 1 if self.active else 0
+                if rows:
+                    self.engine.step_async(rows)
+                if pending is not None:
+                    done = self._deliver(*pending)
+                    with self.cv:
+                        for slot in done:
+                            del self.active[slot]
+                    pending = None
+                if rows:
+                    self.engine.sync()
+                    pending = (self.engine.fetch(rows), rows)
+                    self.steps += 1
         except BaseException as e:  # deliver the failure to every waiting client
             with self.cv:
                 self.running = False
                 for req in list(self.active.values()) + list(self.waiting):
-                    req.out.put(e)
-                    req.out.put(None)
+                    req.put(e)
+                    req.put(None)
                 self.active.clear()
                 self.waiting.clear()
         finally:
             with self.cv:
                 for req in list(self.active.values()) + list(self.waiting):
-                    req.out.put(None)
+                    req.put(None)
 
 
 class MultiGpuScheduler:
@@ -254,6 +315,56 @@ class OpenAIRequest(BaseModel):
     token_ids: list[int] | None = None
 
 
+CHUNK_INTERVAL_S = 0.005  # /stream: at most one chunk per stream per 5 ms after the first
+
+
+async def pcm_chunks(r: Request):
+    """/stream body without a worker thread per stream. The driver's put() wakes this coroutine
+    on the event loop (call_soon_threadsafe, at most one pending wake per stream); each wake
+    sends every frame available at that moment as ONE chunk of 16-bit PCM, then the stream
+    waits CHUNK_INTERVAL_S before the next. The first frame goes out as soon as it exists; later
+    frames coalesce, so 32 streams of a GPU producing ~1000x real time cost at most 200 chunks/s
+    each instead of one event-loop round trip per 80-ms frame (which throttled the whole server).
+    """
+    import asyncio
+
+    loop = asyncio.get_running_loop()
+    ev = asyncio.Event()
+    armed = [False]
+
+    def wake():
+        if armed[0]:
+            armed[0] = False
+            loop.call_soon_threadsafe(ev.set)
+
+    r.waker = wake
+    while True:
+        items = []
+        while True:
+            try:
+                items.append(r.out.get_nowait())
+            except queue.Empty:
+                break
+        batch, done = [], False
+        for item in items:
+            if item is None:
+                done = True
+                break
+            if isinstance(item, BaseException):
+                raise item
+            batch.append(item)
+        if batch:
+            yield pcm_i16_le_bytes(batch[0] if len(batch) == 1 else np.concatenate(batch))
+        if done:
+            return
+        if batch:
+            await asyncio.sleep(CHUNK_INTERVAL_S)
+        ev.clear()
+        armed[0] = True
+        if r.out.empty():
+            await ev.wait()
+
+
 def create_app(service: TTSService):
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import JSONResponse, Response, StreamingResponse
@@ -276,9 +387,9 @@ def create_app(service: TTSService):
         return Response(wav_bytes(r.audio()), media_type="audio/wav")
 
     @app.post("/stream")
-    def stream(req: GenerateRequest):
+    async def stream(req: GenerateRequest):
         r = submit(**req.model_dump())
-        return StreamingResponse((pcm_i16_le_bytes(f) for f in r.stream()), media_type="audio/pcm")
+        return StreamingResponse(pcm_chunks(r), media_type="audio/pcm")
 
     @app.post("/v1/audio/speech")
     def openai_speech(req: OpenAIRequest):
@@ -308,6 +419,12 @@ def main(argv=None):
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
     args = ap.parse_args(argv)
+    # the scheduler thread drops the GIL in every engine call; with the default 5 ms switch
+    # interval it can wait that long to get it back from the HTTP threads (one engine step is
+    # < 1 ms), so hand the GIL over sooner
+    import sys
+
+    sys.setswitchinterval(2e-4)
     engines = [Engine(device=d, max_slots=args.slots, max_ctx=args.max_ctx, weights_path=args.weights, pipeline=True)
                for d in range(args.gpus)]
     voices: dict[str, list[Voice]] = {}

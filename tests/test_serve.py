@@ -59,6 +59,18 @@ class FakeEngine:
         r.pcm[:m], r.valid[:m], r.last[:m] = prev["pcm"][:m], prev["valid"][:m], prev["last"][:m]
         return r
 
+    # split form of step() (ptts_step_async / ptts_sync / ptts_fetch), used by the scheduler
+    def step_async(self, n):
+        self._issued = (self.step(n), n)
+
+    def sync(self):
+        pass
+
+    def fetch(self, n):
+        r, m = self._issued
+        assert m == n
+        return r
+
 
 VOICE = SimpleNamespace(n_frames=10)
 
@@ -130,3 +142,20 @@ def test_http_routes():
         assert c.post("/generate", json={}).status_code == 400
     finally:
         sch.close()
+
+
+def test_stream_batches_coalesces_backlog():
+    """A client behind the engine receives every frame already produced as one chunk, in order."""
+    from pocket_tts_amd.serve import Request
+
+    req = Request(np.zeros(3, np.int32), VOICE, params(5))
+    for k in range(3):
+        req.out.put(np.full(1920, k, np.float32))
+    it = req.stream_batches(timeout=1)
+    first = next(it)
+    assert first.shape == (3 * 1920,) and [int(first[i * 1920]) for i in range(3)] == [0, 1, 2]
+    req.out.put(np.full(1920, 3, np.float32))
+    req.out.put(None)
+    rest = list(it)
+    assert len(rest) == 1 and rest[0].shape == (1920,) and int(rest[0][0]) == 3
+

@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""HTTP load test of the serving front end on ONE GPU (BASELINE configs[3] at one GPU's share:
+256 utterances over 8 GPUs = 32 concurrent streams per GPU; the 8-GPU node is the driver's).
+
+The launcher never touches the GPU. It starts (1) the server, `python -m pocket_tts_amd.serve`
+(real engine, pipelined, 32 slots, a synthetic 125-frame voice prompt) on 127.0.0.1, and (2)
+client processes, so the load generator does not share the server's interpreter. Each client
+thread POSTs /stream (chunked 16-bit PCM) with 40 token ids and eos_threshold = +1e9 (no EOS:
+each request runs its max_gen_len = 22 * 13 = 286 frames, the tts_model.rs:968-969 rule for 40
+ids). Reports whole-job audio-sec/wall-sec through HTTP and the p50 / p90 time to first chunk.
+
+  python tools/serve_load.py [--clients 32] [--procs 4] [--rounds 2] [--port 8765] [--out f.json]"""
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(HERE, "..", "pocket-tts_amd")
+
+
+def ids(i):
+    return [(k * 97 + 13 + 7 * i) % 4000 for k in range(40)]
+
+
+def client(port, first, n, t_go):
+    """n streams (ids first..first+n-1) in threads, all released at wall time t_go (shared by
+    every client process); prints one JSON line per stream."""
+    import httpx
+
+    base = f"http://127.0.0.1:{port}"
+    out = [None] * n
+    # one client per thread, built and connected before the clock starts (building an httpx
+    # client loads a CA bundle: ~tens of ms under the GIL, which is client cost, not serving)
+    clients = [httpx.Client(timeout=300.0) for _ in range(n)]
+    for c in clients:
+        c.get(base + "/health")
+    go = threading.Barrier(n)
+
+    def one(j):
+        go.wait()
+        time.sleep(max(0.0, t_go - time.time()))
+        t0 = time.time()
+        t_first, nbytes = None, 0
+        with clients[j].stream("POST", base + "/stream", json={"token_ids": ids(first + j), "eos_threshold": 1e9}) as r:
+            r.raise_for_status()
+            for chunk in r.iter_bytes():
+                if t_first is None and chunk:
+                    t_first = time.time()
+                nbytes += len(chunk)
+        out[j] = {"start": t0, "first": t_first, "end": time.time(), "samples": nbytes // 2}
+
+    ts = [threading.Thread(target=one, args=(j,)) for j in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=32)
+    ap.add_argument("--procs", type=int, default=4)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--port", type=int, default=8765)
+    ap.add_argument("--out", default="")
+    ap.add_argument("--workdir", default=os.path.join(HERE, "..", "gpurun_out"))
+    args = ap.parse_args()
+
+    import httpx
+
+    os.makedirs(args.workdir, exist_ok=True)
+    prompt_path = os.path.join(args.workdir, "serve_load_prompt.npy")
+    np.save(prompt_path, (0.11 * np.random.default_rng(1).standard_normal((125, 1024))).astype(np.float32))
+    env = dict(os.environ, PYTHONPATH=os.path.abspath(PKG) + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    log = open(os.path.join(args.workdir, "serve_load_server.log"), "w")
+    server = subprocess.Popen([sys.executable, "-m", "pocket_tts_amd.serve", "--voice", f"synth={prompt_path}",
+                               "--slots", "32", "--max-ctx", "480", "--port", str(args.port)],
+                              env=env, stdout=log, stderr=subprocess.STDOUT)
+    try:
+        base = f"http://127.0.0.1:{args.port}"
+        for _ in range(1200):  # first import torch / engine build on a fresh box can take a while
+            if server.poll() is not None:
+                raise SystemExit(f"server exited with {server.returncode}")
+            try:
+                if httpx.get(base + "/health", timeout=1.0).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                time.sleep(0.1)
+        result = {"clients": args.clients, "procs": args.procs, "route": "/stream", "rounds": []}
+        per = [args.clients // args.procs + (1 if p < args.clients % args.procs else 0) for p in range(args.procs)]
+        for rnd in range(args.rounds):
+            procs, first = [], 0
+            t_go = time.time() + 3.0  # client processes start, import httpx and connect first
+            for n in per:
+                procs.append(subprocess.Popen([sys.executable, __file__, "client", str(args.port), str(first), str(n),
+                                               repr(t_go)], stdout=subprocess.PIPE, text=True))
+                first += n
+            streams = []
+            for p in procs:
+                o, _ = p.communicate(timeout=600)
+                if p.returncode != 0:
+                    raise SystemExit(f"client failed ({p.returncode})")
+                streams += json.loads(o.strip().splitlines()[-1])
+            t0 = min(s["start"] for s in streams)
+            wall = max(s["end"] for s in streams) - t0
+            samples = sum(s["samples"] for s in streams)
+            ttfc = sorted(s["first"] - s["start"] for s in streams)
+            rec = {"round": rnd, "wall_s": round(wall, 3), "audio_s": round(samples / 24000.0, 2),
+                   "audio_sec_per_wall_sec": round(samples / 24000.0 / wall, 2),
+                   "frames_per_request": streams[0]["samples"] // 1920,
+                   "ttfc_p50_ms": round(1e3 * ttfc[len(ttfc) // 2], 2),
+                   "ttfc_p90_ms": round(1e3 * ttfc[int(0.9 * (len(ttfc) - 1))], 2)}
+            result["rounds"].append(rec)
+            print(json.dumps(rec), flush=True)
+        r = httpx.post(base + "/v1/audio/speech", json={"token_ids": ids(0), "response_format": "wav"}, timeout=120)
+        r.raise_for_status()
+        result["openai_wav_bytes"] = len(r.content)
+        if args.out:
+            json.dump(result, open(args.out, "w"), indent=1)
+    finally:
+        server.terminate()
+        try:
+            server.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            server.kill()
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "client":
+        client(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5]))
+    else:
+        main()
