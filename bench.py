@@ -51,6 +51,13 @@ def measured_traffic(op):
     return t["ops"][op]["hbm_bytes_per_launch"], t.get("source")
 
 
+def measured_mfma():
+    """Per-op MFMA busy cycles from the committed rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES pass
+    (tools/prof_ops.py mfma), {} if absent."""
+    path = ROOT / "profiles" / "mfma.json"
+    return json.load(open(path))["ops"] if path.exists() else {}
+
+
 def phase_rooflines(per_op, plan, B, K):
     """SURVEY §8(d) per-phase rooflines over one batched step, from the per-op HIP-event times
     (each op timed alone; the plan lists every launch of the step, repeated ops counted per launch):
@@ -67,12 +74,17 @@ def phase_rooflines(per_op, plan, B, K):
     b_flops = B * (525.1e6 + 65_536 * 266)
     fa = f_bytes / (front * 1e-6) / 1e9
     ba = b_flops / (back * 1e-6) / 1e12
+    mf = measured_mfma()  # rocprof MFMA busy over the back ops, against 1,024 SIMDs at 2.4 GHz
+    bops = [n for n, _, _ in plan if (n.startswith(("mimi.", "seanet.")) or n == "commit") and n in mf]
+    busy = sum(mf[n]["mfma_busy_cycles"] for n in bops)
+    dur = sum(mf[n]["rocprof_avg_us"] for n in bops)
     return {
         "front": {"bound": "hbm", "algorithmic_bytes": round(f_bytes), "sum_op_us": round(front, 1),
                   "achieved": round(fa, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fa / HBM_PEAK_GBS, 4)},
         "back": {"bound": "mfma", "algorithmic_flops": round(b_flops), "sum_op_us": round(back, 1),
                  "achieved": round(ba, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                 "frac": round(ba / F32_PEAK_TFLOPS, 4)},
+                 "frac": round(ba / F32_PEAK_TFLOPS, 4),
+                 "rocprof_mfma_busy_frac": round(busy / (1024 * 2.4e9 * dur * 1e-6), 4) if dur else None},
     }
 
 
@@ -228,6 +240,8 @@ def main():
                     "unit": "TFLOP/s"}
         roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
         roof["traffic"], roof["traffic_source"] = measured_traffic(name)
+        mf = measured_mfma().get(name)
+        roof["rocprof_mfma_busy_frac"] = mf["util_peak_clock"] if mf else None
         roof["kernel"] = name
         roof["avg_us"] = round(us, 2)
         roof["algorithmic_bytes"] = by

@@ -57,5 +57,18 @@ if [ "${PMC:-0}" = "1" ]; then
         "$OUT/pmc_$C.json"
   done
   python tools/prof_ops.py traffic "$OUT/pmc_FETCH_SIZE.json" "$OUT/pmc_WRITE_SIZE.json" "$OUT/traffic.json"
+  # MFMA utilisation: one pass with both counters (1 SQ_ + 1 GRBM_ counter: within one pass's limits)
+  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmc_mfma" \
+      -o run --output-format csv \
+      -- python "$ROOT/bench.py" --steps 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-pipeline --no-quant-variant \
+      > "$OUT/pmc_mfma.log" 2>&1)
+  rc=$?
+  echo "pmc mfma rc=$rc"; tail -n 2 "$OUT/pmc_mfma.log"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+  for C in SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE; do
+    python tools/prof_ops.py counters "$OUT/pmc_mfma/run_counter_collection.csv" "$OUT/bench_ops.json" $C "$OUT/pmc_$C.json"
+  done
+  python tools/prof_ops.py mfma "$OUT/pmc_SQ_VALU_MFMA_BUSY_CYCLES.json" "$OUT/pmc_GRBM_GUI_ACTIVE.json" \
+      "$OUT/op_stats.csv" "$OUT/mfma.json"
 fi
 exit 0

@@ -101,6 +101,32 @@ def cmd_traffic(fetch_path, write_path, out_path):
     print(f"traffic for {len(ops)} ops")
 
 
+def cmd_mfma(busy_path, gui_path, op_stats_path, out_path):
+    """Per-op MFMA utilisation from one --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE pass:
+    busy = SIMD cycles the matrix core was busy, summed over the 1,024 SIMDs (MI355X_MICROARCH.md:
+    32 per v_mfma_f32_32x32x16_bf16, 64 per v_mfma_f32_32x32x2_f32, so flops/64 for f32 32x32x2);
+    util_peak_clock = busy / (1024 SIMDs x 2.4 GHz x duration) (the 157.3 TF fp32 peak's clock);
+    util_eff_clock uses the dispatch's own clock GRBM_GUI_ACTIVE / 8 XCDs (reads high on short
+    dispatches). Durations are the rocprofv3 per-dispatch averages of op_stats.csv."""
+    busy = json.load(open(busy_path))["ops"]
+    gui = json.load(open(gui_path))["ops"]
+    stats = {r["op"]: r for r in csv.DictReader(open(op_stats_path))}
+    ops = {}
+    for op, b in busy.items():
+        if op not in stats or b <= 0:
+            continue
+        us = float(stats[op]["rocprof_avg_us"])
+        fl = float(stats[op]["flops"] or 0)
+        cyc_eff = gui.get(op, 0.0) / 8.0
+        ops[op] = {"mfma_busy_cycles": b, "flops_over_64": fl / 64.0, "rocprof_avg_us": us,
+                   "util_peak_clock": round(b / (1024 * 2.4e9 * us * 1e-6), 4),
+                   "util_eff_clock": round(b / (1024 * cyc_eff), 4) if cyc_eff > 0 else None,
+                   "eff_clock_ghz": round(cyc_eff / (us * 1e3), 3)}
+    json.dump({"source": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE pass of bench.py, attributed "
+                         "per op by tools/prof_ops.py", "ops": ops}, open(out_path, "w"), indent=1)
+    print(f"mfma utilisation for {len(ops)} ops")
+
+
 if __name__ == "__main__":
     cmd, args = sys.argv[1], sys.argv[2:]
-    {"trace": cmd_trace, "counters": cmd_counters, "traffic": cmd_traffic}[cmd](*args)
+    {"trace": cmd_trace, "counters": cmd_counters, "traffic": cmd_traffic, "mfma": cmd_mfma}[cmd](*args)
