@@ -1,0 +1,98 @@
+"""Edge cases of the C-ABI boundary on the GPU: argument errors surface as PocketTTSError (the
+reference's anyhow::Error -> PyRuntimeError mapping, pocket-tts-bindings/src/lib.rs:17) and leave
+the engine usable; an empty text segment and a context filled to exactly max_ctx run to the end
+and match the oracle."""
+
+import numpy as np
+import pytest
+from conftest import load_golden, rms
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(**kw):
+    from pocket_tts_amd import GenerationParams
+
+    base = dict(temp=0.0, eos_threshold=float("inf"), max_frames=4)
+    base.update(kw)
+    return GenerationParams(**base)
+
+
+def test_boundary_errors_leave_engine_usable(gpu_engine, oracle):
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    v = gpu_engine.voice_from_prompt(d["prompt"][:6])
+    ids = np.array([260, 2994, 262], np.int32)
+    n = gpu_engine.max_slots
+    bad = [
+        lambda: gpu_engine.step(0),
+        lambda: gpu_engine.step(n + 1),
+        lambda: gpu_engine.open(n, v, ids, _params()),  # slot out of range
+        lambda: gpu_engine.open(-1, v, ids, _params()),
+        lambda: gpu_engine.open(0, v, np.array([4001], np.int32), _params()),  # token id past the vocab
+        lambda: gpu_engine.open(0, v, ids, _params(max_frames=0)),
+        lambda: gpu_engine.open(0, v, ids, _params(frames_after_eos=-1)),
+        lambda: gpu_engine.open(0, v, ids, _params(max_frames=gpu_engine.max_ctx)),  # context overflow
+        lambda: gpu_engine.voice_from_prompt(np.zeros((gpu_engine.max_ctx, 1024), np.float32)),
+    ]
+    for i, f in enumerate(bad):
+        with pytest.raises(pt.PocketTTSError):
+            f()
+    # still works, and matches the oracle
+    gpu_engine.open(0, v, ids, _params(max_frames=3))
+    s = oracle.new_state(256)
+    s.prefill(d["prompt"][:6])
+    s.prefill_tokens(ids)
+    lat = None
+    for _ in range(3):
+        r = gpu_engine.step(1)
+        ref = s.step(lat)
+        lat = ref["latent"]
+        np.testing.assert_allclose(r.latents[0], ref["latent"], atol=1e-4)
+        assert rms(r.pcm[0] - ref["pcm"]) <= 1e-4
+
+
+def test_empty_text_segment_matches_oracle(gpu_engine, oracle):
+    """0 text tokens: the step runs on the voice prefix alone (ptts_slot_open accepts n_ids = 0)."""
+    d = load_golden("e2e_lsd1.safetensors")
+    prompt = d["prompt"][:8]
+    gpu_engine.open(1, gpu_engine.voice_from_prompt(prompt), np.zeros(0, np.int32), _params(max_frames=3))
+    s = oracle.new_state(256)
+    s.prefill(prompt)
+    lat = None
+    for i in range(3):
+        r = gpu_engine.step(2)
+        ref = s.step(lat)
+        lat = ref["latent"]
+        assert r.valid[1] and r.last[1] == (i == 2)
+        np.testing.assert_allclose(r.latents[1], ref["latent"], atol=1e-4)
+        assert rms(r.pcm[1] - ref["pcm"]) <= 1e-4
+
+
+def test_context_filled_to_max_ctx(oracle):
+    """voice + text + max_frames == max_ctx exactly: every frame matches the oracle and the row
+    ends on its max_frames-th frame (the KV cache's last position is written by the last step)."""
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    F, ids = 9, d["text_ids"][:5]
+    frames = 18
+    max_ctx = F + ids.size + frames
+    eng = pt.Engine(device=0, max_slots=1, max_ctx=max_ctx, seed=0x5EED)
+    try:
+        eng.open(0, eng.voice_from_prompt(d["prompt"][:F]), ids, _params(max_frames=frames))
+        s = oracle.new_state(256)
+        s.prefill(d["prompt"][:F])
+        s.prefill_tokens(ids)
+        lat = None
+        for i in range(frames):
+            r = eng.step(1)
+            ref = s.step(lat)
+            lat = ref["latent"]
+            assert r.valid[0] and r.last[0] == (i == frames - 1)
+            np.testing.assert_allclose(r.latents[0], ref["latent"], atol=1e-4)
+            assert rms(r.pcm[0] - ref["pcm"]) <= 1e-4
+        assert not eng.step(1).valid[0]  # finished rows report no frame
+    finally:
+        eng.close()
