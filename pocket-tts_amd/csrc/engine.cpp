@@ -31,6 +31,10 @@ float* Engine::dalloc(size_t n) {
   void* p = nullptr;
   PTTS_HIP(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(float)));
   PTTS_HIP(hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(float)));
+  // hipMemset runs on the null stream, which does not order against the engine's non-blocking
+  // streams: wait for it, or a kernel that fills the buffer next on stream_ can be overwritten
+  // by the zeroing (seen: the transposed input-projection weight zeroed under quantized engines)
+  PTTS_HIP(hipDeviceSynchronize());
   allocs_.push_back(p);
   return (float*)p;
 }
@@ -213,6 +217,13 @@ void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   if (fp8_ && f8map_.empty()) derive_fp8();
+  if (!inw_t_) {  // every element is written by the transpose below: no (null-stream) memset
+    void* p = nullptr;
+    PTTS_HIP(hipMalloc(&p, sizeof(float) * LDIM * D));
+    allocs_.push_back(p);
+    inw_t_ = (float*)p;
+  }
+  transpose(W(L_.input_linear), D, LDIM, inw_t_, stream_);
   TimeEmbedWeights tw;
   for (int i = 0; i < 2; ++i) {
     tw.l1w[i] = W(L_.te_l1w[i]);
@@ -568,7 +579,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
   int S = 1;
   // ---- FlowLM step (flow_lm.rs:98-164): input_linear -> transformer -> out_norm
   {
-    const float *lat = lat_in_, *w = W(L_.input_linear), *lw = W(L_.fl[0].n1w), *lb = W(L_.fl[0].n1b);
+    const float *lat = lat_in_, *w = inw_t_, *lw = W(L_.fl[0].n1w), *lb = W(L_.fl[0].n1b);
     float *x = x_, *h = h_;
     ops.push_back({"flow.input_ln1", [=](hipStream_t s) { input_ln(lat, w, lw, lb, x, h, B, s); },
                    2.0 * B * D * LDIM, 4.0 * ((double)D * LDIM + (double)B * (LDIM + 2 * D))});

@@ -125,6 +125,7 @@ class Engine {
   bool head_chain_ = true;
   bool use_head_chain(int B) const;
   float *hxp_ = nullptr, *hup_ = nullptr;
+  float* inw_t_ = nullptr;  // input_linear weight transposed, [32][1024] (k_input_ln)
   int *hctr_ = nullptr, *herr_ = nullptr;
   float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;
   float* a0_ = nullptr;

@@ -193,8 +193,10 @@ struct FlowHeadArgs {
 };
 bool flow_head_fits(int B);
 // FlowLM input_linear (32 -> 1024, no bias) + layer-0 norm1: x = lat W^T, h = LN(x) (eps 1e-5).
-void input_ln(const float* lat, const float* W, const float* lnw, const float* lnb, float* x, float* h, int M,
+void input_ln(const float* lat, const float* Wt, const float* lnw, const float* lnb, float* x, float* h, int M,
               hipStream_t s);
+// dst [cols][rows] = src [rows][cols]^T
+void transpose(const float* src, int rows, int cols, float* dst, hipStream_t s);
 void flow_head(const FlowHeadArgs& a, hipStream_t s);
 
 // End of the front part: EOS state machine (tts_model.rs:1055-1063), frame flags, the frame's

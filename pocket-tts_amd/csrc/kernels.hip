@@ -2703,7 +2703,9 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
 // FlowLM input projection + the first layer's norm1 in one launch (flow_lm.rs:117 input_linear,
 // transformer.rs:66-90 norm1): x[m] = lat[m] W^T (K = 32, no bias), h[m] = LN(x[m]) (eps 1e-5).
 // One workgroup per row, 4 output columns per thread; replaces a split-K GEMM + row reduce.
-__global__ __launch_bounds__(256) void k_input_ln(const float* __restrict__ lat, const float* __restrict__ W,
+// The weight arrives transposed, Wt [32][1024] (made at finalize), so the 64 lanes of a wave read
+// one contiguous 1-KB run of Wt[k] per load instead of 64 rows 512 B apart.
+__global__ __launch_bounds__(256) void k_input_ln(const float* __restrict__ lat, const float* __restrict__ Wt,
                                                   const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                   float* __restrict__ x, float* __restrict__ h) {
   __shared__ float sh[4];
@@ -2711,15 +2713,18 @@ __global__ __launch_bounds__(256) void k_input_ln(const float* __restrict__ lat,
   float4 lv[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) lv[j] = *reinterpret_cast<const float4*>(lat + (long)m * 32 + 4 * j);
+  float4 wv[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) wv[k] = *reinterpret_cast<const float4*>(Wt + (long)k * 1024 + n);
   float acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float* w = W + (long)(n + q) * 32;
     float t = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float4 wv = *reinterpret_cast<const float4*>(w + 4 * j);
-      t += (lv[j].x * wv.x + lv[j].y * wv.y) + (lv[j].z * wv.z + lv[j].w * wv.w);
+    for (int j = 0; j < 8; ++j) {  // same summation order as the row-major form: ((k0 k1) + (k2 k3)) per float4
+      const float a0 = lv[j].x * (&wv[4 * j].x)[q], a1 = lv[j].y * (&wv[4 * j + 1].x)[q];
+      const float a2 = lv[j].z * (&wv[4 * j + 2].x)[q], a3 = lv[j].w * (&wv[4 * j + 3].x)[q];
+      t += (a0 + a1) + (a2 + a3);
     }
     acc[q] = t;
   }
@@ -2733,9 +2738,21 @@ __global__ __launch_bounds__(256) void k_input_ln(const float* __restrict__ lat,
       make_float4(d.x / den * w4.x + b4.x, d.y / den * w4.y + b4.y, d.z / den * w4.z + b4.z, d.w / den * w4.w + b4.w);
 }
 
-void input_ln(const float* lat, const float* W, const float* lnw, const float* lnb, float* x, float* h, int M,
+void input_ln(const float* lat, const float* Wt, const float* lnw, const float* lnb, float* x, float* h, int M,
               hipStream_t s) {
-  hipLaunchKernelGGL(k_input_ln, dim3(M), dim3(256), 0, s, lat, W, lnw, lnb, x, h);
+  hipLaunchKernelGGL(k_input_ln, dim3(M), dim3(256), 0, s, lat, Wt, lnw, lnb, x, h);
+}
+
+__global__ void k_transpose(const float* src, int rows, int cols, float* dst) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)rows * cols) return;
+  const int r = (int)(i / cols), c = (int)(i % cols);
+  dst[(long)c * rows + r] = src[i];
+}
+
+void transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) {
+  const long n = (long)rows * cols;
+  hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, cols, dst);
 }
 
 bool flow_head_fits(int B) { return B >= 1 && B <= 128; }
