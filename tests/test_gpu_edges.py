@@ -96,3 +96,38 @@ def test_context_filled_to_max_ctx(oracle):
         assert not eng.step(1).valid[0]  # finished rows report no frame
     finally:
         eng.close()
+
+
+def test_http_stream_route_on_real_engine(oracle):
+    """The HTTP surface over the real pipelined engine (FastAPI TestClient, in process): two
+    /stream requests at temperature 0 with token ids return 16-bit PCM equal to each request's
+    oracle run (to 1 LSB), with max_gen_len frames (tts_model.rs:968-969 rule: 4 ids -> 52)."""
+    import pocket_tts_amd as pt
+    from fastapi.testclient import TestClient
+    from pocket_tts_amd.serve import BatchScheduler, TTSService, create_app
+
+    d = load_golden("e2e_lsd1.safetensors")
+    prompt = d["prompt"][:6]
+    eng = pt.Engine(device=0, max_slots=2, max_ctx=128, seed=0x5EED, pipeline=True)
+    sch = BatchScheduler(eng)
+    try:
+        svc = TTSService(sch, {"v": eng.voice_from_prompt(prompt)}, default_voice="v", temp=0.0)
+        client = TestClient(create_app(svc))
+        for ids in ([260, 2994, 262, 578], [17, 4, 3999, 1200]):
+            r = client.post("/stream", json={"token_ids": ids, "temperature": 0.0, "eos_threshold": 1e9})
+            assert r.status_code == 200
+            got = np.frombuffer(r.content, "<i2")
+            assert got.size == 52 * 1920
+            s = oracle.new_state(128)
+            s.prefill(prompt)
+            s.prefill_tokens(np.array(ids, np.int32))
+            lat, ref = None, []
+            for _ in range(52):
+                o = s.step(lat)
+                lat = o["latent"]
+                ref.append(o["pcm"])
+            want = np.clip(np.concatenate(ref), -1.0, 1.0) * 32767.0
+            assert np.abs(got.astype(np.float64) - want).max() <= 1.01  # truncation to i16 + f32 noise
+    finally:
+        sch.close()
+        eng.close()
