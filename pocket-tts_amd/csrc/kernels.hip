@@ -1999,28 +1999,46 @@ __global__ __launch_bounds__(256) void k_flow_cond(const float* P, int S, int B,
                                                    float* eos_out) {
   const int b = blockIdx.x, tid = threadIdx.x;
   const int NC = 513;  // cond_embed (512) | out_eos (1)
-  for (int n = tid; n < 512; n += 256) {
-    float c = 0.f;
-    c = slab_sum(P + (long)b * NC + n, (long)B * NC, S);
-    c += bias[n];
-    for (int s = 0; s < lsd; ++s) ysilu[((long)s * B + b) * 512 + n] = silu(temb[s * 512 + n] + c);
+  // every load of the thread first (its two columns' slabs, thread 0's EOS slabs, the slot
+  // state of the noise lanes), then the arithmetic: one memory round trip, not four
+  const long zs = (long)B * NC;
+  const float* p0 = P + (long)b * NC + tid;
+  float v0[16], v1[16], ve[16];
+#pragma unroll
+  for (int z = 0; z < 16; ++z) {
+    v0[z] = z < S ? p0[z * zs] : 0.f;
+    v1[z] = z < S ? p0[z * zs + 256] : 0.f;
+    ve[z] = (z < S && tid == 0) ? P[(long)b * NC + 512 + z * zs] : 0.f;
   }
   const SlotState& ss = st[b];
-  if (tid == 0) {  // out_eos logit (flow_lm.rs:139-145); the EOS rule runs in front_commit
-    float e = 0.f;
-    e = slab_sum(P + (long)b * NC + 512, (long)B * NC, S);
-    eos_out[b] = e + bias[512];
+  const float temp = ss.temp, clamp = ss.noise_clamp;
+  const unsigned long long seed = ss.seed;
+  const int step = ss.step;
+  const float b0 = bias[tid], b1 = bias[tid + 256], be = bias[512];
+  float c0 = 0.f, c1 = 0.f, e = 0.f;
+#pragma unroll
+  for (int z = 0; z < 16; ++z)
+    if (z < S) {
+      c0 += v0[z];
+      c1 += v1[z];
+      e += ve[z];
+    }
+  c0 += b0;
+  c1 += b1;
+  for (int s = 0; s < lsd; ++s) {
+    ysilu[((long)s * B + b) * 512 + tid] = silu(temb[s * 512 + tid] + c0);
+    ysilu[((long)s * B + b) * 512 + tid + 256] = silu(temb[s * 512 + tid + 256] + c1);
   }
+  if (tid == 0) eos_out[b] = e + be;  // out_eos logit (flow_lm.rs:139-145); the EOS rule runs in front_commit
   if (tid < 32) {
     float x0 = 0.f;
-    const float temp = ss.temp;
     if (temp > 0.f) {  // flow_lm.rs:39-65: N(0, sqrt(temp)), optionally truncated to |x| <= clamp
       const float sd = sqrtf(temp);
-      x0 = sd * normal_at(ss.seed, ss.step, tid, 0);
-      if (ss.noise_clamp > 0.f) {
+      x0 = sd * normal_at(seed, step, tid, 0);
+      if (clamp > 0.f) {
         int att = 1;
-        while (fabsf(x0) > ss.noise_clamp && att < 64) x0 = sd * normal_at(ss.seed, ss.step, tid, att++);
-        x0 = fminf(fmaxf(x0, -ss.noise_clamp), ss.noise_clamp);
+        while (fabsf(x0) > clamp && att < 64) x0 = sd * normal_at(seed, step, tid, att++);
+        x0 = fminf(fmaxf(x0, -clamp), clamp);
       }
     }
     cur[b * 32 + tid] = x0;
