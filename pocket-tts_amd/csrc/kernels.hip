@@ -2150,10 +2150,11 @@ __global__ __launch_bounds__(64) void k_front_commit(FrontCommitArgs a) {
   const int b = blockIdx.x, t = threadIdx.x;
   SlotState& ss = a.st[b];
   const int valid = ss.active;
+  const float e = a.eos[b];                       // loaded with `active`: one round trip
+  const float cv = t < 32 ? a.cur[b * 32 + t] : 0.f;
   __syncthreads();  // every lane has read `active` before lane 0 updates the state
   if (t == 0) {
     FrameFlags f{0, 0};
-    const float e = a.eos[b];
     if (valid) {  // tts_model.rs:1055-1063 + map_while over 0..max_gen_len
       if (e > ss.eos_threshold && ss.eos_step < 0) ss.eos_step = ss.step;
       const bool tail = ss.eos_step >= 0 && ss.step >= ss.eos_step + ss.frames_after_eos;
@@ -2167,9 +2168,8 @@ __global__ __launch_bounds__(64) void k_front_commit(FrontCommitArgs a) {
     a.eos_out[b] = e;
   }
   if (t < 32) {
-    const float v = a.cur[b * 32 + t];
-    a.lat_out[b * 32 + t] = v;
-    if (valid) a.lat_in[b * 32 + t] = v;
+    a.lat_out[b * 32 + t] = cv;
+    if (valid) a.lat_in[b * 32 + t] = cv;
   }
 }
 
