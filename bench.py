@@ -2,18 +2,23 @@
 """Throughput bench of the Pocket TTS generation hot path (BASELINE.json configs[2]).
 
 Workload per GPU: 32 concurrent utterances (batch rows), each a synthetic "10 s" utterance:
-voice prompt [125 x 1024] ~ N(0, 0.11^2), 40 text tokens, generation forced to K frames
+voice prompt [125 x 1024] ~ N(0, 0.11^2), 40 text tokens, generation forced to 125 frames
 (eos_threshold = +inf), temperature 0.7, lsd_decode_steps 1, synthetic weights (seed 0x5EED;
 real checkpoints are gated/offline). One "step" = one batched iteration of the
 generate_stream_segment loop body (tts_model.rs:1006-1070) for all 32 rows: FlowLM step +
-flow head + Mimi decode -> 32 x 1920 PCM samples (32 x 80 ms of audio).
+flow head + Mimi decode -> 32 x 1920 PCM samples (32 x 80 ms of audio), copied to pinned host
+memory inside the step (the graphs end in async D2H copies; fetch() reads host memory).
 
-value = audio seconds produced by all ranks / max-over-ranks wall time of the timed job: admission
-of all B utterances (voice-KV copy + 40-token text prefill per row) followed by exactly K batched
-steps (K = 125 frames = 10 s per utterance by default), with inputs and outputs resident in HBM
-(the PCIe copy of PCM is not in the timed region). The voice state is precomputed (as in
-configs[1]); warmup = one short job of W steps on the same rows.
-Multi-GPU: replicas (independent utterances per GPU, no per-step collective); rank 0 builds the
+The utterance length is fixed at 125 frames whatever --steps says: a timed job is the admission of
+all B utterances (voice-KV copy + 40-token text prefill per row) followed by the 125 batched steps
+that deliver their 10 s of audio. --steps K times ceil(K / 125) such jobs back to back (at least
+one); `steps` in the output is the number of steps actually timed (`steps_requested` = K).
+value = audio seconds produced by all ranks / max-over-ranks wall time of the timed jobs. The voice
+state is precomputed (as in configs[1]); warmup = one short job of W steps on the same rows.
+
+Multi-GPU (--gpus N): replicas (independent utterances per GPU, no per-step collective). Without
+a torch.distributed environment the process re-launches itself as N ranks under
+`torch.distributed.run` (a child process; this parent never touches the GPU); rank 0 builds the
 weights and broadcasts the packed blob over RCCL once at load time.
 """
 
@@ -35,7 +40,7 @@ sys.path.insert(0, str(ROOT / "tests"))
 METRIC = "audio-sec/wall-sec (RTF) per GPU at batch=32 + p50 first-chunk latency"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8 TB/s spec
 F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix/vector peak
-BATCH, PROMPT_FRAMES, TEXT_TOKENS = 32, 125, 40
+BATCH, PROMPT_FRAMES, TEXT_TOKENS, UTT_FRAMES = 32, 125, 40, 125  # 125 frames = 10 s per utterance
 
 
 def measured_traffic(op):
@@ -116,13 +121,86 @@ def text_ids(slot):
     return np.array([(i * 97 + 13 + 7 * slot) % 4000 for i in range(TEXT_TOKENS)], np.int32)
 
 
+class _SelftestEngine:
+    """--launcher-selftest only: a CPU stand-in with the Engine surface bench.py drives, so the
+    multi-rank launch, the gloo collectives and the output line can be checked without a GPU. It
+    computes nothing and the line it yields says so (data: "launcher selftest")."""
+
+    def __init__(self, max_slots, **_):
+        self.n = max_slots
+
+    @staticmethod
+    def weight_blob_bytes():
+        return 4096
+
+    def finalize(self):
+        pass
+
+    def voice_from_prompt(self, prompt):
+        return object()
+
+    def open_many(self, slots, voices, ids, params):
+        self.frames = {s: 0 for s in slots}
+        self.max = {s: p.max_frames for s, p in zip(slots, params)}
+
+    def step_async(self, n):
+        time.sleep(2e-4)
+        for s in self.frames:
+            self.frames[s] += 1
+
+    def sync(self):
+        pass
+
+    def fetch(self, n):
+        import types
+
+        done = np.array([self.frames[s] >= self.max[s] for s in range(n)])
+        return types.SimpleNamespace(valid=done, last=done, pcm=np.zeros((n, 1920), np.float32))
+
+    def close(self):
+        pass
+
+
+def free_port():
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_replicas(n):
+    """--gpus N without a torch.distributed environment: re-run this script as N ranks under
+    torch.distributed.run, as a CHILD process (never exec: the driver forbids replacing a process;
+    this parent has not touched the GPU), and return its exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    return subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode
+
+
+def cpu_baseline_leg(procs):
+    """oracle/cpu_baseline.py in a child process (CPU only): like-for-like configs[2] jobs."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, str(ROOT / "oracle" / "cpu_baseline.py"), "--procs", str(procs)],
+                       capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError("cpu baseline failed: " + r.stderr[-2000:])
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=125)  # 125 frames = one 10 s utterance per row
+    ap.add_argument("--steps", type=int, default=UTT_FRAMES,
+                    help="steps to time: ceil(steps / 125) whole jobs of 125-frame utterances")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=16, help="CPU baseline worker processes (<= CPU share)")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--ops-out", default="", help="write per-op timings of the step plan (JSON)")
     ap.add_argument("--no-op-times", action="store_true", help="skip the per-op HIP-event pass (PMC runs)")
@@ -130,25 +208,47 @@ def main():
                     help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM) and fp8_gemm engines")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sequential stepping (no FlowLM / Mimi overlap across consecutive frames)")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="CPU-only check of the N-rank launch path (gloo, stand-in engine; measures nothing)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_replicas(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
+    selftest = args.launcher_selftest
+    dev = "cpu" if selftest else f"cuda:{local_rank}"
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        if not selftest:
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo" if selftest else "nccl")
 
-    import pocket_tts_amd as pt
+    if selftest:
+        import types
 
-    B, K, W = args.batch, args.steps, args.warmup
+        pt = types.SimpleNamespace(Engine=_SelftestEngine, GenerationParams=__import__("types").SimpleNamespace)
+        args.no_cpu_baseline = args.no_latency = args.no_op_times = args.no_quant_variant = True
+    else:
+        import pocket_tts_amd as pt
+
+    B, W = args.batch, args.warmup
+    K = UTT_FRAMES
+    jobs = max(1, -(-args.steps // K))
     pipeline = not args.no_pipeline
     calls = K + (1 if pipeline else 0)  # overlapped stepping returns each frame one call later
     max_ctx = PROMPT_FRAMES + TEXT_TOKENS + K + 8
+
+    def params(round_id, b, n_frames):
+        return pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), frames_after_eos=3, max_frames=n_frames,
+                                   seed=slot_seed(round_id, rank, b))
 
     # ---- engine (+ one RCCL broadcast of the packed weights at load time)
     if dist is None:
@@ -157,59 +257,66 @@ def main():
     else:
         import torch
 
-        blob = torch.empty(pt.Engine.weight_blob_bytes() // 4, dtype=torch.float32, device=f"cuda:{local_rank}")
+        blob = torch.empty(pt.Engine.weight_blob_bytes() // 4, dtype=torch.float32, device=dev)
         eng = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                         weight_blob=blob.data_ptr(), defer_weights=(rank != 0), pipeline=pipeline)
-        torch.cuda.synchronize()
+        if not selftest:
+            torch.cuda.synchronize()
         broadcast_weights(dist, blob)
-        torch.cuda.synchronize()
+        if not selftest:
+            torch.cuda.synchronize()
         if rank != 0:
             eng.finalize()
 
     def barrier():
         if dist is not None:
-            import torch
+            if not selftest:
+                import torch
 
-            torch.cuda.synchronize()
+                torch.cuda.synchronize()
             dist.barrier()
 
     def timed_job(eng):
-        """Warmup job, then the timed one: admission of all B utterances (voice KV copy + text
-        prefill) and exactly K batched steps, i.e. first prefill to last PCM frame of B
-        utterances of K frames. Returns (elapsed, admission) seconds, max over ranks."""
+        """Warmup job, then the timed ones: per job, admission of all B utterances (voice KV copy +
+        text prefill) and the 125 batched steps of their 10 s of audio, i.e. first prefill to last
+        PCM frame (in pinned host memory) of B utterances. Returns (elapsed, admission) seconds,
+        max over ranks."""
         voice = eng.voice_from_prompt(synth_prompt())  # voice state precomputed (shared by all rows)
 
-        def admit(round_id):  # batched admission (ptts_slots_open): one shared text-prefill pass
+        def admit(round_id, n_frames):  # batched admission (ptts_slots_open): one shared text-prefill pass
             eng.open_many(list(range(B)), [voice] * B, [text_ids(b) for b in range(B)],
-                          [pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), frames_after_eos=3,
-                                               max_frames=K, seed=slot_seed(round_id, rank, b)) for b in range(B)])
+                          [params(round_id, b, n_frames) for b in range(B)])
 
         # warmup: a short job on the same rows (graph capture, caches), then the rows are re-admitted
-        admit(0)
-        for _ in range(W):
+        admit(0, max(1, W))
+        for _ in range(max(1, W) + (1 if pipeline else 0)):
             eng.step_async(B)
         eng.sync()
         barrier()
         eng.sync()
+        admit_s = 0.0
         t0 = time.perf_counter()
-        admit(1)
-        eng.sync()
-        ta = time.perf_counter()
-        for _ in range(calls):
-            eng.step_async(B)
-        eng.sync()
+        for j in range(jobs):
+            ta0 = time.perf_counter()
+            admit(1 + j, K)
+            eng.sync()
+            admit_s += time.perf_counter() - ta0
+            for _ in range(calls):
+                eng.step_async(B)
+            eng.sync()
+            r = eng.fetch(B)  # the last frame of every row, from pinned host memory
+            assert r.valid.all() and r.last.all() and np.isfinite(r.pcm).all(), "bench produced invalid frames"
         t1 = time.perf_counter()
         barrier()
-        elapsed, admit_s = t1 - t0, ta - t0
+        elapsed = t1 - t0
         if dist is not None:
-            elapsed, admit_s = max_over_ranks(dist, [elapsed, admit_s], f"cuda:{local_rank}")
-        r = eng.fetch(B)
-        assert r.valid.all() and r.last.all() and np.isfinite(r.pcm).all(), "bench produced invalid frames"
+            elapsed, admit_s = max_over_ranks(dist, [elapsed, admit_s], dev)
         return elapsed, admit_s
 
     elapsed, admit_s = timed_job(eng)
+    steps = jobs * K
 
-    audio_sec = world * B * K * 1920 / 24000.0
+    audio_sec = world * jobs * B * K * 1920 / 24000.0
     value = audio_sec / elapsed
 
     if rank != 0:
@@ -218,9 +325,9 @@ def main():
         return
 
     # ---- dominant kernel: time every op of the step plan on the engine stream (HIP events)
-    plan = eng.plan(B)
     roof, top, sum_ops_ms = None, None, None
     if not args.no_op_times:
+        plan = eng.plan(B)
         seen, per_op = set(), []
         for name, fl, by in plan:
             if name in seen:
@@ -249,12 +356,14 @@ def main():
         top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
         sum_ops_ms = round(sum(u for u, _, _, _ in per_op) / 1000.0, 3)
         roof["phases"] = phase_rooflines(per_op, plan, B, K)
-    if args.ops_out:
+        if args.ops_out:
+            with open(args.ops_out, "w") as f:
+                json.dump({"n_rows": B, "plan": [n for n, _, _ in plan],
+                           "ops": [{"op": n, "avg_us": u, "flops": fl_, "bytes": by_} for u, n, fl_, by_ in per_op]},
+                          f, indent=1)
+    elif args.ops_out and not selftest:
         with open(args.ops_out, "w") as f:
-            json.dump({"n_rows": B, "plan": [n for n, _, _ in plan],
-                       "ops": [] if args.no_op_times else
-                       [{"op": n, "avg_us": u, "flops": fl_, "bytes": by_} for u, n, fl_, by_ in per_op]},
-                      f, indent=1)
+            json.dump({"n_rows": B, "plan": [n for n, _, _ in eng.plan(B)], "ops": []}, f, indent=1)
 
     # ---- p50 first-chunk latency (config 2): text prefill + 1 step, voice precomputed
     p50 = None
@@ -272,72 +381,64 @@ def main():
         p50 = float(np.median(lat[5:]) * 1000.0)
         e1.close()
 
-    # ---- configs[4] variant: the same job on an engine with the reference's int8 weight
-    # quantization of the FlowLM (quantize.rs); its step GEMMs stream int8 codes. Reported beside
-    # `value`, never as it (different weights from the f32 model).
-    quant = None
+    # ---- configs[4] variants: the same job on an engine with the reference's int8 weight
+    # quantization of the FlowLM (quantize.rs; its step GEMMs stream int8 codes), and with the
+    # large FlowLM step GEMMs as fp8 W8A8 (accuracy-gated against the f32 oracle, tests/test_fp8.py).
+    # Reported beside `value`, never as it (different numerics from the f32 reference).
+    quant = fp8 = None
     eng.close()  # one engine on the GPU at a time
     if not args.no_quant_variant and world == 1:
         eq = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                        pipeline=pipeline, weight_quant=pt.QUANT_FLOW_LM)
         q_el, q_ad = timed_job(eq)
-        quant = {"value": round(B * K * 1920 / 24000.0 / q_el, 2), "unit": "audio-sec/wall-sec",
-                 "ms_per_step": round(1000.0 * q_el / K, 4),
-                 "steady_ms_per_step": round(1000.0 * (q_el - q_ad) / K, 4),
+        quant = {"value": round(jobs * B * K * 1920 / 24000.0 / q_el, 2), "unit": "audio-sec/wall-sec",
+                 "ms_per_step": round(1000.0 * q_el / steps, 4),
+                 "steady_ms_per_step": round(1000.0 * (q_el - q_ad) / steps, 4),
                  "weight_quant": "flow_lm int8 (quantize.rs QuantizeConfig::default, per-tensor symmetric)",
                  "int8_matrices": eq.int8_matrices}
         eq.close()
-    # ---- configs[4] "fp8 MFMA GEMM path": the same job with the large FlowLM step GEMMs as fp8
-    # W8A8 (fp8_gemm); accuracy-gated against the f32 oracle (tests/test_fp8.py), not a reference
-    # numeric. Reported beside `value`, never as it.
-    fp8 = None
-    if not args.no_quant_variant and world == 1:
         ef = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                        pipeline=pipeline, fp8_gemm=True)
         f_el, f_ad = timed_job(ef)
-        fp8 = {"value": round(B * K * 1920 / 24000.0 / f_el, 2), "unit": "audio-sec/wall-sec",
-               "ms_per_step": round(1000.0 * f_el / K, 4),
-               "steady_ms_per_step": round(1000.0 * (f_el - f_ad) / K, 4),
+        fp8 = {"value": round(jobs * B * K * 1920 / 24000.0 / f_el, 2), "unit": "audio-sec/wall-sec",
+               "ms_per_step": round(1000.0 * f_el / steps, 4),
+               "steady_ms_per_step": round(1000.0 * (f_el - f_ad) / steps, 4),
                "gemm": "fp8 e4m3 W8A8 on v_mfma_f32_32x32x16_fp8_fp8 (row-scaled weights, per-slice "
                        "activation scales), FlowLM qkv/linear1/linear2/adaLN",
                "fp8_matrices": ef.fp8_matrices}
         ef.close()
 
-    # ---- CPU baseline: the oracle (C port of the reference algorithm) on the host cores
+    # ---- CPU baseline: the oracle (C restatement of the reference algorithm) on the host cores,
+    # the same 125-frame job per utterance (oracle/cpu_baseline.py, a child process)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        from _oracle import Oracle
-
-        threads = min(16, os.cpu_count() or 1)
-        o = Oracle(0x5EED)
-        n_frames = 4
-        secs = o.bench(B, PROMPT_FRAMES, TEXT_TOKENS, n_frames, threads)
-        cpu = {"value": round(B * n_frames * 0.08 / secs, 3), "unit": "audio-sec/wall-sec", "cores": threads,
-               "kind": "port",
-               "sample": f"{B} utterances x {n_frames} frames after a {PROMPT_FRAMES}+{TEXT_TOKENS} prefill, "
-                         f"fp32 C oracle, one utterance per OpenMP thread"}
+        cpu = cpu_baseline_leg(args.cpu_procs)
 
     out = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "audio-sec/wall-sec",
         "n_gpus": world,
-        "steps": K,
+        "steps": steps,
+        "steps_requested": args.steps,
         "warmup": W,
-        "ms_per_step": round(1000.0 * elapsed / K, 4),
-        "admit_ms": round(1000.0 * admit_s, 3),
-        "steady_ms_per_step": round(1000.0 * (elapsed - admit_s) / K, 4),  # per frame, drain call included
+        "ms_per_step": round(1000.0 * elapsed / steps, 4),
+        "admit_ms": round(1000.0 * admit_s / jobs, 3),
+        "steady_ms_per_step": round(1000.0 * (elapsed - admit_s) / steps, 4),  # per frame, drain call included
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded weights and prompts; real checkpoints are gated offline)",
-        "config": {"workload": "b6369a24 batch=32 concurrent 10 s utterances per GPU, lsd_decode_steps=1 "
+        "data": "launcher selftest (CPU stand-in engine, nothing computed)" if selftest else
+                "synthetic (seeded weights and prompts; real checkpoints are gated offline)",
+        "config": {"workload": f"b6369a24 batch={B} concurrent 10 s utterances per GPU (125 frames, voice prompt "
+                               f"{PROMPT_FRAMES} frames, {TEXT_TOKENS} text tokens), lsd_decode_steps=1 "
                                "(BASELINE configs[2])",
-                   "global_batch": B * world, "utterance_frames": K, "prompt_frames": PROMPT_FRAMES,
+                   "global_batch": B * world, "utterance_frames": K, "jobs": jobs, "prompt_frames": PROMPT_FRAMES,
                    "text_tokens": TEXT_TOKENS, "temp": 0.7, "parallelism": f"replicas x{world}",
                    "stepping": "pipelined (Mimi decode of frame k overlaps FlowLM step k+1)" if pipeline
-                   else "sequential"},
+                   else "sequential",
+                   "pcm_to_host": "every frame, async D2H into pinned memory inside the step graphs"},
         "p50_first_chunk_ms": None if p50 is None else round(p50, 3),
         "int8_flowlm_variant": quant,
         "fp8_flowlm_variant": fp8,

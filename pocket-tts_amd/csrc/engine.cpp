@@ -80,10 +80,13 @@ Engine::Engine(const ptts_engine_config& cfg) {
   cur_ = dalloc((size_t)B * LDIM);
   qprev_ = dalloc((size_t)2 * B * MD);  // [parity][slot][512], see quant_upsample
   eos_ = dalloc(B);
+  static_assert(sizeof(FrameFlags) == 2 * sizeof(float), "FrameFlags packs into two floats");
+  meta_floats_ = (size_t)B * (LDIM + 1 + 2);
   for (int q = 0; q < 2; ++q) {  // front -> back hand-off, one set per step parity
-    lat_out_[q] = dalloc((size_t)B * LDIM);
-    eos_out_[q] = dalloc(B);
-    flags_[q] = (FrameFlags*)dalloc((size_t)2 * B);
+    meta_[q] = dalloc(meta_floats_);
+    lat_out_[q] = meta_[q];                                  // 128-B aligned,
+    flags_[q] = (FrameFlags*)(meta_[q] + (size_t)B * LDIM);  // so FrameFlags stay 8-B aligned
+    eos_out_[q] = meta_[q] + (size_t)B * (LDIM + 2);
     pcm_[q] = dalloc((size_t)B * FRAME);
   }
   // back part's own split-K slabs: Mimi QKV (2 slabs), Mimi ff2 (4), SEANet conv0 (8), convtr0 (4)
@@ -151,10 +154,13 @@ Engine::Engine(const ptts_engine_config& cfg) {
   rope_ = dalloc((size_t)max_ctx_ * 64);
   temb_tmp_ = dalloc((size_t)2 * lsd_ * FD);
 
-  PTTS_HIP(hipHostMalloc((void**)&h_pcm_, sizeof(float) * B * FRAME, hipHostMallocDefault));
-  PTTS_HIP(hipHostMalloc((void**)&h_eos_, sizeof(float) * B, hipHostMallocDefault));
-  PTTS_HIP(hipHostMalloc((void**)&h_lat_, sizeof(float) * B * LDIM, hipHostMallocDefault));
-  PTTS_HIP(hipHostMalloc((void**)&h_fl_, sizeof(FrameFlags) * B, hipHostMallocDefault));
+  for (int q = 0; q < 2; ++q) {
+    PTTS_HIP(hipHostMalloc((void**)&h_pcm_[q], sizeof(float) * B * FRAME, hipHostMallocDefault));
+    PTTS_HIP(hipHostMalloc((void**)&h_meta_[q], sizeof(float) * meta_floats_, hipHostMallocDefault));
+    memset(h_meta_[q], 0, sizeof(float) * meta_floats_);
+  }
+  PTTS_HIP(hipHostMalloc((void**)&h_err_, sizeof(int), hipHostMallocDefault));
+  *h_err_ = 0;
   PTTS_HIP(hipHostMalloc((void**)&h_slots_, sizeof(int) * B, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_st_, sizeof(SlotState) * B, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_fp_, sizeof(int) * B, hipHostMallocDefault));
@@ -167,7 +173,9 @@ Engine::Engine(const ptts_engine_config& cfg) {
     PTTS_HIP(hipEventRecord(ev_front_[q], stream_));
     PTTS_HIP(hipEventRecord(ev_back_[q], stream_));
   }
+  PTTS_HIP(hipEventCreateWithFlags(&ev_admit_, hipEventDisableTiming));
   pipeline_ = cfg.pipeline != 0;
+  head_resident_ = flow_head_max_resident(dev_);
 
   if (!cfg.defer_weights) {
     std::unique_ptr<TensorSource> src = cfg.weights_path && cfg.weights_path[0]
@@ -189,12 +197,14 @@ Engine::~Engine() {
     if (ev_front_[q]) (void)hipEventDestroy(ev_front_[q]);
     if (ev_back_[q]) (void)hipEventDestroy(ev_back_[q]);
   }
+  if (ev_admit_) (void)hipEventDestroy(ev_admit_);
   if (stream_be_) (void)hipStreamDestroy(stream_be_);
   for (void* p : allocs_) (void)hipFree(p);
-  if (h_pcm_) (void)hipHostFree(h_pcm_);
-  if (h_eos_) (void)hipHostFree(h_eos_);
-  if (h_lat_) (void)hipHostFree(h_lat_);
-  if (h_fl_) (void)hipHostFree(h_fl_);
+  for (int q = 0; q < 2; ++q) {
+    if (h_pcm_[q]) (void)hipHostFree(h_pcm_[q]);
+    if (h_meta_[q]) (void)hipHostFree(h_meta_[q]);
+  }
+  if (h_err_) (void)hipHostFree(h_err_);
   for (void* hp : {(void*)h_slots_, (void*)h_st_, (void*)h_fp_, (void*)h_ids_, (void*)h_tab_})
     if (hp) (void)hipHostFree(hp);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -565,6 +575,8 @@ void Engine::prefill_rows(std::vector<Op>& ops, int slot, int T, int p0) {
 // in the packed blob (pack_weights lays the six blocks out identically).
 bool Engine::use_head_chain(int B) const {
   if (!head_chain_ || !flow_head_fits(B)) return false;
+  // every workgroup spins on counters the others bump: all of them must be resident at once
+  if (flow_head_grid(B) > head_resident_) return false;
   const long s = (long)(L_.rb_w0[1] - L_.rb_w0[0]);
   for (int i = 1; i < FDEPTH; ++i)
     if ((long)(L_.rb_lnw[i] - L_.rb_lnw[i - 1]) != s || (long)(L_.rb_lnb[i] - L_.rb_lnb[i - 1]) != s ||
@@ -587,6 +599,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
   flow_layers(ops, B, RowMap{0, 1, 0, fpos_}, 1, true, "flow");
   // ---- flow head (mlp.rs:215-383): cond_embed | out_eos, EOS bookkeeping, noise
   linear_split(ops, "head.cond_eos_gemm", h_, D, B, W(L_.cond_eos_w), NCOND, D, &S);
+  PTTS_REQUIRE(S <= FLOW_COND_MAX_SLABS, "head.flow_cond sums at most 16 split-K slabs");
   {
     const float* P = partial_;
     const float* bias = W(L_.cond_eos_b);
@@ -796,7 +809,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
       a.S = S;
       a.partial = mpartial_;
       PTTS_REQUIRE((size_t)S * MR * MD <= mpcap_, "back split-K slab buffer too small");
-      ops.push_back({p + ".ff2_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * MD * MFF,
+      ops.push_back({p + ".ff2_gemm", [a](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * MD * MFF,
                      4.0 * ((double)MD * MFF + (double)MR * MFF + 2.0 * MR * MD)});
       RowReduceArgs r{};
       r.P = mpartial_;
@@ -934,6 +947,13 @@ hipGraphExec_t Engine::part_graph(int part, int B, int par) {
   PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   try {
     for (const Op& op : ops) op.fn(stream_);
+    if (part == 0) {  // the hand-off timeout word, read by fetch() without a device round trip
+      PTTS_HIP(hipMemcpyAsync(h_err_, herr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    } else {  // the frame of this parity leaves HBM inside the step (fetch() reads host memory)
+      PTTS_HIP(hipMemcpyAsync(h_pcm_[par], pcm_[par], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, stream_));
+      PTTS_HIP(hipMemcpyAsync(h_meta_[par], meta_[par], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
+                              stream_));
+    }
   } catch (...) {
     (void)hipStreamEndCapture(stream_, &g);
     throw;
@@ -971,6 +991,10 @@ void Engine::step_async(int B) {
     PTTS_HIP(hipGraphLaunch(front, stream_));
     PTTS_HIP(hipEventRecord(ev_front_[par], stream_));
     PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[par ^ 1], 0));
+    if (admit_pending_) {  // slot state rewritten since the front part this back part decodes
+      PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
+      admit_pending_ = false;
+    }
     PTTS_HIP(hipGraphLaunch(back, stream_be_));
     PTTS_HIP(hipEventRecord(ev_back_[par ^ 1], stream_be_));
     out_par_ = par ^ 1;
@@ -987,35 +1011,32 @@ void Engine::sync() {
 }
 
 // Outputs of the last call's frame (see step_async); rows past the rows that frame covered
-// report no frame.
+// report no frame. The step's graphs already copied the frame into pinned host memory.
 void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat) {
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
   sync();
   const int q = out_par_;
   const int n = std::min(B, out_rows_);
-  if (n > 0) {
-    if (pcm) PTTS_HIP(hipMemcpy(h_pcm_, pcm_[q], sizeof(float) * n * FRAME, hipMemcpyDeviceToHost));
-    if (eos) PTTS_HIP(hipMemcpy(h_eos_, eos_out_[q], sizeof(float) * n, hipMemcpyDeviceToHost));
-    if (lat) PTTS_HIP(hipMemcpy(h_lat_, lat_out_[q], sizeof(float) * n * LDIM, hipMemcpyDeviceToHost));
-    PTTS_HIP(hipMemcpy(h_fl_, flags_[q], sizeof(FrameFlags) * n, hipMemcpyDeviceToHost));
-  }
-  int herr = 0;  // k_flow_head's bounded hand-off waits: a timeout poisons the frame, fail loudly
-  PTTS_HIP(hipMemcpy(&herr, herr_, sizeof(int), hipMemcpyDeviceToHost));
-  if (herr) {
-    PTTS_HIP(hipMemset(herr_, 0, sizeof(int)));
+  if (*h_err_) {  // k_flow_head's bounded hand-off waits: a timeout poisons the frame, fail loudly
+    *h_err_ = 0;
+    PTTS_HIP(hipMemsetAsync(herr_, 0, sizeof(int), stream_));
+    PTTS_HIP(hipStreamSynchronize(stream_));
     throw Error(PTTS_ERR_HIP, "flow-head persistent launch: an in-launch hand-off wait timed out");
   }
+  const float* hl = h_meta_[q];
+  const FrameFlags* hf = (const FrameFlags*)(h_meta_[q] + (size_t)max_slots_ * LDIM);
+  const float* he = h_meta_[q] + (size_t)max_slots_ * (LDIM + 2);
   for (int b = 0; b < B; ++b) {
-    const bool ok = b < n && h_fl_[b].valid;
+    const bool ok = b < n && hf[b].valid;
     if (valid) valid[b] = ok;
-    if (last) last[b] = ok && h_fl_[b].last;
+    if (last) last[b] = ok && hf[b].last;
     if (pcm) {
-      if (b < n) memcpy(pcm + (size_t)b * FRAME, h_pcm_ + (size_t)b * FRAME, sizeof(float) * FRAME);
+      if (b < n) memcpy(pcm + (size_t)b * FRAME, h_pcm_[q] + (size_t)b * FRAME, sizeof(float) * FRAME);
       else memset(pcm + (size_t)b * FRAME, 0, sizeof(float) * FRAME);
     }
-    if (eos) eos[b] = b < n ? h_eos_[b] : 0.f;
+    if (eos) eos[b] = b < n ? he[b] : 0.f;
     if (lat) {
-      if (b < n) memcpy(lat + (size_t)b * LDIM, h_lat_ + (size_t)b * LDIM, sizeof(float) * LDIM);
+      if (b < n) memcpy(lat + (size_t)b * LDIM, hl + (size_t)b * LDIM, sizeof(float) * LDIM);
       else memset(lat + (size_t)b * LDIM, 0, sizeof(float) * LDIM);
     }
   }
@@ -1485,6 +1506,12 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     flow_layers(ops, T, map, 16, false, "prefill");
     run_ops(ops);
   }
+  mark_admission();
+}
+
+void Engine::mark_admission() {
+  PTTS_HIP(hipEventRecord(ev_admit_, stream_));
+  admit_pending_ = true;
 }
 
 void Engine::slot_close(int slot) {
@@ -1492,14 +1519,20 @@ void Engine::slot_close(int slot) {
   sync();
   SlotState s{};
   s.eos_step = -1;
-  PTTS_HIP(hipMemcpy(st_ + slot, &s, sizeof s, hipMemcpyHostToDevice));
-  for (int q = 0; q < 2; ++q) PTTS_HIP(hipMemset(flags_[q] + slot, 0, sizeof(FrameFlags)));  // drop pending frame
+  memcpy(h_st_, &s, sizeof s);  // pinned staging (free: sync() above)
+  PTTS_HIP(hipMemcpyAsync(st_ + slot, h_st_, sizeof s, hipMemcpyHostToDevice, stream_));
+  for (int q = 0; q < 2; ++q)  // drop a pending frame of the slot
+    PTTS_HIP(hipMemsetAsync(flags_[q] + slot, 0, sizeof(FrameFlags), stream_));
+  mark_admission();
+  PTTS_HIP(hipStreamSynchronize(stream_));
 }
 
 void Engine::set_latent(int slot, const float* lat) {
   PTTS_REQUIRE(slot >= 0 && slot < max_slots_ && lat != nullptr, "bad slot / latent");
   sync();
-  PTTS_HIP(hipMemcpy(lat_in_ + (size_t)slot * LDIM, lat, sizeof(float) * LDIM, hipMemcpyHostToDevice));
+  PTTS_HIP(hipMemcpyAsync(lat_in_ + (size_t)slot * LDIM, lat, sizeof(float) * LDIM, hipMemcpyHostToDevice, stream_));
+  mark_admission();
+  PTTS_HIP(hipStreamSynchronize(stream_));
 }
 
 }  // namespace ptts

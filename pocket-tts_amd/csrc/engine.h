@@ -136,6 +136,8 @@ class Engine {
   float* eos_out_[2] = {};
   FrameFlags* flags_[2] = {};
   float* pcm_[2] = {};
+  float* meta_[2] = {};  // per parity, one allocation: lat_out [B][32] | flags [B] | eos_out [B]
+  size_t meta_floats_ = 0;
   float* mpartial_ = nullptr;
   size_t mpcap_ = 0;
   // in-launch split-K combine (front part only; the back part never uses it)
@@ -149,6 +151,11 @@ class Engine {
   bool pipeline_ = false;
   hipStream_t stream_be_ = nullptr;
   hipEvent_t ev_front_[2] = {}, ev_back_[2] = {};
+  // admission / slot_close / set_latent write slot state on stream_ after the last front part the
+  // next back part decodes: that back part (stream_be_) waits for this event first
+  hipEvent_t ev_admit_ = nullptr;
+  bool admit_pending_ = false;
+  void mark_admission();
   long long k_ = 0;          // steps issued
   int out_par_ = 0;          // parity of the frame the last call produced
   int out_rows_ = 0;         // rows that frame covers
@@ -156,11 +163,12 @@ class Engine {
   float *temb_ = nullptr, *temb_tmp_ = nullptr;
   float* rope_ = nullptr;  // FlowLM RoPE cos/sin table [max_ctx][32][2]
 
-  // pinned host staging
-  float* h_pcm_ = nullptr;
-  float* h_eos_ = nullptr;
-  float* h_lat_ = nullptr;
-  FrameFlags* h_fl_ = nullptr;
+  // pinned host staging: each back graph ends in async D2H copies of its frame (PCM + metadata)
+  // into the host set of its parity, so fetch() only reads host memory
+  float* h_pcm_[2] = {};
+  float* h_meta_[2] = {};
+  int* h_err_ = nullptr;  // copy of herr_ made at the end of every front graph
+  int head_resident_ = 0;  // k_flow_head workgroups that can be co-resident on this device
   int *h_slots_ = nullptr, *h_fp_ = nullptr, *h_ids_ = nullptr, *h_tab_ = nullptr;  // admission staging
   SlotState* h_st_ = nullptr;
 

@@ -164,6 +164,7 @@ struct FrameFlags {
 
 // After the cond_embed|out_eos split-K GEMM: c = sum + b, eos logit -> eos_out,
 // y_s = silu(temb[s] + c) for each lsd step, x0 noise -> cur (reads SlotState only).
+constexpr int FLOW_COND_MAX_SLABS = 16;  // k_flow_cond's unrolled slab loads
 void flow_cond(const float* P, int S, int B, const float* bias, const float* temb, int lsd_steps,
                const SlotState* st, float* ysilu, float* cur, float* eos_out, hipStream_t s);
 
@@ -192,6 +193,8 @@ struct FlowHeadArgs {
   unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr
 };
 bool flow_head_fits(int B);
+int flow_head_grid(int B);             // workgroups of one k_flow_head launch
+int flow_head_max_resident(int dev);   // co-resident k_flow_head workgroups (occupancy x CUs)
 // FlowLM input_linear (32 -> 1024, no bias) + layer-0 norm1: x = lat W^T, h = LN(x) (eps 1e-5).
 void input_ln(const float* lat, const float* Wt, const float* lnw, const float* lnb, float* x, float* h, int M,
               hipStream_t s);

@@ -1838,6 +1838,11 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
   const int row = blockIdx.x, head = blockIdx.y;
   int slot, qp;
   row_slot_pos(mp, row, slot, qp);
+  // a finished row is still stepped (its frame is discarded): once it has filled the cache
+  // (qp == cap) its key/value must not be appended, or position cap would spill into the next
+  // head's (or, for the slot's last head, the next slot's) position 0
+  const bool append = qp < kv.cap;
+  qp = min(qp, kv.cap - 1);
   const int d = nh * 64, ld = 3 * d;
   float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
   float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
@@ -1867,11 +1872,11 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
     const float y0 = x0 * cs - x1 * sn, y1 = x0 * sn + x1 * cs;  // one wave: all reads precede the writes
     s_qkv[part][2 * i] = y0;
     s_qkv[part][2 * i + 1] = y1;
-    if (part == 1) {
+    if (part == 1 && append) {
       kbase[(long)qp * 64 + 2 * i] = y0;
       kbase[(long)qp * 64 + 2 * i + 1] = y1;
     }
-  } else if (tid < 128) {
+  } else if (tid < 128 && append) {
     vbase[(long)qp * 64 + lane] = s_qkv[2][lane];
   }
   __syncthreads();
@@ -2047,6 +2052,7 @@ __global__ __launch_bounds__(256) void k_flow_cond(const float* P, int S, int B,
 
 void flow_cond(const float* P, int S, int B, const float* bias, const float* temb, int lsd_steps,
                const SlotState* st, float* ysilu, float* cur, float* eos_out, hipStream_t s) {
+  if (S < 1 || S > FLOW_COND_MAX_SLABS) throw std::runtime_error("flow_cond: 1..16 split-K slabs");
   hipLaunchKernelGGL(k_flow_cond, dim3(B), dim3(256), 0, s, P, S, B, bias, temb, lsd_steps, st, ysilu, cur, eos_out);
 }
 
@@ -2775,10 +2781,18 @@ void transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) 
 
 bool flow_head_fits(int B) { return B >= 1 && B <= 128; }
 
+int flow_head_grid(int B) { return (B + 15) / 16 * (FH_D / 16); }
+
+int flow_head_max_resident(int dev) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_flow_head, 64 * FH_WAVES, 0) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  return per_cu * cus;
+}
+
 void flow_head(const FlowHeadArgs& a, hipStream_t s) {
   if (!flow_head_fits(a.B)) throw std::runtime_error("flow_head: B out of range");
-  const int RG = (a.B + 15) / 16;
-  hipLaunchKernelGGL(k_flow_head, dim3(RG * (FH_D / 16)), dim3(64 * FH_WAVES), 0, s, a);
+  hipLaunchKernelGGL(k_flow_head, dim3(flow_head_grid(a.B)), dim3(64 * FH_WAVES), 0, s, a);
 }
 
 }  // namespace ptts

@@ -38,6 +38,17 @@ def gpu_engine():
     eng.close()
 
 
+# fp32 parity gates of the GPU tests (both sides compute in fp32; differences are reduction order
+# only). Achieved: latents ~3e-6, PCM ~5e-8 max abs; the golden PCM RMS is 0.035, so PCM_TOL is
+# 6e-5 of the signal (north_star's 1e-4 RMS gate is 50x looser).
+LAT_TOL = 5e-5  # EOS logit and latent, max abs
+PCM_TOL = 2e-6  # PCM, max abs per frame
+
+
+def pcm_err(a):
+    return float(np.abs(np.asarray(a, np.float64)).max())
+
+
 def rms(a):
     a = np.asarray(a, np.float64)
     return float(np.sqrt(np.mean(a * a)))

@@ -234,6 +234,15 @@ def main():
     from safetensors.numpy import save_file
 
     flm, mimi, speaker_proj = build_models(torch)
+    if len(sys.argv) > 1 and sys.argv[1] == "long":  # the bench shape (BASELINE configs[2]) at B = 1
+        # 125-frame "10 s" voice prompt, 40 text tokens, 100 free-running frames at temp 0: the
+        # FlowLM context grows 165 -> 265 (past 256 keys) and the Mimi decoder's 250-key window
+        # slides over 1600 positions (attention.rs:167-264, sdpa.rs:128-171)
+        fx = run_e2e(torch, flm, mimi, F=125, S=40, N=100, lsd_steps=1, tag="e2e_long")
+        del fx["tout"]
+        save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / "e2e_long.safetensors"))
+        print("long fixture written to", HERE)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "voice":  # only the voice-cloning front-end fixtures
         fx = run_encoder_chunked(torch, mimi, speaker_proj, n_frames=5, chunk_frames=2, tag="encc5")
         save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / "encoder_chunked_5f.safetensors"))

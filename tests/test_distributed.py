@@ -72,3 +72,23 @@ def test_replicas_gloo_world2():
         assert same and finite, f"rank {rank}: broadcast blob differs from the packed weights"
         assert times == [2.0, 10.0]  # elementwise max over ranks
         assert n_seeds == 64  # utterance noise streams never collide across ranks
+
+
+def test_bench_gpus_flag_launches_replica_ranks():
+    """`bench.py --gpus 2` outside a torch.distributed environment re-launches itself as 2 ranks
+    under torch.distributed.run (a child process, never exec), each rank runs its replica, rank 0
+    reports the whole job: n_gpus 2, "replicas x2", global batch 2 x 32, 125-frame utterances
+    whatever --steps asks. CPU only: --launcher-selftest swaps in a stand-in engine and gloo."""
+    import json
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--launcher-selftest", "--steps", "20",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # only rank 0 prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "replicas x2"
+    assert out["config"]["global_batch"] == 64 and out["config"]["utterance_frames"] == 125
+    assert out["steps"] == 125 and out["steps_requested"] == 20 and out["scaling"] == "weak"

@@ -1,14 +1,14 @@
 """GPU parity: the HIP engine through the C ABI against the reference's golden vectors
 (tests/golden, produced by the reference's own Python modules) and the C oracle.
 
-Tolerances (north_star: latents/codes at temperature 0, PCM within 1e-4 RMS):
-  eos logit and latent  <= 1e-4 max abs
-  PCM                   <= 1e-4 RMS of the difference, 1e-3 max abs
+Tolerances (conftest.py; north_star asks for PCM within 1e-4 RMS, these are far tighter):
+  eos logit and latent  <= LAT_TOL = 5e-5 max abs
+  PCM                   <= PCM_TOL = 2e-6 max abs per frame
 All arithmetic is fp32 on both sides; differences are reduction order only."""
 
 import numpy as np
 import pytest
-from conftest import load_golden, rms
+from conftest import LAT_TOL, PCM_TOL, load_golden, pcm_err, rms
 
 pytestmark = pytest.mark.gpu
 
@@ -25,10 +25,10 @@ def params(**kw):
 
 def check_step(r, row, d, i):
     assert r.valid[row]
-    assert abs(r.eos_logits[row] - d["eos_logit"][i]) <= 1e-4, (i, r.eos_logits[row], d["eos_logit"][i])
-    np.testing.assert_allclose(r.latents[row], d["latent"][i], atol=1e-4)
+    assert abs(r.eos_logits[row] - d["eos_logit"][i]) <= LAT_TOL, (i, r.eos_logits[row], d["eos_logit"][i])
+    np.testing.assert_allclose(r.latents[row], d["latent"][i], atol=LAT_TOL)
     diff = r.pcm[row] - d["pcm"][i]
-    assert rms(diff) <= 1e-4 and np.abs(diff).max() <= 1e-3, (i, rms(diff), np.abs(diff).max())
+    assert pcm_err(diff) <= PCM_TOL, (i, rms(diff), pcm_err(diff))
 
 
 def test_e2e_matches_reference_golden(gpu_engine):
@@ -91,9 +91,9 @@ def test_ragged_batch_matches_oracle(gpu_engine, oracle):
             o = orc[b].step(lat[b])
             lat[b] = o["latent"]
             assert r.valid[b]
-            assert abs(r.eos_logits[b] - o["eos_logit"]) <= 1e-4
-            np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
-            assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+            assert abs(r.eos_logits[b] - o["eos_logit"]) <= LAT_TOL
+            np.testing.assert_allclose(r.latents[b], o["latent"], atol=LAT_TOL)
+            assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL
 
 
 def test_batched_admission_matches_oracle(gpu_engine, oracle):
@@ -125,9 +125,9 @@ def test_batched_admission_matches_oracle(gpu_engine, oracle):
             o = orc[b].step(lat[b])
             lat[b] = o["latent"]
             assert r.valid[b]
-            assert abs(r.eos_logits[b] - o["eos_logit"]) <= 1e-4
-            np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
-            assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+            assert abs(r.eos_logits[b] - o["eos_logit"]) <= LAT_TOL
+            np.testing.assert_allclose(r.latents[b], o["latent"], atol=LAT_TOL)
+            assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL
 
 
 def test_eos_termination_rule(gpu_engine):
@@ -201,8 +201,8 @@ def test_temperature_sampling_matches_oracle(gpu_engine, oracle, clamp):
         r = gpu_engine.step(1)
         o = s.step(lat, noise=_noise(seed, i, temp, clamp))
         lat = o["latent"]
-        np.testing.assert_allclose(r.latents[0], o["latent"], atol=1e-4)
-        assert rms(r.pcm[0] - o["pcm"]) <= 1e-4
+        np.testing.assert_allclose(r.latents[0], o["latent"], atol=LAT_TOL)
+        assert pcm_err(r.pcm[0] - o["pcm"]) <= PCM_TOL
 
 
 def test_steps_are_deterministic_and_slots_reset(gpu_engine):
@@ -213,7 +213,7 @@ def test_steps_are_deterministic_and_slots_reset(gpu_engine):
         gpu_engine.open(3, v, d["text_ids"], params(max_frames=3))
         runs.append(np.stack([gpu_engine.step(4).pcm[3] for _ in range(3)]))
     assert np.array_equal(runs[0], runs[1])
-    np.testing.assert_allclose(runs[0], d["pcm"][:3], atol=1e-3)
+    np.testing.assert_allclose(runs[0], d["pcm"][:3], atol=PCM_TOL)
 
 
 def test_generate_convenience(gpu_engine):
@@ -222,7 +222,7 @@ def test_generate_convenience(gpu_engine):
     pcm = gpu_engine.generate(0, v, d["text_ids"], params(eos_threshold=-4.0, frames_after_eos=2, max_frames=12))
     # EOS fires at step 0 (every golden logit > -4), so frames 0..2 are produced
     assert pcm.size == 3 * 1920
-    assert rms(pcm - d["pcm"][:3].reshape(-1)) <= 1e-4
+    assert pcm_err(pcm - d["pcm"][:3].reshape(-1)) <= PCM_TOL
 
 
 def test_plan_and_kernel_timer(gpu_engine):
@@ -265,9 +265,9 @@ def test_pipelined_stepping_matches_oracle(oracle):
                 o = orc[b].step(lat[b])
                 lat[b] = o["latent"]
                 got[b] += 1
-                assert abs(r.eos_logits[b] - o["eos_logit"]) <= 1e-4
-                np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
-                assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+                assert abs(r.eos_logits[b] - o["eos_logit"]) <= LAT_TOL
+                np.testing.assert_allclose(r.latents[b], o["latent"], atol=LAT_TOL)
+                assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL
 
         admit([0, 1], 4)
         r = eng.step(4)
@@ -305,10 +305,10 @@ def test_long_utterance_wraps_mimi_ring(gpu_engine, oracle):
         o = s.step(lat)
         lat = o["latent"]
         assert r.valid[0] and r.last[0] == (i == n - 1)
-        np.testing.assert_allclose(r.latents[0], o["latent"], atol=1e-4)
-        worst = max(worst, rms(r.pcm[0] - o["pcm"]))
+        np.testing.assert_allclose(r.latents[0], o["latent"], atol=LAT_TOL)
+        worst = max(worst, pcm_err(r.pcm[0] - o["pcm"]))
         gpu_engine.set_latent(0, o["latent"])  # teacher forcing: no drift over 70 AR steps
-    assert worst <= 1e-4, worst
+    assert worst <= PCM_TOL, worst
 
 
 def test_batch_scheduler_matches_oracle(oracle):
@@ -342,7 +342,7 @@ def test_batch_scheduler_matches_oracle(oracle):
             for f in frames:
                 o = s.step(lat)
                 lat = o["latent"]
-                assert rms(f - o["pcm"]) <= 1e-4
+                assert pcm_err(f - o["pcm"]) <= PCM_TOL
     finally:
         sch.close()
         eng.close()
@@ -378,8 +378,8 @@ def test_flow_head_chain_two_row_groups(oracle, lsd):
                 o = orc[b].step(lat[b], lsd_steps=lsd)
                 lat[b] = o["latent"]
                 assert r.valid[b]
-                np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
-                assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+                np.testing.assert_allclose(r.latents[b], o["latent"], atol=LAT_TOL)
+                assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL
     finally:
         eng.close()
 
@@ -415,7 +415,7 @@ def test_large_batch_uses_multi_launch_head(oracle):
             for b in probe:
                 o = orc[b].step(lat[b])
                 lat[b] = o["latent"]
-                np.testing.assert_allclose(r.latents[b], o["latent"], atol=1e-4)
-                assert rms(r.pcm[b] - o["pcm"]) <= 1e-4
+                np.testing.assert_allclose(r.latents[b], o["latent"], atol=LAT_TOL)
+                assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL
     finally:
         eng.close()

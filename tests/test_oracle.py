@@ -75,3 +75,25 @@ def test_oracle_streaming_state_is_per_utterance(oracle):
     rb2 = b.step(ra["latent"] + 0.5)
     ra2 = a.step(ra["latent"])
     assert not np.allclose(ra2["pcm"], rb2["pcm"])
+
+
+def test_oracle_long_context_matches_reference(oracle):
+    """The bench shape at B = 1 (BASELINE configs[2]): a 125-frame voice prompt, 40 text tokens and
+    100 free-running frames at temperature 0 (golden `e2e_long`, made by the reference's own Python
+    modules). The FlowLM context grows 165 -> 265 positions, past 256 keys, and the Mimi decoder's
+    250-key window slides over 1,600 positions of its ring (attention.rs:167-264, sdpa.rs:128-171).
+    Measured: latents 3.5e-6, EOS logits 2e-6, PCM 5e-8 max abs after 100 frames."""
+    d = load_golden("e2e_long.safetensors")
+    assert d["prompt"].shape == (125, 1024) and d["text_ids"].size == 40 and d["latent"].shape[0] == 100
+    s = oracle.new_state(320)
+    s.prefill(d["prompt"])
+    s.prefill_tokens(d["text_ids"])
+    lat = None
+    for i in range(d["latent"].shape[0]):
+        r = s.step(lat, intermediates=i < 3)
+        lat = r["latent"]
+        assert abs(r["eos_logit"] - d["eos_logit"][i]) < 2e-5, i
+        np.testing.assert_allclose(lat, d["latent"][i], atol=2e-5)
+        np.testing.assert_allclose(r["pcm"], d["pcm"][i], atol=1e-6)
+        if i < 3:
+            np.testing.assert_allclose(r["after_tr"].T, d["after_decoder_transformer"][i], atol=2e-5)

@@ -16,7 +16,7 @@ from pathlib import Path
 
 import numpy as np
 import pytest
-from conftest import load_golden
+from conftest import LAT_TOL, load_golden
 
 REF_ASSETS = Path("/root/reference/assets")
 RATES = (48000, 44100, 16000, 22050, 8000)
@@ -218,7 +218,7 @@ def test_gpu_wav_voice_path_matches_oracle(gpu_engine, oracle, tmp_path):
     s.prefill_tokens(ids)
     r = gpu_engine.step(1)
     ref = s.step(None)
-    np.testing.assert_allclose(r.latents[0], ref["latent"], atol=1e-4)
+    np.testing.assert_allclose(r.latents[0], ref["latent"], atol=LAT_TOL)
     gpu_engine.close_slot(0)
     v.close()
 

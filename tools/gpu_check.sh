@@ -12,7 +12,7 @@ fatal() { # exit codes that mean the GPU or process died: stop everything
   case $1 in 124|134|137|139) return 0 ;; *) return 1 ;; esac
 }
 
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rfP --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
 echo "pytest-gpu rc=$rc"; tail -n 30 "$OUT/pytest_gpu.log"
 if fatal $rc; then exit $rc; fi
