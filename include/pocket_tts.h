@@ -93,6 +93,11 @@ size_t ptts_weight_blob_bytes(void);
  * (cfg.weight_blob + defer_weights) and calls ptts_engine_finalize(). Replaces the per-process
  * VarBuilder load of TTSModel::load_with_params_device (tts_model.rs:86-106). */
 int ptts_pack_weights(uint64_t synth_seed, const char* weights_path, float* host_out, size_t n_bytes);
+/* The checkpoint tensors the packer reads, one line each: "name\tdim0,dim1,...\n" (TTSModel
+ * state-dict keys: flow_lm.* and mimi.*, the VarBuilder prefixes of tts_model.rs:279-426, with the
+ * checkpoint's own shapes). A weights file needs exactly these (extra tensors, e.g. the dropped
+ * VQ codebooks, are ignored; F32, BF16 or F16). *needed = bytes incl. the terminating 0. Host only. */
+int ptts_weight_manifest(char* buf, size_t cap, size_t* needed);
 /* Same with the reference's weight quantization applied (weight_quant = PTTS_QUANT_*;
  * quantize.rs:126-150 quantize_weights with QuantizeConfig::default()). */
 int ptts_pack_weights_ex(uint64_t synth_seed, const char* weights_path, int weight_quant, float* host_out,

@@ -58,6 +58,39 @@ int ptts_pack_weights_ex(uint64_t synth_seed, const char* weights_path, int weig
   });
 }
 
+namespace {
+// Records the (name, shape) of every tensor pack_weights() reads; returns zeros.
+class ManifestSource : public ptts::TensorSource {
+ public:
+  std::string text;
+  std::vector<float> get(const std::string& name, const std::vector<int64_t>& shape) override {
+    int64_t n = 1;
+    text += name + "\t";
+    for (size_t i = 0; i < shape.size(); ++i) {
+      text += (i ? "," : "") + std::to_string(shape[i]);
+      n *= shape[i];
+    }
+    text += "\n";
+    return std::vector<float>((size_t)n, 0.f);
+  }
+};
+}  // namespace
+
+int ptts_weight_manifest(char* buf, size_t cap, size_t* needed) {
+  return guard([&] {
+    ManifestSource ms;
+    std::vector<float> scratch(ptts::pack_weights(nullptr, nullptr).total, 0.f);
+    ptts::pack_weights(&ms, scratch.data());
+    if (needed) *needed = ms.text.size() + 1;
+    if (buf && cap) {
+      const size_t n = std::min(cap - 1, ms.text.size());
+      std::memcpy(buf, ms.text.data(), n);
+      buf[n] = 0;
+      if (n < ms.text.size()) throw ptts::Error(PTTS_ERR_INVALID, "manifest buffer too small");
+    }
+  });
+}
+
 int ptts_quantize_tensor(const float* x, size_t n, int num_levels, float* out, float* scale) {
   return guard([&] {
     if ((!x || !out) && n) throw ptts::Error(PTTS_ERR_INVALID, "null tensor");

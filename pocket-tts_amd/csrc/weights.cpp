@@ -137,7 +137,9 @@ class SafetensorsSource : public TensorSource {
     int64_t n = 1, ne = 1;
     for (auto d : shape) n *= d;
     for (auto d : e.shape) ne *= d;
-    if (n != ne) throw Error(PTTS_ERR_IO, "shape mismatch for " + name);
+    if (n != ne || e.shape != shape) throw Error(PTTS_ERR_IO, "shape mismatch for " + name);
+    if (e.end - e.begin != (size_t)n * (e.dtype == "F32" ? 4 : 2) || data_ + e.end > map_ + size_)
+      throw Error(PTTS_ERR_IO, "data_offsets out of range for " + name);
     std::vector<float> out((size_t)n);
     const uint8_t* p = data_ + e.begin;
     if (e.dtype == "F32") {

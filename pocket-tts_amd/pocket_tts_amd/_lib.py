@@ -55,6 +55,7 @@ SIGNATURES = [
     ("ptts_weight_blob_bytes", C.c_size_t, []),
     ("ptts_pack_weights", C.c_int, [C.c_uint64, C.c_char_p, F32P, C.c_size_t]),
     ("ptts_pack_weights_ex", C.c_int, [C.c_uint64, C.c_char_p, C.c_int, F32P, C.c_size_t]),
+    ("ptts_weight_manifest", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("ptts_quantize_tensor", C.c_int, [F32P, C.c_size_t, C.c_int, F32P, F32P]),
     ("ptts_quant_applies", C.c_int, [C.c_char_p, C.c_size_t, C.c_int]),
     ("ptts_engine_int8_matrices", C.c_int, [C.c_void_p]),

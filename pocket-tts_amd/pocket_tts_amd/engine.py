@@ -99,6 +99,19 @@ class Engine:
                                          out.ctypes.data_as(F32P), out.nbytes))
         return out
 
+    @staticmethod
+    def weight_manifest() -> list[tuple[str, tuple[int, ...]]]:
+        """(checkpoint tensor name, shape) of every tensor the weight packer reads (host only)."""
+        need = C.c_size_t(0)
+        check(lib().ptts_weight_manifest(None, 0, C.byref(need)))
+        buf = C.create_string_buffer(need.value)
+        check(lib().ptts_weight_manifest(buf, need.value, None))
+        out = []
+        for line in buf.value.decode().splitlines():
+            name, dims = line.split("\t")
+            out.append((name, tuple(int(x) for x in dims.split(",")) if dims else ()))
+        return out
+
     @property
     def fp8_matrices(self) -> int:
         """FlowLM GEMM weight matrices on the fp8 W8A8 path (0 unless fp8_gemm)."""

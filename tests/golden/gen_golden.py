@@ -234,6 +234,16 @@ def main():
     from safetensors.numpy import save_file
 
     flm, mimi, speaker_proj = build_models(torch)
+    if len(sys.argv) > 1 and sys.argv[1] == "names":  # the checkpoint's tensor names and shapes
+        import json
+
+        sd = {**{"flow_lm." + k: list(v.shape) for k, v in flm.state_dict().items()},
+              **{"mimi." + k: list(v.shape) for k, v in mimi.state_dict().items()},
+              "flow_lm.speaker_proj_weight": [1024, 512]}
+        with open(HERE / "checkpoint_names.json", "w") as f:
+            json.dump(sd, f, indent=0, sort_keys=True)
+        print(len(sd), "names written to", HERE / "checkpoint_names.json")
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "long":  # the bench shape (BASELINE configs[2]) at B = 1
         # 125-frame "10 s" voice prompt, 40 text tokens, 100 free-running frames at temp 0: the
         # FlowLM context grows 165 -> 265 (past 256 keys) and the Mimi decoder's 250-key window
