@@ -208,6 +208,9 @@ def main():
                     help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM) and fp8_gemm engines")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sequential stepping (no FlowLM / Mimi overlap across consecutive frames)")
+    ap.add_argument("--profile-frames", type=int, default=0,
+                    help="profiling runs only (rocprofv3 PMC passes): utterances of this many frames instead of "
+                         "125; the line then says so and is not the configs[2] measurement")
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU-only check of the N-rank launch path (gloo, stand-in engine; measures nothing)")
     args = ap.parse_args()
@@ -240,8 +243,8 @@ def main():
         import pocket_tts_amd as pt
 
     B, W = args.batch, args.warmup
-    K = UTT_FRAMES
-    jobs = max(1, -(-args.steps // K))
+    K = args.profile_frames if args.profile_frames > 0 else UTT_FRAMES
+    jobs = max(1, -(-args.steps // K)) if args.profile_frames <= 0 else 1
     pipeline = not args.no_pipeline
     calls = K + (1 if pipeline else 0)  # overlapped stepping returns each frame one call later
     max_ctx = PROMPT_FRAMES + TEXT_TOKENS + K + 8
@@ -430,6 +433,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "launcher selftest (CPU stand-in engine, nothing computed)" if selftest else
+                f"PROFILING RUN ({K}-frame utterances, not configs[2])" if args.profile_frames > 0 else
                 "synthetic (seeded weights and prompts; real checkpoints are gated offline)",
         "config": {"workload": f"b6369a24 batch={B} concurrent 10 s utterances per GPU (125 frames, voice prompt "
                                f"{PROMPT_FRAMES} frames, {TEXT_TOKENS} text tokens), lsd_decode_steps=1 "

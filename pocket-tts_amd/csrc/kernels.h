@@ -69,6 +69,9 @@ struct GemmArgs {
   // * wscale[n]; the A rows are quantized to e4m3 in-kernel with one scale per (row, K slice)
   // and the tile runs on v_mfma_f32_32x32x16_fp8_fp8. Replaces W when non-null.
   const uint8_t* Wf8;
+  // XCD placement of the tile grid (set by gemm(); speed only): the 8 XCDs split the N tiles
+  // into xcd_pn parts and the M tiles into 8 / xcd_pn parts; 0 = contiguous runs of tiles
+  int xcd_pn;
   // split-K
   int S;
   float* partial;  // [S][M][N] when S > 1

@@ -152,14 +152,25 @@ __device__ __forceinline__ void gemm_store_tile(const GemmArgs& a, const floatx1
   gemm_store_fast<16>(a, v, 0, tm0, tn0, h, r);
 }
 
-// XCD-aware tile order. Workgroups are dealt round-robin to the 8 XCDs by linear id, so
-// consecutive ids land on different L2s and the N-tiles that share one A row block would each
-// miss in their own L2. Id L -> tile (L % 8) * (T / 8) + L / 8 gives every XCD a contiguous run
-// of tiles (x fastest), so those N-tiles meet in one L2. Identity when T % 8 != 0 or when the
-// in-launch split-K combine keys its tickets on blockIdx.
-__device__ __forceinline__ void xcd_tile(bool on, int& bx, int& by) {
-  const int gx = gridDim.x, T = gx * gridDim.y;
+// XCD-aware tile order (speed only; any placement is correct). Workgroups are dealt round-robin
+// to the 8 XCDs by linear id (MI355X_MICROARCH.md §Workgroup dispatch), so XCD x runs ids
+// x, x + 8, ... Each XCD is given one block of the tile grid: the N tiles split into xcd_pn
+// parts, the M tiles into 8 / xcd_pn, so an XCD reads 1/xcd_pn of the weights and
+// xcd_pn/8 of the A rows, each once through its L2 (gemm() picks xcd_pn to minimise
+// (8/pn) * |W| + pn * |A|: weight-heavy Mimi GEMMs and SEANet convs share weight tiles, the
+// activation-heavy late SEANet stages share A row blocks). xcd_pn = 0, or a grid that does not
+// split evenly: contiguous runs of T/8 tiles per XCD (x fastest); identity when T % 8 != 0 or
+// when the in-launch split-K combine keys its tickets on blockIdx.
+__device__ __forceinline__ void xcd_tile(const GemmArgs& a, bool on, int& bx, int& by) {
+  const int gx = gridDim.x, gy = gridDim.y, T = gx * gy;
   const int L = blockIdx.x + blockIdx.y * gx;
+  const int pn = a.xcd_pn;
+  if (on && (T & 7) == 0 && pn > 0) {
+    const int pm = 8 / pn, xcd = L & 7, j = L >> 3, tnx = gx / pn;
+    bx = (xcd % pn) * tnx + j % tnx;
+    by = (xcd / pn) * (gy / pm) + j / tnx;
+    return;
+  }
   const int t = (on && (T & 7) == 0) ? (L & 7) * (T >> 3) + (L >> 3) : L;
   bx = t % gx;
   by = t / gx;
@@ -187,7 +198,7 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
   constexpr int WM = Lay<LAYOUT>::WM, WN = Lay<LAYOUT>::WN;
   const int wm = KS ? 0 : wave / WN, wn = KS ? 0 : wave % WN;
   int bx, by;
-  xcd_tile(!a.fuse, bx, by);
+  xcd_tile(a, !a.fuse, bx, by);
   const int n0 = (bx * WN + wn) * 32, m0 = (by * WM + wm) * 32, z = blockIdx.z;
   const int nchunks = a.K >> 5;
   int cb = 0, ce = nchunks, phase = 0;
@@ -545,7 +556,7 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int r = lane & 31, h = lane >> 5;
   int bx, by;
-  xcd_tile(!a.fuse, bx, by);
+  xcd_tile(a, !a.fuse, bx, by);
   const int n0 = bx * TN, m0 = by * TM, z = blockIdx.z;
   const int nchunks = a.K / BK;
   int cb = 0, ce = nchunks, phase = 0;
@@ -714,7 +725,7 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
   int bx, by;
-  xcd_tile(true, bx, by);
+  xcd_tile(a, true, bx, by);
   const int n0 = bx * 32 * TN, m0 = by * 32 * TM, z = blockIdx.z;
   const int nchunks = a.K >> 5;
   int cb = 0, ce = nchunks, phase = 0;
@@ -1113,14 +1124,36 @@ void fp8_codes(const float* W, int N, int K, uint8_t* q, float* s, hipStream_t s
   hipLaunchKernelGGL(k_fp8_codes, dim3((unsigned)N), dim3(256), 0, st, W, K, q, s);
 }
 
+// xcd_pn of a tile grid gx x gy (see xcd_tile): the split of the 8 XCDs over N and M tiles that
+// moves the fewest operand bytes through the L2s, (8/pn) * |W| + pn * |A|; 0 when none divides.
+static int choose_xcd_pn(const GemmArgs& a, int gx, int gy) {
+  if (((long)gx * gy) % 8) return 0;
+  const double wb = (double)a.N * a.K;
+  const double ab = a.mode == 0 ? (double)a.M * a.K : (double)(a.M / a.Tq) * a.T_in * a.cin;
+  int best = 0;
+  double bc = 0;
+  for (int pn : {8, 4, 2, 1}) {
+    const int pm = 8 / pn;
+    if (gx % pn || gy % pm) continue;
+    const double c = pm * wb + pn * ab;
+    if (!best || c < bc) best = pn, bc = c;
+  }
+  return best;
+}
+template <typename K>
+static void launch_tiled(K kernel, dim3 grid, int threads, hipStream_t s, const GemmArgs& a) {
+  GemmArgs b = a;
+  b.xcd_pn = choose_xcd_pn(a, (int)grid.x, (int)grid.y);
+  hipLaunchKernelGGL(kernel, grid, dim3(threads), 0, s, b);
+}
+
 template <int MODE>
 static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
   switch (a.layout) {
 #define PTTS_GLDS(L, WM_, WN_, BK_, NB_)                                                               \
   case L:                                                                                               \
-    hipLaunchKernelGGL((k_gemm_glds<MODE, WM_, WN_, BK_, NB_>),                                         \
-                       dim3((a.N + 32 * WN_ - 1) / (32 * WN_), (a.M + 32 * WM_ - 1) / (32 * WM_), grid_z), \
-                       dim3(256), 0, s, a);                                                            \
+    launch_tiled((k_gemm_glds<MODE, WM_, WN_, BK_, NB_>),                                              \
+                 dim3((a.N + 32 * WN_ - 1) / (32 * WN_), (a.M + 32 * WM_ - 1) / (32 * WM_), grid_z), 256, s, a); \
     return;
     PTTS_GLDS(6, 2, 2, 32, 2)
     PTTS_GLDS(7, 1, 4, 32, 2)
@@ -1134,10 +1167,9 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
 #undef PTTS_GLDS
 #define PTTS_GLRB(L, WM_, WN_, NB_, TMW_, TNW_)                                                       \
   case L:                                                                                             \
-    hipLaunchKernelGGL((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_>),                             \
-                       dim3((a.N + 32 * WN_ * TNW_ - 1) / (32 * WN_ * TNW_),                          \
-                            (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z),                  \
-                       dim3(256), 0, s, a);                                                          \
+    launch_tiled((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_>),                                   \
+                 dim3((a.N + 32 * WN_ * TNW_ - 1) / (32 * WN_ * TNW_),                                \
+                      (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z), 256, s, a);            \
     return;
     // register-blocked LDS-DMA tiles (per-wave TMW x TNW accumulators)
     PTTS_GLRB(21, 2, 2, 3, 2, 2)  // 128 x 128
@@ -1161,34 +1193,34 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
                          a);
       break;
     case 1:
-      hipLaunchKernelGGL((k_gemm<MODE, 1>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), dim3(256), 0, s, a);
+      launch_tiled((k_gemm<MODE, 1>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), 256, s, a);
       break;
     case 2:
-      hipLaunchKernelGGL((k_gemm<MODE, 2>), dim3((a.N + 127) / 128, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+      launch_tiled((k_gemm<MODE, 2>), dim3((a.N + 127) / 128, (a.M + 31) / 32, grid_z), 256, s, a);
       break;
     case 3:
-      hipLaunchKernelGGL((k_gemm<MODE, 3>), dim3((a.N + 31) / 32, (a.M + 127) / 128, grid_z), dim3(256), 0, s, a);
+      launch_tiled((k_gemm<MODE, 3>), dim3((a.N + 31) / 32, (a.M + 127) / 128, grid_z), 256, s, a);
       break;
     case 9:
-      hipLaunchKernelGGL((k_gemm<MODE, 9>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(512), 0, s, a);
+      launch_tiled((k_gemm<MODE, 9>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 512, s, a);
       break;
     case 18:
-      hipLaunchKernelGGL((k_gemm_rb<MODE, 1, 2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+      launch_tiled((k_gemm_rb<MODE, 1, 2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), 256, s, a);
       break;
     case 19:
-      hipLaunchKernelGGL((k_gemm_rb<MODE, 2, 1>), dim3((a.N + 31) / 32, (a.M + 63) / 64, grid_z), dim3(256), 0, s, a);
+      launch_tiled((k_gemm_rb<MODE, 2, 1>), dim3((a.N + 31) / 32, (a.M + 63) / 64, grid_z), 256, s, a);
       break;
     case 20:
-      hipLaunchKernelGGL((k_gemm_rb<MODE, 2, 2>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), dim3(256), 0, s, a);
+      launch_tiled((k_gemm_rb<MODE, 2, 2>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), 256, s, a);
       break;
     case 10:
-      hipLaunchKernelGGL((k_gemm<MODE, 10>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+      launch_tiled((k_gemm<MODE, 10>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 256, s, a);
       break;
     case 17:
-      hipLaunchKernelGGL((k_gemm<MODE, 17>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(512), 0, s, a);
+      launch_tiled((k_gemm<MODE, 17>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 512, s, a);
       break;
     default:
-      hipLaunchKernelGGL((k_gemm<MODE, 0>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s, a);
+      launch_tiled((k_gemm<MODE, 0>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 256, s, a);
   }
 }
 

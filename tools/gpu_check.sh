@@ -37,7 +37,7 @@ fi
 
 if [ "${PROFILE:-1}" = "1" ]; then
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-      -- python "$ROOT/bench.py" --steps 30 --warmup 5 --no-cpu-baseline --no-latency --no-pipeline --no-quant-variant \
+      -- python "$ROOT/bench.py" --profile-frames 30 --warmup 5 --no-cpu-baseline --no-latency --no-pipeline --no-quant-variant \
       --ops-out "$OUT/prof_ops.json" > "$OUT/prof.log" 2>&1)
   rc=$?
   echo "rocprof rc=$rc"; tail -n 2 "$OUT/prof.log"
@@ -48,7 +48,7 @@ fi
 if [ "${PMC:-0}" = "1" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -d "$OUT/pmc_$C" -o run --output-format csv \
-        -- python "$ROOT/bench.py" --steps 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-pipeline --no-quant-variant \
+        -- python "$ROOT/bench.py" --profile-frames 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-pipeline --no-quant-variant \
         > "$OUT/pmc_$C.log" 2>&1)
     rc=$?
     echo "pmc $C rc=$rc"; tail -n 2 "$OUT/pmc_$C.log"
@@ -60,7 +60,7 @@ if [ "${PMC:-0}" = "1" ]; then
   # MFMA utilisation: one pass with both counters (1 SQ_ + 1 GRBM_ counter: within one pass's limits)
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmc_mfma" \
       -o run --output-format csv \
-      -- python "$ROOT/bench.py" --steps 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-pipeline --no-quant-variant \
+      -- python "$ROOT/bench.py" --profile-frames 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-pipeline --no-quant-variant \
       > "$OUT/pmc_mfma.log" 2>&1)
   rc=$?
   echo "pmc mfma rc=$rc"; tail -n 2 "$OUT/pmc_mfma.log"

@@ -21,6 +21,12 @@ import json
 import sys
 
 
+def is_engine(name):
+    """Engine kernels live in namespace ptts; the runtime's copy kernels of the graphs' D2H nodes
+    (frame to pinned host memory) are not ops of the plan."""
+    return "ptts::" in name
+
+
 def step_windows(names, n):
     windows = [i + 1 - n for i, nm in enumerate(names) if "k_commit" in nm and i + 1 >= n]
     seqs = collections.Counter(tuple(names[w:w + n]) for w in windows)
@@ -34,7 +40,7 @@ def cmd_trace(trace_path, ops_path, out_path):
     ops = json.load(open(ops_path))
     plan = ops["plan"]
     event_us = {o["op"]: o for o in ops["ops"]}
-    rows = list(csv.DictReader(open(trace_path)))
+    rows = [r for r in csv.DictReader(open(trace_path)) if is_engine(r["Kernel_Name"])]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     n = len(plan)
     ref_seq, steps = step_windows([r["Kernel_Name"] for r in rows], n)
@@ -68,7 +74,7 @@ def cmd_counters(cc_path, ops_path, counter, out_path):
     plan = json.load(open(ops_path))["plan"]
     disp = {}
     for r in csv.DictReader(open(cc_path)):
-        if r["Counter_Name"] != counter:
+        if r["Counter_Name"] != counter or not is_engine(r["Kernel_Name"]):
             continue
         d = disp.setdefault(int(r["Dispatch_Id"]), [r["Kernel_Name"], 0.0])
         d[1] += float(r["Counter_Value"])
