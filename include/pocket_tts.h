@@ -184,6 +184,14 @@ int ptts_fetch(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uin
                float* eos_logits, float* latents);
 /* Test hook (teacher forcing): overwrite the backbone input latent of `slot`. */
 int ptts_slot_set_latent(ptts_engine* e, int slot, const float* latent32);
+/* MimiModel::decode_from_latent (mimi.rs:143-157) after the denorm + DummyQuantizer of
+ * tts_model.rs:1033-1038 (the kernel-level seam of SURVEY §8(b)): n_frames FlowLM latents
+ * [n][32] decoded in sequence on `slot`'s streaming state, which is reset first; every pending
+ * frame of the engine is dropped (call on an idle engine). Outputs (each optional, NULL = skip):
+ * pcm [n][1920]; quantized [n][512]; after_upsample and after_transformer [n][16][512]
+ * (time-major; the reference's tensors are [1][512][16]). */
+int ptts_decode_latents(ptts_engine* e, int slot, const float* latents, int n_frames, float* pcm, float* quantized,
+                        float* after_upsample, float* after_transformer);
 
 /* TTSModel::generate for one segment (tts_model.rs:687-703) on row `slot`: loops ptts_step
  * until the row's last frame. pcm_out receives up to max_samples samples. */

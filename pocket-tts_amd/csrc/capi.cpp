@@ -214,6 +214,11 @@ int ptts_probe_overlap(ptts_engine* e, int n_rows, int reps, double* us8) {
 
 int ptts_slot_close(ptts_engine* e, int slot) { return guard([&] { eng(e).slot_close(slot); }); }
 
+int ptts_decode_latents(ptts_engine* e, int slot, const float* latents, int n_frames, float* pcm, float* quantized,
+                        float* after_upsample, float* after_transformer) {
+  return guard([&] { eng(e).decode_latents(slot, latents, n_frames, pcm, quantized, after_upsample, after_transformer); });
+}
+
 int ptts_slot_set_latent(ptts_engine* e, int slot, const float* latent32) {
   return guard([&] { eng(e).set_latent(slot, latent32); });
 }

@@ -1514,6 +1514,84 @@ void Engine::mark_admission() {
   admit_pending_ = true;
 }
 
+// MimiModel::decode_from_latent (mimi.rs:143-157) with the denorm + quantize of tts_model.rs:
+// 1033-1038 in front, on `slot`'s own streaming state, for n frames in sequence: the back part
+// of the step plan run eagerly for rows [0, slot], only `slot` marked as carrying a frame.
+// Every pending frame of the engine is dropped and the slot is reset first (use on an idle
+// engine, as the reference's test_decoder_parity builds its own state). Optional outputs per
+// frame: quant [512] (the 32 -> 512 quantizer output), up [16][512] (after the upsample
+// convtr), tr [16][512] (after the decoder transformer), time-major.
+void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float* quant, float* up, float* tr) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
+  PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
+  PTTS_REQUIRE(lat != nullptr && n >= 1, "no latents");
+  sync();
+  for (int q = 0; q < 2; ++q) PTTS_HIP(hipMemsetAsync(flags_[q], 0, sizeof(FrameFlags) * max_slots_, stream_));
+  {
+    SlotState s{};
+    s.eos_step = -1;
+    *h_slots_ = slot;
+    *h_st_ = s;
+    *h_fp_ = 0;
+    PTTS_HIP(hipMemcpyAsync(admit_slots_, h_slots_, sizeof(int), hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(admit_st_, h_st_, sizeof(SlotState), hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(admit_fpos_, h_fp_, sizeof(int), hipMemcpyHostToDevice, stream_));
+    ResetArgs r{};
+    for (int i = 0; i < 8; ++i) {
+      r.buf[i] = hist_[i];
+      r.per_slot[i] = (long)hist_P_[i] * hist_C_[i];
+    }
+    r.buf[8] = qprev_;
+    r.per_slot[8] = MD;
+    r.buf[9] = qprev_ + (size_t)max_slots_ * MD;
+    r.per_slot[9] = MD;
+    r.nb = 10;
+    r.slots = admit_slots_;
+    r.n = 1;
+    r.lat_in = lat_in_;
+    r.bos = W(L_.bos);
+    r.st_src = admit_st_;
+    r.fpos_src = admit_fpos_;
+    r.st = st_;
+    r.fpos = fpos_;
+    r.mpos = mpos_;
+    r.flags0 = flags_[0];
+    r.flags1 = flags_[1];
+    slot_reset(r, stream_);
+    PTTS_HIP(hipGetLastError());
+  }
+  const FrameFlags on{1, 0}, off{0, 0};
+  auto rows16 = [&](float* dst, const float* src) {  // the slot's 16 Mimi rows [16][512]
+    PTTS_HIP(hipMemcpyAsync(dst, src + (size_t)slot * UP * MD, sizeof(float) * UP * MD, hipMemcpyDeviceToHost,
+                            stream_));
+  };
+  for (int i = 0; i < n; ++i) {
+    const int par = i & 1;  // quant_upsample reads the previous frame's quantizer output from par ^ 1
+    PTTS_HIP(hipMemcpyAsync(lat_out_[par] + (size_t)slot * LDIM, lat + (size_t)i * LDIM, sizeof(float) * LDIM,
+                            hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(flags_[par] + slot, &on, sizeof on, hipMemcpyHostToDevice, stream_));
+    std::vector<Op> ops;
+    build_back(ops, slot + 1, par);
+    size_t j = 0;
+    for (; j < ops.size(); ++j) {
+      if (ops[j].name == "seanet.conv0" && tr) rows16(tr + (size_t)i * UP * MD, mx_);
+      ops[j].fn(stream_);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) throw Error(PTTS_ERR_HIP, "launch of " + ops[j].name + " failed: " + hipGetErrorString(e));
+      if (j == 0 && up) rows16(up + (size_t)i * UP * MD, mx_);
+    }
+    if (pcm)
+      PTTS_HIP(hipMemcpyAsync(pcm + (size_t)i * FRAME, pcm_[par] + (size_t)slot * FRAME, sizeof(float) * FRAME,
+                              hipMemcpyDeviceToHost, stream_));
+    if (quant)
+      PTTS_HIP(hipMemcpyAsync(quant + (size_t)i * MD, qprev_ + ((size_t)par * max_slots_ + slot) * MD,
+                              sizeof(float) * MD, hipMemcpyDeviceToHost, stream_));
+    PTTS_HIP(hipMemcpyAsync(flags_[par] + slot, &off, sizeof off, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipStreamSynchronize(stream_));
+  }
+  mark_admission();
+}
+
 void Engine::slot_close(int slot) {
   PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
   sync();

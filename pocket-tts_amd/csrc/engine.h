@@ -48,6 +48,7 @@ class Engine {
                   const ptts_gen_params* params);
   void slot_close(int slot);
   void set_latent(int slot, const float* lat);
+  void decode_latents(int slot, const float* lat, int n, float* pcm, float* quant, float* up, float* tr);
 
   void step_async(int B);
   void sync();

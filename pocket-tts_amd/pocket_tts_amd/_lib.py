@@ -83,6 +83,7 @@ SIGNATURES = [
     ("ptts_sync", C.c_int, [C.c_void_p]),
     ("ptts_fetch", C.c_int, [C.c_void_p, C.c_int, F32P, U8P, U8P, F32P, F32P]),
     ("ptts_slot_set_latent", C.c_int, [C.c_void_p, C.c_int, F32P]),
+    ("ptts_decode_latents", C.c_int, [C.c_void_p, C.c_int, F32P, C.c_int, F32P, F32P, F32P, F32P]),
     ("ptts_generate", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, I32P, C.c_int, C.POINTER(GenParams), F32P, C.c_int,
                                 C.POINTER(C.c_int)]),
     ("ptts_time_kernel", C.c_int, [C.c_void_p, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_double)]),

@@ -200,6 +200,18 @@ class Engine:
         v = np.ascontiguousarray(latent, np.float32).reshape(LDIM)
         check(lib().ptts_slot_set_latent(self.handle, slot, fptr(v)))
 
+    def decode_latents(self, slot: int, latents: np.ndarray) -> dict:
+        """MimiModel::decode_from_latent of n FlowLM latents [n, 32] on a reset slot (idle engine):
+        pcm [n, 1920], quantized [n, 512], after_upsample / after_transformer [n, 16, 512]."""
+        lat = np.ascontiguousarray(latents, np.float32).reshape(-1, LDIM)
+        n = lat.shape[0]
+        out = {"pcm": np.zeros((n, FRAME), np.float32), "quantized": np.zeros((n, 512), np.float32),
+               "after_upsample": np.zeros((n, 16, 512), np.float32),
+               "after_transformer": np.zeros((n, 16, 512), np.float32)}
+        check(lib().ptts_decode_latents(self.handle, slot, fptr(lat), n, fptr(out["pcm"]), fptr(out["quantized"]),
+                                        fptr(out["after_upsample"]), fptr(out["after_transformer"])))
+        return out
+
     # -- the batched hot path
     def step(self, n_rows: int) -> StepResult:
         r = StepResult(np.zeros((n_rows, FRAME), np.float32), np.zeros(n_rows, np.uint8), np.zeros(n_rows, np.uint8),

@@ -234,6 +234,24 @@ def main():
     from safetensors.numpy import save_file
 
     flm, mimi, speaker_proj = build_models(torch)
+    if len(sys.argv) > 1 and sys.argv[1] == "refdata":  # the reference's own real-data fixtures, as data
+        import shutil
+        import wave
+
+        from safetensors.numpy import load_file
+
+        with wave.open(str(REF.parent / "assets" / "ref.wav"), "rb") as w:
+            assert (w.getnchannels(), w.getsampwidth(), w.getframerate()) == (1, 2, 48000)
+            raw = np.frombuffer(w.readframes(w.getnframes()), np.int16)
+        mi = load_file(str(REF.parent / "assets" / "ref_mimi_input.safetensors"))["mimi_input"].reshape(-1)
+        save_file({"refwav_i16": np.ascontiguousarray(raw), "ref_mimi_input": np.ascontiguousarray(mi, np.float32)},
+                  str(HERE / "ref_voice.safetensors"))
+        # real-weight intermediates of the reference's test_decoder_parity / voice conditioning
+        # (meaningful only with the gated checkpoint; the weights-gated GPU tests use them)
+        for f in ("ref_decoder_intermediates.safetensors", "ref_voice_conditioning.safetensors"):
+            shutil.copyfile(REF.parent / "assets" / f, HERE / f)
+        print("reference data fixtures written to", HERE)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "names":  # the checkpoint's tensor names and shapes
         import json
 

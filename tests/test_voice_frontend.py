@@ -231,3 +231,17 @@ def test_gpu_voice_errors(gpu_engine):
         gpu_engine.voice_from_audio(np.zeros(100, np.float32), 0)
     with pytest.raises(PocketTTSError):
         gpu_engine.voice_from_audio(np.zeros(1920 * 600, np.float32), 24000)  # > max_ctx frames
+
+
+def test_oracle_resample_matches_whole_reference_pair():
+    """The whole assets/ref.wav -> assets/ref_mimi_input pair (tests/golden/ref_voice.safetensors):
+    the oracle's resample_poly restatement equals the reference's convert_audio output, which the
+    reference zero-pads to whole frames (87 x 1920)."""
+    from _oracle import resample
+
+    g = load_golden("ref_voice.safetensors")
+    x = g["refwav_i16"].astype(np.float32) / np.float32(32768.0)
+    y = resample(x, 48000)
+    mi = g["ref_mimi_input"]
+    assert x.size == 331708 and y.size == 165854 and mi.size == 87 * 1920
+    assert np.abs(y - mi[:y.size]).max() <= 1e-6 and not mi[y.size:].any()
