@@ -13,7 +13,9 @@ The reference server serializes every generation behind one mutex
 
 Works with both stepping modes of the engine (with `pipeline=True` a row's frames arrive one
 step after they are computed). `MultiGpuScheduler` spreads requests over one scheduler per GPU
-(replicas, no inter-GPU traffic: DESIGN.md §6).
+(replicas, no inter-GPU traffic: DESIGN.md §6) inside one process; `main(--gpus N)` instead runs
+one worker process per GPU, each a whole server on one shared SO_REUSEPORT port (the weights
+packed once and broadcast over RCCL at load time).
 
 HTTP (`create_app`, FastAPI; routes of pocket-tts-cli/src/server/routes.rs:20-30):
   GET  /health             {"status": "healthy", "version": ...}
@@ -377,37 +379,146 @@ def create_app(service: TTSService):
         except ValueError as e:
             raise HTTPException(status_code=400, detail=str(e)) from e
 
+    worker = getattr(service, "worker", None) or {"rank": 0, "world": 1, "pid": os.getpid()}
+    hdr = {"X-PTTS-Rank": str(worker["rank"])}
+
     @app.get("/health")
     def health():
-        return JSONResponse({"status": "healthy", "version": VERSION})
+        return JSONResponse({"status": "healthy", "version": VERSION, "worker": worker}, headers=hdr)
 
     @app.post("/generate")
     def generate(req: GenerateRequest):
         r = submit(**req.model_dump())
-        return Response(wav_bytes(r.audio()), media_type="audio/wav")
+        return Response(wav_bytes(r.audio()), media_type="audio/wav", headers=hdr)
 
     @app.post("/stream")
     async def stream(req: GenerateRequest):
         r = submit(**req.model_dump())
-        return StreamingResponse(pcm_chunks(r), media_type="audio/pcm")
+        return StreamingResponse(pcm_chunks(r), media_type="audio/pcm", headers=hdr)
 
     @app.post("/v1/audio/speech")
     def openai_speech(req: OpenAIRequest):
         r = submit(text=req.input, token_ids=req.token_ids, voice=req.voice)
         audio = r.audio()
         if (req.response_format or "wav") == "pcm":
-            return Response(pcm_i16_le_bytes(audio), media_type="audio/pcm")
-        return Response(wav_bytes(audio), media_type="audio/wav")
+            return Response(pcm_i16_le_bytes(audio), media_type="audio/pcm", headers=hdr)
+        return Response(wav_bytes(audio), media_type="audio/wav", headers=hdr)
 
     return app
 
 
+class StandInEngine:
+    """--stand-in-engine only (CPU; launcher and routing self-test of the multi-process server): the
+    engine surface the scheduler drives, computing nothing. Row frames of utterance u (its first
+    token id) at step k hold u * 1000 + k, delivered one call late as by a pipelined engine."""
+
+    def __init__(self, max_slots=32, max_ctx=1024, **_):
+        self.max_slots, self.max_ctx, self.pipeline = max_slots, max_ctx, True
+        self.rows, self.pending = {}, None
+
+    @staticmethod
+    def weight_blob_bytes():
+        return 4096
+
+    def finalize(self):
+        pass
+
+    def voice_from_prompt(self, prompt):
+        from types import SimpleNamespace
+
+        return SimpleNamespace(n_frames=int(np.asarray(prompt).shape[0]))
+
+    def open_many(self, slots, voices, ids_list, params_list):
+        for s, ids, p in zip(slots, ids_list, params_list):
+            self.rows[s] = [int(ids[0]) if len(ids) else 0, 0, p.max_frames]
+            if self.pending is not None:
+                self.pending[1][s] = False
+
+    def step_async(self, n):
+        pcm, valid, last = np.zeros((n, FRAME), np.float32), np.zeros(n, bool), np.zeros(n, bool)
+        for s, st in list(self.rows.items()):
+            if s < n:
+                pcm[s], valid[s] = st[0] * 1000 + st[1], True
+                st[1] += 1
+                last[s] = st[1] == st[2]
+                if last[s]:
+                    del self.rows[s]
+        prev, self.pending = self.pending, (pcm, valid, last)
+        self.out = (np.zeros((n, FRAME), np.float32), np.zeros(n, bool), np.zeros(n, bool))
+        if prev is not None:  # the previous call's frame, over this call's rows
+            m = min(n, prev[1].size)
+            for a, b in zip(self.out, prev):
+                a[:m] = b[:m]
+
+    def sync(self):
+        pass
+
+    def fetch(self, n):
+        from types import SimpleNamespace
+
+        return SimpleNamespace(pcm=self.out[0], valid=self.out[1], last=self.out[2])
+
+    def close(self):
+        pass
+
+
+def _listen_socket(host: str, port: int):
+    """A listening TCP socket with SO_REUSEPORT: every per-GPU worker process binds the same port
+    and the kernel spreads incoming connections over them (no proxy process in the data path)."""
+    import socket
+
+    so = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    so.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    so.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    so.bind((host, port))
+    so.listen(1024)
+    return so
+
+
+def _worker_engine(args, Engine):
+    """This process's engine. Under torch.distributed (one rank per GPU): rank 0 packs the weights
+    (checkpoint or synthetic) into its engine-owned blob, ONE broadcast over RCCL (xGMI) copies it
+    to every rank at load time, the other ranks finalize from it (no per-step
+    collective). Returns (engine, rank, world, blob checksum)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    kw = dict(max_slots=args.slots, max_ctx=args.max_ctx, weights_path=args.weights, pipeline=True)
+    if world == 1:
+        return Engine(device=local, **kw), 0, 1, None
+    import torch
+    import torch.distributed as dist
+
+    stand_in = Engine is StandInEngine
+    if not stand_in:
+        torch.cuda.set_device(local)
+    dist.init_process_group("gloo" if stand_in else "nccl")
+    dev = "cpu" if stand_in else f"cuda:{local}"
+    blob = torch.empty(Engine.weight_blob_bytes() // 4, dtype=torch.float32, device=dev)
+    if stand_in and rank == 0:
+        blob.copy_(torch.arange(blob.numel(), dtype=torch.float32))
+    eng = Engine(device=local, weight_blob=blob.data_ptr(), defer_weights=rank != 0, **kw)
+    if not stand_in:
+        torch.cuda.synchronize()
+    dist.broadcast(blob, src=0)
+    if not stand_in:
+        torch.cuda.synchronize()
+    if rank != 0:
+        eng.finalize()
+    checksum = float(blob[:1024].double().sum().item())
+    dist.barrier()
+    return eng, rank, world, checksum
+
+
 def main(argv=None):
     """python -m pocket_tts_amd.serve --voice NAME=prompt.npy [--voice ...] [--tokenizer t.json]
-    [--gpus N] [--slots 32] [--port 8000]"""
-    import argparse
+    [--gpus N] [--slots 32] [--port 8000]
 
-    from .engine import Engine
+    --gpus N > 1: one worker PROCESS per GPU (launched as N ranks of torch.distributed.run, a
+    child process; this parent never touches the GPU), each with its own engine, scheduler and
+    HTTP server on the same SO_REUSEPORT port: no shared GIL, no proxy hop; the weights are packed
+    once and broadcast over RCCL at load time."""
+    import argparse
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--voice", action="append", default=[], help="NAME=path (.npy prompt [F,1024] or .wav)")
@@ -418,37 +529,53 @@ def main(argv=None):
     ap.add_argument("--max-ctx", type=int, default=1024)
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--stand-in-engine", action="store_true",
+                    help="CPU self-test of the launcher and routing: a stand-in engine that computes nothing")
     args = ap.parse_args(argv)
+    import sys
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import socket
+        import subprocess
+
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            mport = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={mport}", "-m", "pocket_tts_amd.serve",
+               *(argv if argv is not None else sys.argv[1:])]
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   PYTHONPATH=os.pathsep.join([os.path.dirname(os.path.dirname(__file__)),
+                                               os.environ.get("PYTHONPATH", "")]))
+        sys.exit(subprocess.run(cmd, env=env).returncode)
     # the scheduler thread drops the GIL in every engine call; with the default 5 ms switch
     # interval it can wait that long to get it back from the HTTP threads (one engine step is
     # < 1 ms), so hand the GIL over sooner
-    import sys
-
     sys.setswitchinterval(2e-4)
-    engines = [Engine(device=d, max_slots=args.slots, max_ctx=args.max_ctx, weights_path=args.weights, pipeline=True)
-               for d in range(args.gpus)]
-    voices: dict[str, list[Voice]] = {}
+    if args.stand_in_engine:
+        Engine = StandInEngine
+    else:
+        from .engine import Engine
+    engine, rank, world, checksum = _worker_engine(args, Engine)
+    voices: dict[str, Voice] = {}
     for spec in args.voice or []:
         name, path = spec.split("=", 1)
         if path.endswith(".npy"):
-            prompt = np.load(path, allow_pickle=False).astype(np.float32)
-            voices[name] = [e.voice_from_prompt(prompt) for e in engines]
+            voices[name] = engine.voice_from_prompt(np.load(path, allow_pickle=False).astype(np.float32))
         else:
             from .tts_model import read_wav_mono
 
-            x = read_wav_mono(path)
-            voices[name] = [e.voice_from_pcm(x) for e in engines]
+            voices[name] = engine.voice_from_pcm(read_wav_mono(path))
     if not voices:
         raise SystemExit("at least one --voice NAME=path is required")
-    scheds = [BatchScheduler(e) for e in engines]
-    sched = scheds[0] if len(scheds) == 1 else MultiGpuScheduler(scheds)
-    if len(scheds) == 1:
-        voices = {k: v[0] for k, v in voices.items()}
-    service = TTSService(sched, voices, default_voice=next(iter(voices)),
+    service = TTSService(BatchScheduler(engine), voices, default_voice=next(iter(voices)),
                          tokenizer=load_tokenizer(args.tokenizer) if args.tokenizer else None)
+    service.worker = {"rank": rank, "world": world, "pid": os.getpid(), "weights_checksum": checksum}
     import uvicorn
 
-    uvicorn.run(create_app(service), host=args.host, port=args.port)
+    app = create_app(service)
+    so = _listen_socket(args.host, args.port)
+    uvicorn.Server(uvicorn.Config(app, log_level="warning")).run(sockets=[so])
 
 
 if __name__ == "__main__":

@@ -159,3 +159,61 @@ def test_stream_batches_coalesces_backlog():
     rest = list(it)
     assert len(rest) == 1 and rest[0].shape == (1920,) and int(rest[0][0]) == 3
 
+
+
+def test_multiprocess_server_one_worker_per_gpu(tmp_path):
+    """`serve --gpus 2` (CPU self-test: stand-in engines, gloo): the parent launches 2 worker
+    processes as torch.distributed ranks (a child process, never exec); rank 0's weight blob
+    reaches rank 1 through the load-time broadcast; both workers serve the SAME port
+    (SO_REUSEPORT, the kernel spreads connections, no proxy hop) and answer /generate with their
+    own engine's frames."""
+    import os
+    import signal
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    import httpx
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    np.save(tmp_path / "v.npy", np.zeros((4, 1024), np.float32))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=os.path.join(root, "pocket-tts_amd"))
+    p = subprocess.Popen([sys.executable, "-m", "pocket_tts_amd.serve", "--gpus", "2", "--stand-in-engine",
+                          "--port", str(port), "--slots", "4", "--voice", f"v={tmp_path / 'v.npy'}"],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        base = f"http://127.0.0.1:{port}"
+        deadline = time.time() + 120
+        while True:
+            try:
+                if httpx.get(base + "/health", timeout=2).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                pass
+            assert p.poll() is None and time.time() < deadline, p.stdout.read().decode()[-3000:]
+            time.sleep(0.5)
+        seen, sums = set(), set()
+        for i in range(40):
+            with httpx.Client(timeout=30) as c:  # a fresh connection each time
+                h = c.get(base + "/health").json()["worker"]
+                seen.add(h["rank"])
+                sums.add(h["weights_checksum"])
+                r = c.post(base + "/generate", json={"token_ids": [7, 1, 2], "eos_threshold": 1e9})
+                assert r.status_code == 200 and r.headers["x-ptts-rank"] in ("0", "1")
+                pcm = np.frombuffer(r.content[44:], "<i2")
+                assert pcm.size == (1 + 2) * 13 * 1920  # max_gen_len for 3 ids, stand-in frames
+            if seen == {0, 1} and i >= 8:
+                break
+        assert seen == {0, 1}, seen
+        assert sums == {float(sum(range(1024)))}  # rank 1 holds rank 0's broadcast blob
+    finally:
+        os.killpg(p.pid, signal.SIGTERM)
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
