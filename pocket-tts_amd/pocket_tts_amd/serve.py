@@ -265,18 +265,22 @@ class TTSService:
 
     def request(self, text: str | None = None, token_ids=None, voice: str | None = None,
                 temperature: float | None = None, eos_threshold: float | None = None,
-                noise_clamp: float | None = None, lsd_steps: int | None = None) -> Request:
+                noise_clamp: float | None = None, lsd_steps: int | None = None, words: int | None = None,
+                max_frames: int | None = None) -> Request:
         if lsd_steps is not None and lsd_steps != self.lsd_decode_steps:
             raise ValueError(f"lsd_steps is fixed at engine creation ({self.lsd_decode_steps})")
-        if token_ids is not None:
+        if token_ids is not None:  # extension: ids carry no word count, the client states it
             ids = np.asarray(token_ids, np.int32).reshape(-1)
-            mgl, fae = (max(1, ids.size // 2) + 2) * 13, 3
+            if words is None and max_frames is None:
+                raise ValueError("token_ids need `words` (word count of their text) or `max_frames`")
+            mgl = max_frames or (words + 2) * 13
+            fae = 3 if words is None else (5 if words <= 4 else 3)
         elif text is not None:
             if self.tokenizer is None:
                 raise ValueError("no tokenizer configured: send token_ids")
             prepared = prepare_text_prompt(text)
             ids = np.asarray(self.tokenizer(prepared), np.int32)
-            mgl, fae = max_gen_len(prepared), estimate_frames_after_eos(text)
+            mgl, fae = max_frames or max_gen_len(prepared), estimate_frames_after_eos(text)
         else:
             raise ValueError("text or token_ids required")
         name = voice or self.default_voice
@@ -300,6 +304,8 @@ class GenerateRequest(BaseModel):
 
     text: str | None = None
     token_ids: list[int] | None = None
+    words: int | None = None  # with token_ids: word count of their text (max_gen_len rule)
+    max_frames: int | None = None
     voice: str | None = None
     temperature: float | None = None
     lsd_steps: int | None = None
@@ -315,6 +321,7 @@ class OpenAIRequest(BaseModel):
     voice: str | None = None
     response_format: str | None = None
     token_ids: list[int] | None = None
+    words: int | None = None
 
 
 CHUNK_INTERVAL_S = 0.005  # /stream: at most one chunk per stream per 5 ms after the first
@@ -398,7 +405,7 @@ def create_app(service: TTSService):
 
     @app.post("/v1/audio/speech")
     def openai_speech(req: OpenAIRequest):
-        r = submit(text=req.input, token_ids=req.token_ids, voice=req.voice)
+        r = submit(text=req.input, token_ids=req.token_ids, voice=req.voice, words=req.words)
         audio = r.audio()
         if (req.response_format or "wav") == "pcm":
             return Response(pcm_i16_le_bytes(audio), media_type="audio/pcm", headers=hdr)

@@ -175,12 +175,19 @@ class TTSModel:
             if r.last[0]:
                 return
 
-    def generate_stream(self, text_or_ids, voice_state: Voice, max_frames: int | None = None) -> Iterator[np.ndarray]:
+    def generate_stream(self, text_or_ids, voice_state: Voice, max_frames: int | None = None,
+                        words: int | None = None) -> Iterator[np.ndarray]:
         """tts_model.rs:894-913. Text: one segment per sentence chunk; max_gen_len and the EOS tail
-        from each chunk (:968-969). Token ids: one segment (max_frames or a length estimate)."""
+        from each chunk (:968-969). Token ids (an extension for callers with their own tokenizer):
+        one segment; ids carry no word count, so the caller passes `words` (the reference's rules
+        then apply: max_gen_len = (words + 2) * 13, tail 5 frames up to 4 words else 3) or an
+        explicit max_frames (tail 3)."""
         if not isinstance(text_or_ids, str):
             ids = np.asarray(text_or_ids, np.int32).reshape(-1)
-            yield from self._segment(ids, voice_state, max_frames or (max(1, ids.size // 2) + 2) * 13, 3)
+            if words is None and max_frames is None:
+                raise ValueError("token ids carry no word count: pass words= or max_frames=")
+            fae = 3 if words is None else (5 if words <= 4 else 3)
+            yield from self._segment(ids, voice_state, max_frames or (words + 2) * 13, fae)
             return
         tok = self._tok()
         for chunk in self.split_into_best_sentences(text_or_ids):
@@ -189,9 +196,10 @@ class TTSModel:
             yield from self._segment(ids, voice_state, max_frames or max_gen_len(prepared),
                                      estimate_frames_after_eos(chunk))
 
-    def generate(self, text_or_ids, voice_state: Voice, max_frames: int | None = None) -> np.ndarray:
+    def generate(self, text_or_ids, voice_state: Voice, max_frames: int | None = None,
+                 words: int | None = None) -> np.ndarray:
         """tts_model.rs:687-703: all frames concatenated, [1, N*1920]."""
-        frames = list(self.generate_stream(text_or_ids, voice_state, max_frames))
+        frames = list(self.generate_stream(text_or_ids, voice_state, max_frames, words))
         if not frames:
             raise RuntimeError("No audio generated")
         return np.concatenate(frames, axis=2)[0]

@@ -101,7 +101,7 @@ def test_context_filled_to_max_ctx(oracle):
 def test_http_stream_route_on_real_engine(oracle):
     """The HTTP surface over the real pipelined engine (FastAPI TestClient, in process): two
     /stream requests at temperature 0 with token ids return 16-bit PCM equal to each request's
-    oracle run (to 1 LSB), with max_gen_len frames (tts_model.rs:968-969 rule: 4 ids -> 52)."""
+    oracle run (to 1 LSB), with max_gen_len frames (tts_model.rs:968-969 rule for the stated 2 words: (2 + 2) * 13 = 52)."""
     import pocket_tts_amd as pt
     from fastapi.testclient import TestClient
     from pocket_tts_amd.serve import BatchScheduler, TTSService, create_app
@@ -114,7 +114,7 @@ def test_http_stream_route_on_real_engine(oracle):
         svc = TTSService(sch, {"v": eng.voice_from_prompt(prompt)}, default_voice="v", temp=0.0)
         client = TestClient(create_app(svc))
         for ids in ([260, 2994, 262, 578], [17, 4, 3999, 1200]):
-            r = client.post("/stream", json={"token_ids": ids, "temperature": 0.0, "eos_threshold": 1e9})
+            r = client.post("/stream", json={"token_ids": ids, "words": 2, "temperature": 0.0, "eos_threshold": 1e9})
             assert r.status_code == 200
             got = np.frombuffer(r.content, "<i2")
             assert got.size == 52 * 1920

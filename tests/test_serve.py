@@ -128,7 +128,7 @@ def test_http_routes():
     try:
         c = TestClient(create_app(svc))
         assert c.get("/health").json()["status"] == "healthy"
-        r = c.post("/generate", json={"token_ids": [3, 1, 2, 2]})  # max_gen_len (4//2+2)*13 = 52 frames
+        r = c.post("/generate", json={"token_ids": [3, 1, 2, 2], "words": 2})  # max_gen_len (2+2)*13 = 52 frames
         assert r.status_code == 200 and r.headers["content-type"] == "audio/wav"
         w = wave.open(io.BytesIO(r.content), "rb")
         assert w.getnframes() == 52 * 1920
@@ -137,8 +137,8 @@ def test_http_routes():
         r = c.post("/v1/audio/speech", json={"model": "pocket-tts", "input": "Hi there friend.",
                                              "response_format": "pcm"})
         assert r.status_code == 200 and len(r.content) % 3840 == 0
-        assert c.post("/generate", json={"token_ids": [1], "voice": "nope"}).status_code == 400
-        assert c.post("/generate", json={"token_ids": [1], "lsd_steps": 4}).status_code == 400
+        assert c.post("/generate", json={"token_ids": [1], "words": 1, "voice": "nope"}).status_code == 400
+        assert c.post("/generate", json={"token_ids": [1], "words": 1, "lsd_steps": 4}).status_code == 400
         assert c.post("/generate", json={}).status_code == 400
     finally:
         sch.close()
@@ -202,7 +202,7 @@ def test_multiprocess_server_one_worker_per_gpu(tmp_path):
                 h = c.get(base + "/health").json()["worker"]
                 seen.add(h["rank"])
                 sums.add(h["weights_checksum"])
-                r = c.post(base + "/generate", json={"token_ids": [7, 1, 2], "eos_threshold": 1e9})
+                r = c.post(base + "/generate", json={"token_ids": [7, 1, 2], "words": 1, "eos_threshold": 1e9})
                 assert r.status_code == 200 and r.headers["x-ptts-rank"] in ("0", "1")
                 pcm = np.frombuffer(r.content[44:], "<i2")
                 assert pcm.size == (1 + 2) * 13 * 1920  # max_gen_len for 3 ids, stand-in frames
@@ -217,3 +217,21 @@ def test_multiprocess_server_one_worker_per_gpu(tmp_path):
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, signal.SIGKILL)
             p.wait()
+
+
+def test_token_ids_need_a_word_count():
+    """Token ids carry no word count, so the reference's max_gen_len rule ((words + 2) * 13,
+    tts_model.rs:968) needs the client's `words` (or an explicit max_frames); neither -> 400."""
+    from fastapi.testclient import TestClient
+
+    eng = FakeEngine(max_slots=2)
+    sch = BatchScheduler(eng)
+    try:
+        c = TestClient(create_app(TTSService(sch, {"v": VOICE}, default_voice="v")))
+        assert c.post("/generate", json={"token_ids": [3, 1]}).status_code == 400
+        r = c.post("/generate", json={"token_ids": [3, 1], "max_frames": 5})
+        assert r.status_code == 200 and len(r.content) == 44 + 5 * 1920 * 2
+        r = c.post("/generate", json={"token_ids": [3, 1], "words": 6})
+        assert r.status_code == 200 and len(r.content) == 44 + (6 + 2) * 13 * 1920 * 2
+    finally:
+        sch.close()

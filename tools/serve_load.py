@@ -6,8 +6,8 @@ The launcher never touches the GPU. It starts (1) the server, `python -m pocket_
 (real engine, pipelined, 32 slots, a synthetic 125-frame voice prompt) on 127.0.0.1, and (2)
 client processes, so the load generator does not share the server's interpreter. Each client
 thread POSTs /stream (chunked 16-bit PCM) with 40 token ids and eos_threshold = +1e9 (no EOS:
-each request runs its max_gen_len = 22 * 13 = 286 frames, the tts_model.rs:968-969 rule for 40
-ids). Reports whole-job audio-sec/wall-sec through HTTP and the p50 / p90 time to first chunk.
+each request runs its max_gen_len = 22 * 13 = 286 frames, the tts_model.rs:968-969 rule for the 20
+words stated with the ids). Reports whole-job audio-sec/wall-sec through HTTP and the p50 / p90 time to first chunk.
 
   python tools/serve_load.py [--clients 32] [--procs 4] [--rounds 2] [--port 8765] [--out f.json]"""
 
@@ -48,7 +48,7 @@ def client(port, first, n, t_go):
         time.sleep(max(0.0, t_go - time.time()))
         t0 = time.time()
         t_first, nbytes = None, 0
-        with clients[j].stream("POST", base + "/stream", json={"token_ids": ids(first + j), "eos_threshold": 1e9}) as r:
+        with clients[j].stream("POST", base + "/stream", json={"token_ids": ids(first + j), "words": 20, "eos_threshold": 1e9}) as r:
             r.raise_for_status()
             for chunk in r.iter_bytes():
                 if t_first is None and chunk:
@@ -120,7 +120,7 @@ def main():
                    "ttfc_p90_ms": round(1e3 * ttfc[int(0.9 * (len(ttfc) - 1))], 2)}
             result["rounds"].append(rec)
             print(json.dumps(rec), flush=True)
-        r = httpx.post(base + "/v1/audio/speech", json={"token_ids": ids(0), "response_format": "wav"}, timeout=120)
+        r = httpx.post(base + "/v1/audio/speech", json={"token_ids": ids(0), "words": 20, "response_format": "wav"}, timeout=120)
         r.raise_for_status()
         result["openai_wav_bytes"] = len(r.content)
         if args.out:
