@@ -123,6 +123,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
   // measured slower than a separate row_reduce launch on every front GEMM (ff2 43 vs 13 us with
   // the LayerNorm row finisher, ff1 15.6 vs 11.4 us tile-local): opt-in only
   fuse_splitk_ = getenv("PTTS_FUSED_SPLITK") != nullptr;
+  // pipelined stepping: the back part's kernels run at most one workgroup per CU, so the
+  // latency-bound front part always finds room on every CU (measured 0.735 -> 0.688 ms per step
+  // for the GEMMs alone; tools/sweep_env.sh)
+  back_cap_ = getenv("PTTS_BACK_WG_CAP") ? atoi(getenv("PTTS_BACK_WG_CAP")) : 1;
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
   mods_ = dalloc((size_t)lsd_ * B * NADA);
   xf_ = dalloc((size_t)B * FD);
@@ -945,6 +949,8 @@ hipGraphExec_t Engine::part_graph(int part, int B, int par) {
   else build_back(ops, B, par);
   hipGraph_t g = nullptr;
   PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+  // back part of a pipelined step: its launches leave room for the concurrent front part
+  set_wg_cap(part == 1 && pipeline_ ? back_cap_ : 0);
   try {
     for (const Op& op : ops) op.fn(stream_);
     if (part == 0) {  // the hand-off timeout word, read by fetch() without a device round trip
@@ -955,9 +961,11 @@ hipGraphExec_t Engine::part_graph(int part, int B, int par) {
                               stream_));
     }
   } catch (...) {
+    set_wg_cap(0);
     (void)hipStreamEndCapture(stream_, &g);
     throw;
   }
+  set_wg_cap(0);
   PTTS_HIP(hipStreamEndCapture(stream_, &g));
   hipGraphExec_t ge = nullptr;
   PTTS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));

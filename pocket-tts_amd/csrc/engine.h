@@ -146,6 +146,7 @@ class Engine {
   int* tickets_ = nullptr;
   int* row_tickets_ = nullptr;
   bool fuse_splitk_ = false;
+  int back_cap_ = 1;  // PTTS_BACK_WG_CAP: max workgroups per CU of the pipelined back part's kernels
   GemmArgs last_split_{};
   size_t last_split_op_ = (size_t)-1;
   // pipelined stepping (cfg.pipeline): back part on its own stream, parity events

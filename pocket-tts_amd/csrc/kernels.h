@@ -72,6 +72,9 @@ struct GemmArgs {
   // XCD placement of the tile grid (set by gemm(); speed only): the 8 XCDs split the N tiles
   // into xcd_pn parts and the M tiles into 8 / xcd_pn parts; 0 = contiguous runs of tiles
   int xcd_pn;
+  // > 0: at most this many workgroups of the launch per CU (dynamic LDS reserved to enforce it),
+  // leaving room on every CU for the concurrently running part of a pipelined step
+  int max_wg_per_cu;
   // split-K
   int S;
   float* partial;  // [S][M][N] when S > 1
@@ -195,6 +198,9 @@ struct FlowHeadArgs {
   int* err;
   unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr
 };
+// Launches issued while a cap > 0 is set reserve dynamic LDS so that at most `cap` workgroups of
+// each kernel share a CU (0 = no cap). Process-wide; the engine sets it around graph capture.
+void set_wg_cap(int cap);
 bool flow_head_fits(int B);
 int flow_head_grid(int B);             // workgroups of one k_flow_head launch
 int flow_head_max_resident(int dev);   // co-resident k_flow_head workgroups (occupancy x CUs)

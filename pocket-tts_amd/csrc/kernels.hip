@@ -13,6 +13,20 @@
 
 namespace ptts {
 
+// Workgroups-per-CU cap of the launches issued while it is set (set_wg_cap; the engine sets it
+// while capturing the back part of a pipelined step): dynamic LDS is reserved so that at most
+// `cap` workgroups of a kernel share a CU, leaving room for the concurrently running front part.
+static int g_wg_cap = 0;
+void set_wg_cap(int cap) { g_wg_cap = cap; }
+template <typename K>
+static size_t cap_lds(K kernel, int cap) {
+  if (cap <= 0) return 0;
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel)) != hipSuccess) return 0;
+  const size_t need = 163840 / (cap + 1) + 16;  // cap + 1 workgroups no longer fit (160 KiB per CU)
+  return need > fa.sharedSizeBytes ? need - fa.sharedSizeBytes : 0;
+}
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float gelu_tanh(float x) {
@@ -1144,7 +1158,7 @@ template <typename K>
 static void launch_tiled(K kernel, dim3 grid, int threads, hipStream_t s, const GemmArgs& a) {
   GemmArgs b = a;
   b.xcd_pn = choose_xcd_pn(a, (int)grid.x, (int)grid.y);
-  hipLaunchKernelGGL(kernel, grid, dim3(threads), 0, s, b);
+  hipLaunchKernelGGL(kernel, grid, dim3(threads), cap_lds(kernel, std::max(a.max_wg_per_cu, g_wg_cap)), s, b);
 }
 
 template <int MODE>
@@ -1423,11 +1437,11 @@ __device__ void splitk_combine(const GemmArgs& g, int m0, int n0, int ncols, flo
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s) {
   dim3 grid(a.M, (a.N + 1023) / 1024);
-  if (a.S <= 1) hipLaunchKernelGGL(k_row_reduce<1>, grid, dim3(256), 0, s, a);
-  else if (a.S <= 2) hipLaunchKernelGGL(k_row_reduce<2>, grid, dim3(256), 0, s, a);
-  else if (a.S <= 4) hipLaunchKernelGGL(k_row_reduce<4>, grid, dim3(256), 0, s, a);
-  else if (a.S <= 8) hipLaunchKernelGGL(k_row_reduce<8>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_row_reduce<16>, grid, dim3(256), 0, s, a);
+  if (a.S <= 1) hipLaunchKernelGGL(k_row_reduce<1>, grid, dim3(256), cap_lds(k_row_reduce<1>, g_wg_cap), s, a);
+  else if (a.S <= 2) hipLaunchKernelGGL(k_row_reduce<2>, grid, dim3(256), cap_lds(k_row_reduce<2>, g_wg_cap), s, a);
+  else if (a.S <= 4) hipLaunchKernelGGL(k_row_reduce<4>, grid, dim3(256), cap_lds(k_row_reduce<4>, g_wg_cap), s, a);
+  else if (a.S <= 8) hipLaunchKernelGGL(k_row_reduce<8>, grid, dim3(256), cap_lds(k_row_reduce<8>, g_wg_cap), s, a);
+  else hipLaunchKernelGGL(k_row_reduce<16>, grid, dim3(256), cap_lds(k_row_reduce<16>, g_wg_cap), s, a);
 }
 
 // LayerNorm, one wave per row (N <= 1024, multiple of 64).
@@ -1461,7 +1475,7 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, long ldx, flo
 }
 void layernorm(const float* x, long ldx, float* y, long ldy, int M, int N, const float* w, const float* b,
                float eps, hipStream_t s) {
-  hipLaunchKernelGGL(k_layernorm, dim3((M + 3) / 4), dim3(256), 0, s, x, ldx, y, ldy, M, N, w, b, eps);
+  hipLaunchKernelGGL(k_layernorm, dim3((M + 3) / 4), dim3(256), cap_lds(k_layernorm, g_wg_cap), s, x, ldx, y, ldy, M, N, w, b, eps);
 }
 
 // =============================================================================================
@@ -1519,7 +1533,7 @@ __global__ __launch_bounds__(256) void k_qkv_rope(const float* P, int S, const f
 void qkv_rope_append(const float* P, int S, const float* dense, int M, int nh, RowMap map, KvStore kv, float* Q,
                      hipStream_t s) {
   const int total = M * nh * 32;
-  hipLaunchKernelGGL(k_qkv_rope, dim3((total + 255) / 256), dim3(256), 0, s, P, S, dense, M, nh, map, kv, Q);
+  hipLaunchKernelGGL(k_qkv_rope, dim3((total + 255) / 256), dim3(256), cap_lds(k_qkv_rope, g_wg_cap), s, P, S, dense, M, nh, map, kv, Q);
 }
 
 // =============================================================================================
@@ -1999,17 +2013,17 @@ void rope_table(float* tab, int npos, hipStream_t s) {
 
 void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O, hipStream_t s) {
   if (qg == 1 && window <= 0) {
-    hipLaunchKernelGGL(k_attn_decode, dim3(M, nh), dim3(256), 0, s, Q, nh, map, kv, O);
+    hipLaunchKernelGGL(k_attn_decode, dim3(M, nh), dim3(256), cap_lds(k_attn_decode, g_wg_cap), s, Q, nh, map, kv, O);
   } else if (qg == 16) {
     // 16-row groups never straddle slots (rows-per-slot is 16 or the whole group)
     const dim3 grid((M + 15) / 16, nh);
     if ((kv.cap & (kv.cap - 1)) == 0)
-      hipLaunchKernelGGL(k_attn16<true>, grid, dim3(64 * A16_WAVES), 0, s, Q, M, nh, map, kv, window, O);
+      hipLaunchKernelGGL(k_attn16<true>, grid, dim3(64 * A16_WAVES), cap_lds(k_attn16<true>, g_wg_cap), s, Q, M, nh, map, kv, window, O);
     else
-      hipLaunchKernelGGL(k_attn16<false>, grid, dim3(64 * A16_WAVES), 0, s, Q, M, nh, map, kv, window, O);
+      hipLaunchKernelGGL(k_attn16<false>, grid, dim3(64 * A16_WAVES), cap_lds(k_attn16<false>, g_wg_cap), s, Q, M, nh, map, kv, window, O);
   } else {
     dim3 grid((M + qg - 1) / qg, nh);
-    hipLaunchKernelGGL(k_attention, grid, dim3(256), 0, s, Q, M, nh, map, kv, window, qg, O);
+    hipLaunchKernelGGL(k_attention, grid, dim3(256), cap_lds(k_attention, g_wg_cap), s, Q, M, nh, map, kv, window, qg, O);
   }
 }
 
@@ -2162,7 +2176,7 @@ __global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, con
 void quant_upsample(const float* latent, int B, const float* emb_std, const float* emb_mean, const float* wq,
                     const float* wup, const float* qprev_in, float* qprev_out, const FrameFlags* fl, float* x,
                     float* h, const float* ln_w, const float* ln_b, hipStream_t s) {
-  hipLaunchKernelGGL(k_quant_upsample, dim3(B, 4), dim3(256), 0, s, latent, emb_std, emb_mean, wq, wup, qprev_in,
+  hipLaunchKernelGGL(k_quant_upsample, dim3(B, 4), dim3(256), cap_lds(k_quant_upsample, g_wg_cap), s, latent, emb_std, emb_mean, wq, wup, qprev_in,
                      qprev_out, fl, x, h, ln_w, ln_b);
 }
 
@@ -2216,7 +2230,7 @@ void front_commit(const FrontCommitArgs& a, hipStream_t s) {
 }
 
 void step_commit(const CommitArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_commit, dim3(a.nh + 1, a.B), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_commit, dim3(a.nh + 1, a.B), dim3(256), cap_lds(k_commit, g_wg_cap), s, a);
 }
 
 __global__ __launch_bounds__(256) void k_slot_reset(ResetArgs a) {
@@ -2352,7 +2366,7 @@ void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, co
                 float* Y, int elu_in, hipStream_t s) {
   const long waves = (long)B * ((T + 63) / 64);  // one lane per input channel: cin == 64, k == 3
   (void)k;
-  hipLaunchKernelGGL(k_conv_cout1<3>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, X, H, B, T, cin, w, bias,
+  hipLaunchKernelGGL(k_conv_cout1<3>, dim3((unsigned)((waves + 3) / 4)), dim3(256), cap_lds(k_conv_cout1<3>, g_wg_cap), s, X, H, B, T, cin, w, bias,
                      Y, elu_in);
 }
 
