@@ -1094,9 +1094,11 @@ void Engine::overlap_probe(int B, int reps, double* us) {
   PTTS_HIP(hipStreamCreateWithPriority(&s_lo, hipStreamNonBlocking, prio_lo));
   hipGraphExec_t ge[2] = {};
   hipGraph_t g[2] = {};
-  for (int part = 0; part < 2; ++part) {
+  for (int part = 0; part < 2; ++part) {  // as captured for pipelined stepping (back part capped)
     PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    set_wg_cap(part == 1 ? back_cap_ : 0);
     for (size_t i = part ? cut : 0; i < (part ? ops.size() : cut); ++i) ops[i].fn(stream_);
+    set_wg_cap(0);
     PTTS_HIP(hipStreamEndCapture(stream_, &g[part]));
     PTTS_HIP(hipGraphInstantiate(&ge[part], g[part], nullptr, nullptr, 0));
   }

@@ -1872,11 +1872,13 @@ __device__ __forceinline__ float row16_sum(float v) {
 // 4i + l/16 - exactly the key whose V dims it holds from V load i, so P.V needs no broadcast.
 // The rows (l/16) are combined once per wave at the end. Each wave issues its first block's
 // loads before the QKV/RoPE phase: the cached keys do not depend on this step's token.
-__global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict__ P, int S, int M, int nh, RowMap mp,
+template <int NW, int KQ>
+__global__ __launch_bounds__(64 * NW) void k_attn_decode_qkv(const float* __restrict__ P, int S, int M, int nh, RowMap mp,
                                                          KvStore kv, const float* __restrict__ rope,
                                                          float* __restrict__ O) {
-  __shared__ float s_m[4], s_l[4];
-  __shared__ __attribute__((aligned(16))) float s_o[4][64];
+  constexpr int BLK = 4 * KQ * NW;  // keys per round: NW waves x KQ loads of 4 keys
+  __shared__ float s_m[NW], s_l[NW];
+  __shared__ __attribute__((aligned(16))) float s_o[NW][64];
   __shared__ __attribute__((aligned(16))) float s_qkv[3][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1893,16 +1895,16 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
   float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
   float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
   const int last = qp - 1;
-  float4 k[16], v[16];
+  float4 k[KQ], v[KQ];
   auto load_block = [&](int base) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < KQ; ++i) {
       const long off = (long)min(base + 4 * i + g, last) * 64 + c4;
       k[i] = *reinterpret_cast<const float4*>(kbase + off);
       v[i] = *reinterpret_cast<const float4*>(vbase + off);
     }
   };
-  int base = 64 * wave;
+  int base = 4 * KQ * wave;
   if (base < qp) load_block(base);
   if (tid < 192) {  // q | k | v column of this head, summed over the slabs in z order
     const int part = tid >> 6;
@@ -1929,11 +1931,11 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
   const float4 q = *reinterpret_cast<const float4*>(&s_qkv[0][c4]);
   float m = -INFINITY, l = 0.f;
   float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (; base < qp; base += 256) {  // cached keys 0 .. qp-1, block `base` already in registers
-    float sc[16];
+  for (; base < qp; base += BLK) {  // cached keys 0 .. qp-1, block `base` already in registers
+    float sc[KQ];
     float bm = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < KQ; ++i) {
       const float part = q.x * k[i].x + q.y * k[i].y + q.z * k[i].z + q.w * k[i].w;
       const float t = row16_sum(part) * 0.125f;  // 1/sqrt(64) (attention.rs:191,229)
       sc[i] = base + 4 * i + g <= last ? t : -INFINITY;
@@ -1946,7 +1948,7 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
     float ps = 0.f;
     o.x *= alpha; o.y *= alpha; o.z *= alpha; o.w *= alpha;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < KQ; ++i) {
       const float p = expf(sc[i] - mn);  // 0 for masked keys
       ps += p;
       o.x += p * v[i].x; o.y += p * v[i].y; o.z += p * v[i].z; o.w += p * v[i].w;
@@ -1955,7 +1957,7 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
     ps += __shfl_xor(ps, 32, 64);
     l = l * alpha + ps;
     m = mn;
-    if (base + 256 < qp) load_block(base + 256);
+    if (base + BLK < qp) load_block(base + BLK);
   }
   // combine the 4 key rows (lanes l, l^16, l^32, l^48 hold the same dims)
   o.x += __shfl_xor(o.x, 16, 64); o.y += __shfl_xor(o.y, 16, 64);
@@ -1980,10 +1982,12 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
   if (lane < 16) *reinterpret_cast<float4*>(&s_o[wave][c4]) = o;
   __syncthreads();
   if (wave == 0) {
-    const float Mx = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    float Mx = s_m[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) Mx = fmaxf(Mx, s_m[w]);
     float num = 0.f, den = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float e = s_m[w] == -INFINITY ? 0.f : expf(s_m[w] - Mx);
       num += s_o[w][lane] * e;
       den += s_l[w] * e;
@@ -1994,7 +1998,16 @@ __global__ __launch_bounds__(256) void k_attn_decode_qkv(const float* __restrict
 
 void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStore kv, const float* rope, float* O,
                         hipStream_t s) {
-  hipLaunchKernelGGL(k_attn_decode_qkv, dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
+  // 4 waves x 32 keys (128 keys per round, 133 VGPRs): in the pipelined step the front part's
+  // attention shares each CU with a back-part workgroup, and this register budget keeps two of
+  // its workgroups resident beside it. Steady step 0.690 -> 0.673 ms against 4 x 64 keys
+  // (238 VGPRs, faster alone); 8 x 32, 4 x 48, 4 x 16, 2 x 64, 8 x 48 measured in between
+  // (tools/sweep_env.sh). PTTS_ATTN_WIDE=1 selects the 4 x 64 form.
+  static const bool wide = getenv("PTTS_ATTN_WIDE") != nullptr;
+  if (wide)
+    hipLaunchKernelGGL((k_attn_decode_qkv<4, 16>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
+  else
+    hipLaunchKernelGGL((k_attn_decode_qkv<4, 8>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
 }
 
 __global__ __launch_bounds__(256) void k_rope_table(float* tab, int npos) {
