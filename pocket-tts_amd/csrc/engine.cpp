@@ -397,6 +397,10 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   a.W = Wt;
   a.S = S;
   a.partial = partial_;
+  {  // FlowLM / flow-head step weights are read once per step: non-temporal loads (PTTS_NT bits)
+    const int nt = getenv("PTTS_NT") ? atoi(getenv("PTTS_NT")) : 3;
+    a.w_nt = M <= 64 && ((layout != 0 && (nt & 1)) || (layout == 0 && (nt & 4)));
+  }
   ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
                  (w8 || wf8 ? (double)N * K + 4.0 * N : 4.0 * N * K) + 4.0 * ((double)M * K + (double)S * M * N)});
   last_split_ = a;

@@ -75,6 +75,8 @@ struct GemmArgs {
   // > 0: at most this many workgroups of the launch per CU (dynamic LDS reserved to enforce it),
   // leaving room on every CU for the concurrently running part of a pipelined step
   int max_wg_per_cu;
+  // 1: the weight stream is read with non-temporal loads (once-read FlowLM step weights)
+  int w_nt;
   // split-K
   int S;
   float* partial;  // [S][M][N] when S > 1

@@ -262,10 +262,20 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
   constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
   auto load = [&](int cc, float4 (&A)[4], float4 (&Bv)[4]) {
     const float* ap = a_ptr(cc << 5);
+    if (a.w_nt) {  // wave-uniform: the once-read weight stream with the non-temporal hint
+      typedef float f4v __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      Bv[i] = *reinterpret_cast<const float4*>(wrow + (cc << 5) + 4 * i);
-      A[i] = *reinterpret_cast<const float4*>(ap + 4 * i);
+      for (int i = 0; i < 4; ++i) {
+        const f4v w = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(wrow + (cc << 5) + 4 * i));
+        Bv[i] = make_float4(w.x, w.y, w.z, w.w);
+        A[i] = *reinterpret_cast<const float4*>(ap + 4 * i);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        Bv[i] = *reinterpret_cast<const float4*>(wrow + (cc << 5) + 4 * i);
+        A[i] = *reinterpret_cast<const float4*>(ap + 4 * i);
+      }
     }
   };
   auto mma = [&](float4 (&A)[4], float4 (&Bv)[4]) {
@@ -544,6 +554,20 @@ __device__ __forceinline__ void glds16(const float* gsrc, unsigned lds_byte) {
       : "v"(gsrc), "s"(lds_byte)
       : "memory");
 }
+// The same with the non-temporal hint (weights that one CU reads once per step: the decode's
+// weight stream, MI355X_MICROARCH.md price row nt-weights).
+__device__ __forceinline__ void glds16_nt(const float* gsrc, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_byte)
+      : "memory");
+}
 __device__ __forceinline__ unsigned lds_addr(const float* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) float*)(p);
 }
@@ -633,7 +657,8 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
       }
       // wave-uniform LDS base of this instruction; lane l -> + 16*l bytes
       const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)((buf * ROWS * BK + j * RPI * BK) * 4));
-      glds16(src, dst);
+      if (a.w_nt && j * RPI >= TM) glds16_nt(src, dst);  // wave-uniform: a W row instruction
+      else glds16(src, dst);
     }
   };
   constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
@@ -1872,7 +1897,7 @@ __device__ __forceinline__ float row16_sum(float v) {
 // 4i + l/16 - exactly the key whose V dims it holds from V load i, so P.V needs no broadcast.
 // The rows (l/16) are combined once per wave at the end. Each wave issues its first block's
 // loads before the QKV/RoPE phase: the cached keys do not depend on this step's token.
-template <int NW, int KQ>
+template <int NW, int KQ, bool NT = false>
 __global__ __launch_bounds__(64 * NW) void k_attn_decode_qkv(const float* __restrict__ P, int S, int M, int nh, RowMap mp,
                                                          KvStore kv, const float* __restrict__ rope,
                                                          float* __restrict__ O) {
@@ -1900,8 +1925,16 @@ __global__ __launch_bounds__(64 * NW) void k_attn_decode_qkv(const float* __rest
 #pragma unroll
     for (int i = 0; i < KQ; ++i) {
       const long off = (long)min(base + 4 * i + g, last) * 64 + c4;
-      k[i] = *reinterpret_cast<const float4*>(kbase + off);
-      v[i] = *reinterpret_cast<const float4*>(vbase + off);
+      if (NT) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v kk = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(kbase + off));
+        const f4v vv = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(vbase + off));
+        k[i] = make_float4(kk.x, kk.y, kk.z, kk.w);
+        v[i] = make_float4(vv.x, vv.y, vv.z, vv.w);
+      } else {
+        k[i] = *reinterpret_cast<const float4*>(kbase + off);
+        v[i] = *reinterpret_cast<const float4*>(vbase + off);
+      }
     }
   };
   int base = 4 * KQ * wave;
@@ -2004,7 +2037,10 @@ void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStor
   // (238 VGPRs, faster alone); 8 x 32, 4 x 48, 4 x 16, 2 x 64, 8 x 48 measured in between
   // (tools/sweep_env.sh). PTTS_ATTN_WIDE=1 selects the 4 x 64 form.
   static const bool wide = getenv("PTTS_ATTN_WIDE") != nullptr;
-  if (wide)
+  static const bool nt = !getenv("PTTS_NT") || (atoi(getenv("PTTS_NT")) & 2);
+  if (nt)
+    hipLaunchKernelGGL((k_attn_decode_qkv<4, 8, true>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
+  else if (wide)
     hipLaunchKernelGGL((k_attn_decode_qkv<4, 16>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
   else
     hipLaunchKernelGGL((k_attn_decode_qkv<4, 8>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
