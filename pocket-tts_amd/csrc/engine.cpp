@@ -82,7 +82,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   eos_ = dalloc(B);
   static_assert(sizeof(FrameFlags) == 2 * sizeof(float), "FrameFlags packs into two floats");
   meta_floats_ = (size_t)B * (LDIM + 1 + 2);
-  for (int q = 0; q < 2; ++q) {  // front -> back hand-off, one set per step parity
+  for (int q = 0; q < NHB; ++q) {  // front -> back hand-off buffers
     meta_[q] = dalloc(meta_floats_);
     lat_out_[q] = meta_[q];                                  // 128-B aligned,
     flags_[q] = (FrameFlags*)(meta_[q] + (size_t)B * LDIM);  // so FrameFlags stay 8-B aligned
@@ -126,6 +126,9 @@ Engine::Engine(const ptts_engine_config& cfg) {
   // pipelined stepping: the back part's kernels run at most one workgroup per CU, so the
   // latency-bound front part always finds room on every CU (measured 0.735 -> 0.688 ms per step
   // for the GEMMs alone; tools/sweep_env.sh)
+  // two hand-off buffers by default: the step is front-bound, and letting the front part run two
+  // frames ahead (3 buffers) measured 0.5% slower (more front/back overlap, same front work)
+  nhb_ = getenv("PTTS_HANDOFF_BUFS") && atoi(getenv("PTTS_HANDOFF_BUFS")) == 3 ? 3 : 2;
   back_cap_ = getenv("PTTS_BACK_WG_CAP") ? atoi(getenv("PTTS_BACK_WG_CAP")) : 1;
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
   mods_ = dalloc((size_t)lsd_ * B * NADA);
@@ -158,7 +161,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   rope_ = dalloc((size_t)max_ctx_ * 64);
   temb_tmp_ = dalloc((size_t)2 * lsd_ * FD);
 
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NHB; ++q) {
     PTTS_HIP(hipHostMalloc((void**)&h_pcm_[q], sizeof(float) * B * FRAME, hipHostMallocDefault));
     PTTS_HIP(hipHostMalloc((void**)&h_meta_[q], sizeof(float) * meta_floats_, hipHostMallocDefault));
     memset(h_meta_[q], 0, sizeof(float) * meta_floats_);
@@ -171,7 +174,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_HIP(hipHostMalloc((void**)&h_ids_, sizeof(int) * PREFILL, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_tab_, sizeof(int) * PREFILL, hipHostMallocDefault));
   PTTS_HIP(hipStreamCreateWithFlags(&stream_be_, hipStreamNonBlocking));
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NHB; ++q) {
     PTTS_HIP(hipEventCreateWithFlags(&ev_front_[q], hipEventDisableTiming));
     PTTS_HIP(hipEventCreateWithFlags(&ev_back_[q], hipEventDisableTiming));
     PTTS_HIP(hipEventRecord(ev_front_[q], stream_));
@@ -197,14 +200,14 @@ Engine::~Engine() {
   if (stream_be_) (void)hipStreamSynchronize(stream_be_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NHB; ++q) {
     if (ev_front_[q]) (void)hipEventDestroy(ev_front_[q]);
     if (ev_back_[q]) (void)hipEventDestroy(ev_back_[q]);
   }
   if (ev_admit_) (void)hipEventDestroy(ev_admit_);
   if (stream_be_) (void)hipStreamDestroy(stream_be_);
   for (void* p : allocs_) (void)hipFree(p);
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NHB; ++q) {
     if (h_pcm_[q]) (void)hipHostFree(h_pcm_[q]);
     if (h_meta_[q]) (void)hipHostFree(h_meta_[q]);
   }
@@ -594,8 +597,8 @@ bool Engine::use_head_chain(int B) const {
   return true;
 }
 
-// FRONT part of a step (FlowLM + flow head) for rows [0, B), handing its frame to parity `par`.
-void Engine::build_front(std::vector<Op>& ops, int B, int par) {
+// FRONT part of a step (FlowLM + flow head) for rows [0, B), handing its frame to buffer `hb`.
+void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
   int S = 1;
   // ---- FlowLM step (flow_lm.rs:98-164): input_linear -> transformer -> out_norm
   {
@@ -752,25 +755,26 @@ void Engine::build_front(std::vector<Op>& ops, int B, int par) {
     c.eos = eos_;
     c.cur = cur_;
     c.lat_in = lat_in_;
-    c.lat_out = lat_out_[par];
-    c.eos_out = eos_out_[par];
-    c.flags = flags_[par];
+    c.lat_out = lat_out_[hb];
+    c.eos_out = eos_out_[hb];
+    c.flags = flags_[hb];
     c.fpos = fpos_;
     ops.push_back({"front_commit", [c](hipStream_t s) { front_commit(c, s); }});
   }
 }
 
-// BACK part of a step: Mimi decode of the frames the front part left in parity `par`.
-void Engine::build_back(std::vector<Op>& ops, int B, int par) {
+// BACK part of a step: Mimi decode of the frames the front part left in buffer `hb`; `qp` is the
+// frame's parity for the quantizer history (the previous frame's quantizer output is in qp ^ 1).
+void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   // ---- Mimi decode (mimi.rs:143-157): quantize + upsample, decoder transformer, SEANet decoder
   {
-    const float *lat = lat_out_[par], *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w),
+    const float *lat = lat_out_[hb], *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w),
                 *wu = W(L_.up_w);
     const float *lw = W(L_.mdec[0].n1w), *lb = W(L_.mdec[0].n1b);
-    const float* qin = qprev_ + (size_t)(par ^ 1) * max_slots_ * MD;
-    float* qout = qprev_ + (size_t)par * max_slots_ * MD;
+    const float* qin = qprev_ + (size_t)(qp ^ 1) * max_slots_ * MD;
+    float* qout = qprev_ + (size_t)qp * max_slots_ * MD;
     float *x = mx_, *h = mh_;
-    const FrameFlags* fl = flags_[par];
+    const FrameFlags* fl = flags_[hb];
     ops.push_back({"mimi.quant_upsample",
                    [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qin, qout, fl, x, h, lw, lb, s); }});
   }
@@ -909,7 +913,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
   }
   {
     const float *X = ca_[2], *H = hist_[7], *w = W(L_.dfin_w), *b = W(L_.dfin_b);
-    float* Y = pcm_[par];
+    float* Y = pcm_[hb];
     ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, FRAME, 64, 3, w, b, Y, 0, s); }});
   }
   // ---- commit of the back part: conv histories and Mimi positions of rows with a frame
@@ -919,17 +923,17 @@ void Engine::build_back(std::vector<Op>& ops, int B, int par) {
     for (int i = 0; i < 8; ++i) c.h[i] = HistDesc{srcs[i], hist_[i], hist_T_[i], hist_C_[i], hist_P_[i]};
     c.nh = 8;
     c.B = B;
-    c.flags = flags_[par];
+    c.flags = flags_[hb];
     c.mpos = mpos_;
     ops.push_back({"commit", [c](hipStream_t s) { step_commit(c, s); }});
   }
 }
 
-// The whole step in plan order (front then back, parity 0): plan listing and per-op timing.
+// The whole step in plan order (front then back, buffer 0): plan listing and per-op timing.
 std::vector<Op> Engine::build_step(int B) {
   std::vector<Op> ops;
   build_front(ops, B, 0);
-  build_back(ops, B, 0);
+  build_back(ops, B, 0, 0);
   return ops;
 }
 
@@ -944,13 +948,14 @@ std::vector<std::string> Engine::plan_names(int B) {
   return v;
 }
 
-hipGraphExec_t Engine::part_graph(int part, int B, int par) {
-  const int key = (B * 2 + part) * 2 + par;
+hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
+  if (part == 0) qp = 0;  // the front part does not use the quantizer history
+  const int key = ((B * 2 + part) * NHB + hb) * 2 + qp;
   auto it = graphs_.find(key);
   if (it != graphs_.end()) return it->second;
   std::vector<Op> ops;
-  if (part == 0) build_front(ops, B, par);
-  else build_back(ops, B, par);
+  if (part == 0) build_front(ops, B, hb);
+  else build_back(ops, B, hb, qp);
   hipGraph_t g = nullptr;
   PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   // back part of a pipelined step: its launches leave room for the concurrent front part
@@ -959,9 +964,9 @@ hipGraphExec_t Engine::part_graph(int part, int B, int par) {
     for (const Op& op : ops) op.fn(stream_);
     if (part == 0) {  // the hand-off timeout word, read by fetch() without a device round trip
       PTTS_HIP(hipMemcpyAsync(h_err_, herr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
-    } else {  // the frame of this parity leaves HBM inside the step (fetch() reads host memory)
-      PTTS_HIP(hipMemcpyAsync(h_pcm_[par], pcm_[par], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, stream_));
-      PTTS_HIP(hipMemcpyAsync(h_meta_[par], meta_[par], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
+    } else {  // the frame of this buffer leaves HBM inside the step (fetch() reads host memory)
+      PTTS_HIP(hipMemcpyAsync(h_pcm_[hb], pcm_[hb], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, stream_));
+      PTTS_HIP(hipMemcpyAsync(h_meta_[hb], meta_[hb], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
                               stream_));
     }
   } catch (...) {
@@ -981,35 +986,37 @@ hipGraphExec_t Engine::part_graph(int part, int B, int par) {
 // One call = one step of the generation loop for rows [0, B).
 //   sequential: front(k) then back(k) on one stream; the call's frame is frame k.
 //   pipelined:  front(k) on stream_ || back(k-1) on stream_be_ (the back part decodes the frame
-//               the previous call's front part produced); the call's frame is frame k-1. The
-//               parity buffers make the two independent: front(k) only waits for back(k-2)
-//               (last reader of its parity), back(k-1) for front(k-1).
+//               the previous call's front part produced); the call's frame is frame k-1. Frame
+//               k's hand-off buffer is k % nhb_ (2, or 3 with PTTS_HANDOFF_BUFS=3): front(k)
+//               waits only for back(k - nhb_), the last reader of its buffer, and back(k-1) for
+//               front(k-1).
 void Engine::step_async(int B) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
   PTTS_HIP(hipSetDevice(dev_));
-  const int par = (int)(k_ & 1);
-  hipGraphExec_t front = part_graph(0, B, par);
+  const int hb = (int)(k_ % nhb_), qp = (int)(k_ & 1);
+  hipGraphExec_t front = part_graph(0, B, hb, 0);
   if (!pipeline_) {
-    hipGraphExec_t back = part_graph(1, B, par);
+    hipGraphExec_t back = part_graph(1, B, hb, qp);
     PTTS_HIP(hipGraphLaunch(front, stream_));
     PTTS_HIP(hipGraphLaunch(back, stream_));
-    out_par_ = par;
+    out_hb_ = hb;
     out_rows_ = B;
   } else {
     const int prev_rows = k_ > 0 ? front_rows_ : B;
-    hipGraphExec_t back = part_graph(1, prev_rows, par ^ 1);
-    PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[par], 0));
+    const int hb1 = (hb + nhb_ - 1) % nhb_, qp1 = qp ^ 1;  // frame k-1
+    hipGraphExec_t back = part_graph(1, prev_rows, hb1, qp1);
+    PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
     PTTS_HIP(hipGraphLaunch(front, stream_));
-    PTTS_HIP(hipEventRecord(ev_front_[par], stream_));
-    PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[par ^ 1], 0));
+    PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
+    PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[hb1], 0));
     if (admit_pending_) {  // slot state rewritten since the front part this back part decodes
       PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
       admit_pending_ = false;
     }
     PTTS_HIP(hipGraphLaunch(back, stream_be_));
-    PTTS_HIP(hipEventRecord(ev_back_[par ^ 1], stream_be_));
-    out_par_ = par ^ 1;
+    PTTS_HIP(hipEventRecord(ev_back_[hb1], stream_be_));
+    out_hb_ = hb1;
     out_rows_ = prev_rows;
   }
   front_rows_ = B;
@@ -1026,10 +1033,15 @@ void Engine::sync() {
 // report no frame. The step's graphs already copied the frame into pinned host memory.
 void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat) {
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
-  sync();
-  const int q = out_par_;
+  // Pipelined: wait only for the back part that produced this call's frame. The front part of
+  // the next frame keeps running, so the front stream never idles across calls (the next call's
+  // front graph is queued behind it while this one still runs).
+  if (pipeline_) PTTS_HIP(hipEventSynchronize(ev_back_[out_hb_]));
+  else sync();
+  const int q = out_hb_;
   const int n = std::min(B, out_rows_);
   if (*h_err_) {  // k_flow_head's bounded hand-off waits: a timeout poisons the frame, fail loudly
+    sync();
     *h_err_ = 0;
     PTTS_HIP(hipMemsetAsync(herr_, 0, sizeof(int), stream_));
     PTTS_HIP(hipStreamSynchronize(stream_));
@@ -1478,6 +1490,7 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     r.mpos = mpos_;
     r.flags0 = flags_[0];
     r.flags1 = flags_[1];
+    r.flags2 = flags_[2];
     slot_reset(r, stream_);
     PTTS_HIP(hipGetLastError());
   }
@@ -1540,7 +1553,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
   PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
   PTTS_REQUIRE(lat != nullptr && n >= 1, "no latents");
   sync();
-  for (int q = 0; q < 2; ++q) PTTS_HIP(hipMemsetAsync(flags_[q], 0, sizeof(FrameFlags) * max_slots_, stream_));
+  for (int q = 0; q < NHB; ++q) PTTS_HIP(hipMemsetAsync(flags_[q], 0, sizeof(FrameFlags) * max_slots_, stream_));
   {
     SlotState s{};
     s.eos_step = -1;
@@ -1571,6 +1584,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
     r.mpos = mpos_;
     r.flags0 = flags_[0];
     r.flags1 = flags_[1];
+    r.flags2 = flags_[2];
     slot_reset(r, stream_);
     PTTS_HIP(hipGetLastError());
   }
@@ -1585,7 +1599,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
                             hipMemcpyHostToDevice, stream_));
     PTTS_HIP(hipMemcpyAsync(flags_[par] + slot, &on, sizeof on, hipMemcpyHostToDevice, stream_));
     std::vector<Op> ops;
-    build_back(ops, slot + 1, par);
+    build_back(ops, slot + 1, par, par);
     size_t j = 0;
     for (; j < ops.size(); ++j) {
       if (ops[j].name == "seanet.conv0" && tr) rows16(tr + (size_t)i * UP * MD, mx_);
@@ -1613,7 +1627,7 @@ void Engine::slot_close(int slot) {
   s.eos_step = -1;
   memcpy(h_st_, &s, sizeof s);  // pinned staging (free: sync() above)
   PTTS_HIP(hipMemcpyAsync(st_ + slot, h_st_, sizeof s, hipMemcpyHostToDevice, stream_));
-  for (int q = 0; q < 2; ++q)  // drop a pending frame of the slot
+  for (int q = 0; q < NHB; ++q)  // drop a pending frame of the slot
     PTTS_HIP(hipMemsetAsync(flags_[q] + slot, 0, sizeof(FrameFlags), stream_));
   mark_admission();
   PTTS_HIP(hipStreamSynchronize(stream_));

@@ -69,9 +69,11 @@ class Engine {
   void prefill_rows(std::vector<Op>& ops, int slot, int T, int p0);
   void run_ops(const std::vector<Op>& ops);
   std::vector<Op> build_step(int B);
-  void build_front(std::vector<Op>& ops, int B, int par);
-  void build_back(std::vector<Op>& ops, int B, int par);
-  hipGraphExec_t part_graph(int part, int B, int par);
+  // hb: front -> back hand-off buffer (frame index mod NHB); qp: parity of the back part's
+  // quantizer history (frame index mod 2; the back part reads the previous frame's half)
+  void build_front(std::vector<Op>& ops, int B, int hb);
+  void build_back(std::vector<Op>& ops, int B, int hb, int qp);
+  hipGraphExec_t part_graph(int part, int B, int hb, int qp);
   void push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r);
   void flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag);
   void linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M, const float* Wt,
@@ -133,11 +135,15 @@ class Engine {
   float *cb_[3] = {}, *cv_[3] = {}, *ca_[3] = {}, *ce_[3] = {};
   float* trb_[3] = {};  // transposed-conv biases replicated over the r output phases [r][Cout]
   // front -> back hand-off per step parity, and the back part's own split-K slabs
-  float* lat_out_[2] = {};
-  float* eos_out_[2] = {};
-  FrameFlags* flags_[2] = {};
-  float* pcm_[2] = {};
-  float* meta_[2] = {};  // per parity, one allocation: lat_out [B][32] | flags [B] | eos_out [B]
+  // Up to three hand-off buffers: front(k) writes buffer k % nhb_ and waits only for back(k - nhb_)
+  // (nhb_ = 3 lets front and back drift a step apart instead of running in lockstep).
+  static constexpr int NHB = 3;
+  int nhb_ = 2;  // buffers in use (2 or 3)
+  float* lat_out_[NHB] = {};
+  float* eos_out_[NHB] = {};
+  FrameFlags* flags_[NHB] = {};
+  float* pcm_[NHB] = {};
+  float* meta_[NHB] = {};  // per parity, one allocation: lat_out [B][32] | flags [B] | eos_out [B]
   size_t meta_floats_ = 0;
   float* mpartial_ = nullptr;
   size_t mpcap_ = 0;
@@ -152,14 +158,14 @@ class Engine {
   // pipelined stepping (cfg.pipeline): back part on its own stream, parity events
   bool pipeline_ = false;
   hipStream_t stream_be_ = nullptr;
-  hipEvent_t ev_front_[2] = {}, ev_back_[2] = {};
+  hipEvent_t ev_front_[NHB] = {}, ev_back_[NHB] = {};
   // admission / slot_close / set_latent write slot state on stream_ after the last front part the
   // next back part decodes: that back part (stream_be_) waits for this event first
   hipEvent_t ev_admit_ = nullptr;
   bool admit_pending_ = false;
   void mark_admission();
   long long k_ = 0;          // steps issued
-  int out_par_ = 0;          // parity of the frame the last call produced
+  int out_hb_ = 0;           // hand-off buffer of the frame the last call produced
   int out_rows_ = 0;         // rows that frame covers
   int front_rows_ = 0;       // rows of the last front part
   float *temb_ = nullptr, *temb_tmp_ = nullptr;
@@ -167,8 +173,8 @@ class Engine {
 
   // pinned host staging: each back graph ends in async D2H copies of its frame (PCM + metadata)
   // into the host set of its parity, so fetch() only reads host memory
-  float* h_pcm_[2] = {};
-  float* h_meta_[2] = {};
+  float* h_pcm_[NHB] = {};
+  float* h_meta_[NHB] = {};
   int* h_err_ = nullptr;  // copy of herr_ made at the end of every front graph
   int head_resident_ = 0;  // k_flow_head workgroups that can be co-resident on this device
   int *h_slots_ = nullptr, *h_fp_ = nullptr, *h_ids_ = nullptr, *h_tab_ = nullptr;  // admission staging

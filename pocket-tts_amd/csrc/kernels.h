@@ -264,8 +264,9 @@ struct ResetArgs {
   const float* bos;
   const SlotState* st_src;
   const int* fpos_src;
-  FrameFlags* flags0;  // both parity buffers: an undrained frame of the slot's previous
+  FrameFlags* flags0;  // every hand-off buffer: an undrained frame of the slot's previous
   FrameFlags* flags1;  // utterance is discarded
+  FrameFlags* flags2;
   SlotState* st;
   int* fpos;
   int* mpos;

@@ -2297,6 +2297,7 @@ __global__ __launch_bounds__(256) void k_slot_reset(ResetArgs a) {
     a.mpos[slot] = 0;
     a.flags0[slot] = FrameFlags{0, 0};
     a.flags1[slot] = FrameFlags{0, 0};
+    a.flags2[slot] = FrameFlags{0, 0};
   }
 }
 
