@@ -129,6 +129,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   // two hand-off buffers by default: the step is front-bound, and letting the front part run two
   // frames ahead (3 buffers) measured 0.5% slower (more front/back overlap, same front work)
   nhb_ = getenv("PTTS_HANDOFF_BUFS") && atoi(getenv("PTTS_HANDOFF_BUFS")) == 3 ? 3 : 2;
+  mimi_attn_fused_ = !getenv("PTTS_MIMI_ATTN_UNFUSED");
   back_cap_ = getenv("PTTS_BACK_WG_CAP") ? atoi(getenv("PTTS_BACK_WG_CAP")) : 1;
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
   mods_ = dalloc((size_t)lsd_ * B * NADA);
@@ -136,8 +137,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
   hf_ = dalloc((size_t)B * FD);
   uf_ = dalloc((size_t)B * FD);
   head_chain_ = !getenv("PTTS_HEAD_CHAIN_OFF");
-  hxp_ = dalloc((size_t)B * FD);
-  hup_ = dalloc((size_t)B * FD);
+  PTTS_REQUIRE(hx_floats(B) * 4 < (1ull << 31), "flow-head hand-off regions exceed 2 GB (lsd_decode_steps too large)");
+  hx_ = dalloc(hx_floats(B));
+  PTTS_HIP(hipMemset(hx_, 0xFF, hx_floats(B) * 4));  // empty (the launch ahead re-arms the used part)
+  PTTS_HIP(hipDeviceSynchronize());                    // null-stream memset: see dalloc
   hctr_ = (int*)dalloc(4 * ((B + 15) / 16) + 4);
   herr_ = (int*)dalloc(4);
   mx_ = dalloc((size_t)B * UP * MD);
@@ -418,7 +421,7 @@ void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowRed
   const bool prev_is_gemm = !ops.empty() && last_split_op_ == ops.size() - 1;
   const bool tiles_ok = g.layout == 0 || g.layout == 13 || g.layout == 7;
   const bool ln_ok = !r.ln || (r.N % 256 == 0 && r.N <= 1024);
-  const bool same = prev_is_gemm && r.P == g.partial && r.S == g.S && r.M == g.M && r.N == g.N;
+  const bool same = prev_is_gemm && r.P == g.partial && r.S == g.S && r.M == g.M && r.N == g.N && !r.fill;
   if (fuse_splitk_ && same && tiles_ok && ln_ok) {
     const int gx = (g.layout == 13 || g.layout == 7) ? (g.N + 127) / 128 : (g.N + 31) / 32;
     const int gy = (g.M + 31) / 32;
@@ -631,6 +634,10 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     a.bias = W(L_.ada_b);
     a.Y = mods_;
     a.ldy = NADA;
+    if (use_head_chain(B)) {  // side job: empty the hand-off regions k_flow_head uses next
+      a.fill = hx_;
+      a.fill_n4 = (long)(hx_floats(B) / 4);
+    }
     push_rr(ops, "head.ada_reduce", a);
   }
   // lsd_decode Euler steps (flow_lm.rs:7-22) over ResBlocks (mlp.rs:146-213): one persistent
@@ -654,15 +661,18 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     f.blk = (long)(L_.rb_w0[1] - L_.rb_w0[0]);
     f.fin_w = W(L_.fin_w);
     f.fin_b = W(L_.fin_b);
-    f.xp = hxp_;
-    f.up = hup_;
+    f.hx = hx_;
     f.ctr = hctr_;
     f.err = herr_;
     f.dbg = getenv("PTTS_HEAD_DBG") ? (unsigned long long*)strtoull(getenv("PTTS_HEAD_DBG"), nullptr, 0) : nullptr;
     const double fl = 2.0 * lsd_ * B * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD);
     const double by = 4.0 * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD) +
                       4.0 * lsd_ * B * ((double)FDEPTH * 3 * FD + 2 * FD);
-    ops.push_back({"head.chain", [f](hipStream_t s) { flow_head(f, s); }, fl, by});
+    float* hx = hx_;
+    const size_t nhx = hx_floats(B);
+    Op op{"head.chain", [f](hipStream_t s) { flow_head(f, s); }, fl, by};
+    op.prep = [hx, nhx](hipStream_t s) { PTTS_HIP(hipMemsetD32Async(hx, 0xFFFFFFFFu, nhx, s)); };
+    ops.push_back(op);
   }
   for (int st = 0; st < lsd_ && !use_head_chain(B); ++st) {
     const float* mods = mods_ + (size_t)st * B * NADA;
@@ -791,12 +801,13 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
                fat ? 15 : 0);
       const float* qkv = mqkv_;
       float* Q = mq_;
-      ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(nullptr, 0, qkv, MR, MNH, mmap, kv, Q, s); }});
-    }
-    {
-      const float* Q = mq_;
       float* O = mo_;
-      ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, MR, MNH, mmap, kv, MCTX, UP, O, s); }});
+      if (mimi_attn_fused_) {  // RoPE + ring append inside the attention launch
+        ops.push_back({p + ".attention", [=](hipStream_t s) { attention16_qkv(qkv, MR, MNH, mmap, kv, MCTX, O, s); }});
+      } else {
+        ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(nullptr, 0, qkv, MR, MNH, mmap, kv, Q, s); }});
+        ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, MR, MNH, mmap, kv, MCTX, UP, O, s); }});
+      }
     }
     dense_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, nullptr, ACT_NONE, W(t.ls1), mx_, mx_);
     {
@@ -1079,13 +1090,33 @@ double Engine::time_op(int B, const std::string& name, int reps) {
   hipEvent_t e0, e1;
   PTTS_HIP(hipEventCreate(&e0));
   PTTS_HIP(hipEventCreate(&e1));
-  sel->fn(stream_);  // warm
-  PTTS_HIP(hipEventRecord(e0, stream_));
-  for (int i = 0; i < reps; ++i) sel->fn(stream_);
-  PTTS_HIP(hipEventRecord(e1, stream_));
-  PTTS_HIP(hipEventSynchronize(e1));
   float ms = 0.f;
-  PTTS_HIP(hipEventElapsedTime(&ms, e0, e1));
+  if (sel->prep) {  // each replay behind its own prep: (prep, op) x reps minus prep x reps
+    sel->prep(stream_);
+    sel->fn(stream_);  // warm
+    PTTS_HIP(hipEventRecord(e0, stream_));
+    for (int i = 0; i < reps; ++i) {
+      sel->prep(stream_);
+      sel->fn(stream_);
+    }
+    PTTS_HIP(hipEventRecord(e1, stream_));
+    PTTS_HIP(hipEventSynchronize(e1));
+    float both = 0.f, prep = 0.f;
+    PTTS_HIP(hipEventElapsedTime(&both, e0, e1));
+    PTTS_HIP(hipEventRecord(e0, stream_));
+    for (int i = 0; i < reps; ++i) sel->prep(stream_);
+    PTTS_HIP(hipEventRecord(e1, stream_));
+    PTTS_HIP(hipEventSynchronize(e1));
+    PTTS_HIP(hipEventElapsedTime(&prep, e0, e1));
+    ms = both - prep;
+  } else {
+    sel->fn(stream_);  // warm
+    PTTS_HIP(hipEventRecord(e0, stream_));
+    for (int i = 0; i < reps; ++i) sel->fn(stream_);
+    PTTS_HIP(hipEventRecord(e1, stream_));
+    PTTS_HIP(hipEventSynchronize(e1));
+    PTTS_HIP(hipEventElapsedTime(&ms, e0, e1));
+  }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return 1000.0 * ms / reps;

@@ -24,6 +24,8 @@ struct Op {
   std::string name;
   std::function<void(hipStream_t)> fn;
   double flops = 0, bytes = 0;  // algorithmic cost of one launch (GEMM/conv ops)
+  // state an isolated replay of `fn` needs first (time_op), which the step's previous ops provide
+  std::function<void(hipStream_t)> prep = nullptr;
 };
 
 class Engine {
@@ -127,7 +129,8 @@ class Engine {
   // persistent flow-head chain (k_flow_head): hand-off rows, counters, timeout word
   bool head_chain_ = true;
   bool use_head_chain(int B) const;
-  float *hxp_ = nullptr, *hup_ = nullptr;
+  float* hx_ = nullptr;  // flow-head hand-off regions [lsd * 13][roundup(B, 16)][512] (k_flow_head)
+  size_t hx_floats(int B) const { return (size_t)lsd_ * 13 * ((B + 15) / 16 * 16) * FD; }
   float* inw_t_ = nullptr;  // input_linear weight transposed, [32][1024] (k_input_ln)
   int *hctr_ = nullptr, *herr_ = nullptr;
   float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;
@@ -139,6 +142,7 @@ class Engine {
   // (nhb_ = 3 lets front and back drift a step apart instead of running in lockstep).
   static constexpr int NHB = 3;
   int nhb_ = 2;  // buffers in use (2 or 3)
+  bool mimi_attn_fused_ = true;  // Mimi step: RoPE + ring append inside the attention launch
   float* lat_out_[NHB] = {};
   float* eos_out_[NHB] = {};
   FrameFlags* flags_[NHB] = {};

@@ -47,6 +47,10 @@ struct RowReduceArgs {
   long ldm;
   float* Hout;
   long ldh;
+  // side job: fill[0 .. 4 * fill_n4) = 0xFFFFFFFF (re-arms the flow-head hand-off regions in the
+  // launch just ahead of k_flow_head), or nullptr
+  float* fill;
+  long fill_n4;
 };
 struct GemmArgs {
   int mode;    // 0 dense, 1 conv
@@ -140,6 +144,8 @@ void qkv_rope_append(const float* P, int S, const float* dense, int M, int nh, R
 
 // Causal (optionally windowed) softmax attention for rows mapped as above; rows are processed
 // in groups of qg (<= 16) consecutive rows of one slot. O[M][nh*64].
+// Mimi decoder step: RoPE + ring append of the dense QKV rows fused into the 16-row attention
+void attention16_qkv(const float* qkv, int M, int nh, RowMap map, KvStore kv, int window, float* O, hipStream_t s);
 void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O,
                hipStream_t s);
 // One-query-per-row step attention fused with the QKV slab sum, RoPE and KV append (positions
@@ -195,7 +201,9 @@ struct FlowHeadArgs {
   const float *lnw, *lnb, *w0, *b0, *w2, *b2;
   long blk;
   const float *fin_w, *fin_b;
-  float *xp, *up;
+  // hand-off regions: 13 per Euler step (x0, then u_i, x_{i+1} per ResBlock), each
+  // [ceil(B/16) * 16][512], all 0xFFFFFFFF (empty) at launch
+  float* hx;
   int* ctr;
   int* err;
   unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr

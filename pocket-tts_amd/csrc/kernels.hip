@@ -1353,6 +1353,11 @@ __device__ __forceinline__ float4 rr_ln(const RowReduceArgs& a, int m, int n, fl
 template <int SMAX>
 __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   __shared__ float sh[4];
+  if (a.fill) {
+    const long nthr = (long)gridDim.x * gridDim.y * 256;
+    for (long i = ((long)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x; i < a.fill_n4; i += nthr)
+      reinterpret_cast<uint4*>(a.fill)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
   const int m = blockIdx.x;
   const int n0 = blockIdx.y * 1024 + 4 * threadIdx.x;
   const bool ok = n0 < a.N;
@@ -1743,7 +1748,20 @@ __global__ __launch_bounds__(256) void k_attn_decode(const float* __restrict__ Q
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr int A16_WAVES = 8;
 
-template <bool RING>
+// rope.rs:9-16: inv_freq = exp(-ln(max_period) * 2i / head_dim), angle = position * inv_freq
+// (the same expressions as k_qkv_rope, so both paths rotate identically)
+__device__ __forceinline__ void rope_cs(int pos, int i, float& cs, float& sn) {
+  const float freq = expf((float)i * (-logf(10000.0f) * 2.0f / 64.0f));
+  const float ang = (float)pos * freq;
+  cs = cosf(ang);
+  sn = sinf(ang);
+}
+
+// FUSE: Q is the dense QKV projection [M][3d] (Mimi decoder step) instead of rotated queries:
+// the workgroup rotates its 16 rows' q and k (RoPE), appends k and v at their positions in the
+// ring, and attends over the ring after a workgroup barrier (replaces the k_qkv_rope launch; the
+// ring holds window + 16 positions, so the appended rows never evict a key inside the window).
+template <bool RING, bool FUSE = false>
 __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restrict__ Q, int M, int nh, RowMap mp,
                                                           KvStore kv, int window, float* __restrict__ O) {
   __shared__ float s_m[A16_WAVES][16], s_l[A16_WAVES][16];
@@ -1770,7 +1788,36 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
   auto kidx = [&](int kp) { return RING ? (kp & cmask) : kp; };
   // Q^T fragment: query c (rows past nrows reuse the last row; never stored), dims 16G..16G+15
   float qf[16];
-  {
+  if (FUSE) {
+    const int ld = 3 * d;
+    {  // append: thread (row r, rotation pair i) of the 16 x 32 (A16_WAVES = 8: 512 threads)
+      const int r = threadIdx.x >> 5, i = threadIdx.x & 31;
+      if (r < nrows) {
+        const float* pr = Q + (long)(row0 + r) * ld + head * 64 + 2 * i;
+        const float k0 = pr[d], k1 = pr[d + 1], v0 = pr[2 * d], v1 = pr[2 * d + 1];
+        float cs, sn;
+        rope_cs(qpos0 + r, i, cs, sn);
+        float* kb = kv.base + (long)slot * kv.slot_stride + ((long)head * kv.cap + kidx(qpos0 + r)) * 64 + 2 * i;
+        float* vb = kv.base + (long)slot * kv.slot_stride + ((long)(nh + head) * kv.cap + kidx(qpos0 + r)) * 64 + 2 * i;
+        *reinterpret_cast<float2*>(kb) = make_float2(k0 * cs - k1 * sn, k0 * sn + k1 * cs);
+        *reinterpret_cast<float2*>(vb) = make_float2(v0, v1);
+      }
+    }
+    const int rq = min(c, nrows - 1);
+    const float4* q4 = reinterpret_cast<const float4*>(Q + (long)(row0 + rq) * ld + head * 64 + 16 * G);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 t = q4[i];
+      float cs, sn;
+      rope_cs(qpos0 + rq, 8 * G + 2 * i, cs, sn);
+      qf[4 * i] = t.x * cs - t.y * sn;
+      qf[4 * i + 1] = t.x * sn + t.y * cs;
+      rope_cs(qpos0 + rq, 8 * G + 2 * i + 1, cs, sn);
+      qf[4 * i + 2] = t.z * cs - t.w * sn;
+      qf[4 * i + 3] = t.z * sn + t.w * cs;
+    }
+    __syncthreads();  // the appended keys / values are read back by every wave below
+  } else {
     const float4* q4 = reinterpret_cast<const float4*>(Q + (long)(row0 + min(c, nrows - 1)) * d + head * 64 + 16 * G);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2058,6 +2105,15 @@ __global__ __launch_bounds__(256) void k_rope_table(float* tab, int npos) {
 
 void rope_table(float* tab, int npos, hipStream_t s) {
   hipLaunchKernelGGL(k_rope_table, dim3((unsigned)((npos * 32L + 255) / 256)), dim3(256), 0, s, tab, npos);
+}
+
+void attention16_qkv(const float* qkv, int M, int nh, RowMap map, KvStore kv, int window, float* O, hipStream_t s) {
+  if (map.tab != nullptr || map.rps != 16) throw std::runtime_error("attention16_qkv: needs 16 rows per slot");
+  if ((kv.cap & (kv.cap - 1)) != 0 || kv.cap < window + 16)
+    throw std::runtime_error("attention16_qkv: ring too small for the fused append");
+  const dim3 grid((M + 15) / 16, nh);
+  hipLaunchKernelGGL((k_attn16<true, true>), grid, dim3(64 * A16_WAVES), cap_lds(k_attn16<true, true>, g_wg_cap), s,
+                     qkv, M, nh, map, kv, window, O);
 }
 
 void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O, hipStream_t s) {
@@ -2530,16 +2586,21 @@ void resample(const float* x, int n_in, const float* taps, const ResamplePlan& p
 // launches this is 28 GEMM + row-reduce kernels of M = B rows x 512 (each ~1 MB of weights), a
 // chain of launch gaps and HBM round trips. Here a grid of ceil(B/16) row groups x 32 column
 // groups (16 rows x 16 output columns per workgroup, 8 waves splitting K = 512) runs the chain
-// with in-launch hand-offs (cdna_hip_programming.md Guideline 16, sc1 form):
-//   producer: the storing wave writes its 16x16 tile with sc1 (write-through) buffer stores,
-//             s_waitcnt vmcnt(0), then lane 0 adds 1 to the row group's counter (agent scope);
-//   consumer: thread 0 polls the counter with sc1 loads (bounded spin), __syncthreads(), then
-//             every load of handed-off bytes is an sc1 buffer load.
+// with in-launch hand-offs in which the data is its own flag (the tag-free form of the granule
+// hand-off, cdna_hip_programming.md Guideline 16 R2):
+//   every hand-off has its own region, filled with 0xFFFFFFFF (a NaN no arithmetic produces) by
+//   the launch just ahead (k_row_reduce's side job in the adaLN reduce);
+//   producer: the storing wave writes its 16x16 tile with sc1 (write-through) 16-B buffer stores
+//             and moves on (no drain, no counter);
+//   consumer: each wave sweeps its 16 rows x 64 columns with sc1 buffer loads and re-reads every
+//             float4 that still holds the empty pattern (bounded spin) - a 4-byte word is read
+//             either empty or final, so a word that is not empty is the producer's value.
 // Each workgroup keeps its 16x16 tile of the residual stream x in registers for the whole chain;
 // consumers rebuild the full rows (LayerNorm statistics need all 512 columns) from the published
 // copy. Weights, LayerNorm affines and adaLN modulations do not depend on the chain and are
-// loaded before each wait. Counters are zeroed at allocation and re-armed by the last workgroup
-// to finish, so the kernel can be replayed (graphs, timing loops) without a memset node.
+// loaded before each wait. The latent `cur` between Euler steps (lsd > 1) is handed off with a
+// counter (sc1 stores, drain, agent-scope add); counters are zeroed at allocation and re-armed by
+// the last workgroup to finish.
 // v_mfma_f32_16x16x4_f32 fragments as in k_attn16: lane (c = l & 15, G = l >> 4) supplies
 // A[row c][k] and B[k][col c] for k = 64*wave + 16*G + s at step s; D reg g -> row 4G+g, col c.
 // =============================================================================================
@@ -2580,6 +2641,32 @@ __device__ __forceinline__ void fh_wait(int* ctr, int target, int* err, bool& de
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
 }
 __device__ __forceinline__ float4 f4ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ bool fh_empty(float4 v) {
+  return (__float_as_uint(v.x) == ~0u) | (__float_as_uint(v.y) == ~0u) | (__float_as_uint(v.z) == ~0u) |
+         (__float_as_uint(v.w) == ~0u);
+}
+// consumer: this lane's 16 values of a region (byte offset `off`), re-read until none is empty.
+// The loop condition is wave-uniform; a timeout sets *err and stops waiting for the rest of the
+// launch (the frame is poisoned, fetch() reports it).
+__device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, float4 (&v)[4], int* err, bool& dead) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = fh_ld(r, off + 16 * j);
+  unsigned spins = 0;
+  while (!dead) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ok &= !fh_empty(v[j]);
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (fh_empty(v[j])) v[j] = fh_ld(r, off + 16 * j);
+    if (++spins > (1u << 20)) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dead = true;
+    }
+  }
+}
 
 // LayerNorm (eps 1e-6, optional affine) + adaLN modulate (mlp.rs:29-58,135-137) of this lane's
 // 16 values of row c; row statistics combine the 4 lane groups and the 8 waves in a fixed order.
@@ -2621,6 +2708,8 @@ __device__ __forceinline__ void fh_ln(float4 (&v)[4], float (*s_st)[FH_WAVES][16
 }
 // 16 MFMA steps over this lane's k range, then the 8 wave partials summed in wave order; wave 0
 // lane t returns the 16x16 tile's row t/4, columns 4(t%4)..+3
+// (consecutive GEMMs alternate between two s_red buffers: no barrier is needed between wave 0's
+// reads of one and the other waves' writes of the next)
 __device__ __forceinline__ float4 fh_gemm(const float4 (&a)[4], const float4 (&b)[4], float (*s_red)[16][16],
                                           int wave, int c, int G, int lane) {
   floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -2653,7 +2742,7 @@ struct FhOps {
 
 __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   __shared__ float s_st[2][FH_WAVES][16];
-  __shared__ __attribute__((aligned(16))) float s_red[FH_WAVES][16][16];
+  __shared__ __attribute__((aligned(16))) float s_red2[2][FH_WAVES][16][16];
   __shared__ __attribute__((aligned(16))) float s_ln[FH_DEPTH][2][FH_D];  // ResBlock LayerNorm affines
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2668,10 +2757,12 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   const int crow = min(orow, a.B - 1);
   const bool ostore = orow < a.B;
   const bool fin = cg < FH_L / 16;  // column groups 0 and 1 own the 32 latent columns
-  const __amdgpu_buffer_rsrc_t xr = fh_rsrc(a.xp), ur = fh_rsrc(a.up), cr = fh_rsrc(a.cur);
-  int* cx = a.ctr + 4 * rg;  // [0] x published, [1] u published, [2] cur published
-  int *cu = cx + 1, *cc = cx + 2;
-  int nx = 0, nu = 0;
+  const __amdgpu_buffer_rsrc_t hr = fh_rsrc(a.hx), cr = fh_rsrc(a.cur);
+  int* cc = a.ctr + 4 * rg + 2;  // cur published (lsd > 1)
+  const int rstride = RG * 16 * FH_D * 4;  // bytes per hand-off region
+  const int aoff = (arow * FH_D + k0) * 4, ooff = (orow * FH_D + ocol) * 4;  // sweep / store offsets
+  int q = 0;   // next hand-off region
+  int gi = 0;  // GEMMs done (s_red buffer parity)
   bool dead = false;
   float4 xo = make_float4(0.f, 0.f, 0.f, 0.f);  // wave 0: residual tile x[orow][ocol..+3]
   const float4 zero4[4] = {};
@@ -2686,6 +2777,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       reinterpret_cast<float4*>(&s_ln[i][tid < FH_D / 4 ? 0 : 1][0])[tid & (FH_D / 4 - 1)] =
           f4ld(src + 4 * (tid & (FH_D / 4 - 1)));
     }
+  __syncthreads();  // s_ln before the first LayerNorm (the sweeps have no barrier)
   // operand loaders (i: ResBlock, or FH_DEPTH for the FinalLayer)
   auto load_ln_ops = [&](FhOps& o, const float* mods, int i) {
     if (i == FH_DEPTH && !fin) return;
@@ -2733,19 +2825,16 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
         acc[q] = t;
       }
       xo = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      if (ostore) fh_st(xr, (orow * FH_D + ocol) * 4, xo);
-      fh_publish(cx);
+      if (ostore) fh_st(hr, q * rstride + ooff, xo);
     }
-    ++nx;
+    ++q;
 #pragma unroll 1
     for (int i = 0; i < FH_DEPTH; ++i) {
       // ---- h = modulate(LN(x)), u = silu(h W0^T + b0)
       float4 v[4];
       FH_STAMP();
-      fh_wait(cx, 32 * nx, a.err, dead);
+      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
       FH_STAMP();
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = fh_ld(xr, (arow * FH_D + k0 + 4 * j) * 4);
       float4 lw[4], lb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -2754,43 +2843,37 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       }
       fh_ln(v, s_st, wave, c, G, lw, lb, true, p0.sc, p0.sf);
       FH_STAMP();
-      float4 r = fh_gemm(v, p0.w, s_red, wave, c, G, lane);
+      float4 r = fh_gemm(v, p0.w, s_red2[gi++ & 1], wave, c, G, lane);
       FH_STAMP();
       if (wave != 0) load_ln_ops(p0, mods, i + 1);
       if (wave == 0) {
         const float4 bb = p0.e0;
         const float4 u = make_float4(silu(r.x + bb.x), silu(r.y + bb.y), silu(r.z + bb.z), silu(r.w + bb.w));
-        if (ostore) fh_st(ur, (orow * FH_D + ocol) * 4, u);
-        fh_publish(cu);
+        if (ostore) fh_st(hr, q * rstride + ooff, u);
         load_ln_ops(p0, mods, i + 1);
       }
       FH_STAMP();
-      ++nu;
+      ++q;
       // ---- x += gate * (u W2^T + b2)
-      fh_wait(cu, 32 * nu, a.err, dead);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = fh_ld(ur, (arow * FH_D + k0 + 4 * j) * 4);
-      r = fh_gemm(v, p2.w, s_red, wave, c, G, lane);
+      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
+      r = fh_gemm(v, p2.w, s_red2[gi++ & 1], wave, c, G, lane);
       if (wave != 0 && i + 1 < FH_DEPTH) load_mlp2_ops(p2, mods, i + 1);
       if (wave == 0) {
         xo = f4add(xo, f4mul(p2.e0, f4add(r, p2.e1)));
-        if (ostore) fh_st(xr, (orow * FH_D + ocol) * 4, xo);
-        fh_publish(cx);
+        if (ostore) fh_st(hr, q * rstride + ooff, xo);
         if (i + 1 < FH_DEPTH) load_mlp2_ops(p2, mods, i + 1);
       }
-      ++nx;
+      ++q;
     }
     // ---- FinalLayer (mlp.rs:182-213): modulate(LN_noaffine(x)) W_f^T + b_f, Euler x += v / N
     const float* nmods = mods + (long)a.B * a.ldm;  // next Euler step's modulations
     const bool more = st + 1 < a.lsd;
     if (fin) {
       float4 v[4];
-      fh_wait(cx, 32 * nx, a.err, dead);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = fh_ld(xr, (arow * FH_D + k0 + 4 * j) * 4);
+      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
       if (wave != 0 && more) load_mlp2_ops(p2, nmods, 0);
       fh_ln(v, s_st, wave, c, G, zero4, zero4, false, p0.sc, p0.sf);
-      const float4 r = fh_gemm(v, p0.w, s_red, wave, c, G, lane);
+      const float4 r = fh_gemm(v, p0.w, s_red2[gi++ & 1], wave, c, G, lane);
       if (wave != 0 && more) load_ln_ops(p0, nmods, 0);
       if (wave == 0) {
         const int off = (crow * FH_L + ocol) * 4;

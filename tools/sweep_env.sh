@@ -8,14 +8,15 @@ mkdir -p gpurun_out
 REPS=${REPS:-1}
 for r in $(seq 1 "$REPS"); do
   for v in $VALUES; do
+    t=$(echo "$v" | tr '/' '_')
     if [ "$v" = "-" ]; then
       timeout -k 10 200 python bench.py --no-cpu-baseline --no-quant-variant --no-op-times --no-latency \
-          ${BENCH_ARGS:-} > gpurun_out/sweep_$v.log 2>&1 || { echo "$VAR unset failed"; tail -5 gpurun_out/sweep_$v.log; exit 1; }
+          ${BENCH_ARGS:-} > gpurun_out/sweep_$t.log 2>&1 || { echo "$VAR unset failed"; tail -5 gpurun_out/sweep_$t.log; exit 1; }
     else
       env "$VAR=$v" timeout -k 10 200 python bench.py --no-cpu-baseline --no-quant-variant --no-op-times --no-latency \
-          ${BENCH_ARGS:-} > gpurun_out/sweep_$v.log 2>&1 || { echo "$VAR=$v failed"; tail -5 gpurun_out/sweep_$v.log; exit 1; }
+          ${BENCH_ARGS:-} > gpurun_out/sweep_$t.log 2>&1 || { echo "$VAR=$v failed"; tail -5 gpurun_out/sweep_$t.log; exit 1; }
     fi
-    python - "$VAR=$v" gpurun_out/sweep_$v.log <<'PY'
+    python - "$VAR=$v" gpurun_out/sweep_$t.log <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 print(sys.argv[1], "value", d["value"], "steady_ms", d["steady_ms_per_step"], flush=True)
