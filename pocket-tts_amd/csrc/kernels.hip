@@ -2642,8 +2642,8 @@ __device__ __forceinline__ void fh_wait(int* ctr, int target, int* err, bool& de
 }
 __device__ __forceinline__ float4 f4ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ bool fh_empty(float4 v) {
-  return (__float_as_uint(v.x) == ~0u) | (__float_as_uint(v.y) == ~0u) | (__float_as_uint(v.z) == ~0u) |
-         (__float_as_uint(v.w) == ~0u);
+  return ((int)(__float_as_uint(v.x) == ~0u) | (int)(__float_as_uint(v.y) == ~0u) |
+          (int)(__float_as_uint(v.z) == ~0u) | (int)(__float_as_uint(v.w) == ~0u)) != 0;
 }
 // consumer: this lane's 16 values of a region (byte offset `off`), re-read until none is empty.
 // The loop condition is wave-uniform; a timeout sets *err and stops waiting for the rest of the

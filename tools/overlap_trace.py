@@ -2,7 +2,7 @@
 """Pipelined-step timeline from a rocprofv3 --kernel-trace of bench.py (pipelined engine).
 
 Splits the engine kernels by queue (front graph on the engine stream, back graph on the second
-stream), finds the steady-state steps (front windows ending at k_front_commit, back windows
+stream), finds the steady-state steps (front windows ending at k_front_commit (or k_flow_head when the commit runs inside it), back windows
 ending at k_commit), and reports per-part spans and per-op durations overlapped, next to the
 isolated HIP-event times of bench_ops.json. Usage:
   overlap_trace.py <run_kernel_trace.csv> <bench_ops.json>"""
@@ -27,7 +27,8 @@ def main(trace, ops_path):
     res = {}
     for q, rs in by_q.items():
         names = [r["Kernel_Name"] for r in rs]
-        for part, seq, last in (("front", front, "k_front_commit"), ("back", back, "k_commit")):
+        fend = "k_front_commit" if front[-1] == "front_commit" else "k_flow_head"
+        for part, seq, last in (("front", front, fend), ("back", back, "k_commit")):
             n = len(seq)
             wins = [i + 1 - n for i, nm in enumerate(names) if last in nm and i + 1 >= n]
             if not wins:

@@ -30,8 +30,9 @@ def main(trace, ops_path, out):
     ops = json.load(open(ops_path))
     plan = ops["plan"]
     alone = {o["op"]: o["avg_us"] for o in ops["ops"]}
-    nf = next(i for i, n in enumerate(plan) if n == "front_commit") + 1
-    parts = {"front": (plan[:nf], "k_front_commit"), "back": (plan[nf:], "k_commit")}
+    nf = plan.index("mimi.quant_upsample")  # the front part ends in front_commit or in the chain
+    fend = "k_front_commit" if plan[nf - 1] == "front_commit" else "k_flow_head"
+    parts = {"front": (plan[:nf], fend), "back": (plan[nf:], "k_commit")}
     rows = list(csv.DictReader(open(trace)))
     qkey = "Queue_Id" if "Queue_Id" in rows[0] else "Stream_Id"
     byq = collections.defaultdict(list)
