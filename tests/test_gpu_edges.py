@@ -213,3 +213,30 @@ def test_head_chain_needs_coresident_workgroups(gpu_engine):
     grid fits on the device at once (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs); the
     8-slot engine's 32-workgroup grid always fits on an MI355X."""
     assert "head.chain" in gpu_engine.plan_ops(8)
+
+
+def test_nan_latent_propagates_without_stalling_the_head_chain(gpu_engine, oracle):
+    """A NaN backbone input (set_latent) makes that row's frame NaN, as in the reference, and does
+    not stall the persistent flow-head launch: its hand-offs use an empty pattern that is itself a
+    NaN, and every stored NaN is canonicalised. The other row's frame is unaffected."""
+    import time
+
+    d = load_golden("e2e_lsd1.safetensors")
+    prompt = d["prompt"][:6]
+    v = gpu_engine.voice_from_prompt(prompt)
+    ids = np.array([260, 2994, 262], np.int32)
+    for slot in (0, 1):
+        gpu_engine.open(slot, v, ids, _params(max_frames=2))
+    gpu_engine.step(2)  # first frame of both rows
+    gpu_engine.set_latent(1, np.full(32, np.nan, np.float32))
+    t0 = time.perf_counter()
+    r = gpu_engine.step(2)
+    assert time.perf_counter() - t0 < 1.0  # a timed-out hand-off wait takes seconds
+    assert np.isnan(r.latents[1]).all() and np.isnan(r.pcm[1]).all()
+    s = oracle.new_state(256)
+    s.prefill(prompt)
+    s.prefill_tokens(ids)
+    lat = s.step(None)["latent"]
+    ref = s.step(lat)
+    np.testing.assert_allclose(r.latents[0], ref["latent"], atol=LAT_TOL)
+    assert pcm_err(r.pcm[0] - ref["pcm"]) <= PCM_TOL
