@@ -27,6 +27,27 @@ int pick_splits(int M, int N, int K) {
 }
 }  // namespace
 
+// Tuning override of an op's tile layout / split-K count (tools/back_tune.py):
+// PTTS_OVR="name=L[:S],...", read at every plan build.
+static void tile_override(const std::string& name, int& layout, int& ksplit) {
+  const char* e = getenv("PTTS_OVR");
+  if (!e) return;
+  const std::string s(e);
+  size_t p = 0;
+  while (p < s.size()) {
+    size_t q = s.find(',', p);
+    if (q == std::string::npos) q = s.size();
+    const std::string item = s.substr(p, q - p);
+    p = q + 1;
+    const size_t eq = item.find('=');
+    if (eq == std::string::npos || item.compare(0, eq, name) != 0 || eq != name.size()) continue;
+    const std::string v = item.substr(eq + 1);
+    const size_t c = v.find(':');
+    layout = atoi(v.substr(0, c).c_str());
+    if (c != std::string::npos) ksplit = atoi(v.substr(c + 1).c_str());
+  }
+}
+
 float* Engine::dalloc(size_t n) {
   void* p = nullptr;
   PTTS_HIP(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(float)));
@@ -442,7 +463,9 @@ void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowRed
 void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,
                       int K, const float* bias, int act, const float* rscale, const float* R, float* Y, int layout) {
   PTTS_REQUIRE(K % 32 == 0, "GEMM K must be a multiple of 32");
-  PTTS_REQUIRE(layout != 15 || K % 64 == 0, "layout 15 needs K % 64 == 0");
+  int ks = 1;
+  tile_override(name, layout, ks);
+  PTTS_REQUIRE(!(layout == 8 || layout == 15 || layout == 16) || K % 64 == 0, "BK 64 tiles need K % 64 == 0");
   GemmArgs a{};
   a.mode = 0;
   a.layout = layout;
@@ -470,6 +493,8 @@ void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float*
                      const float* bias, const float* R, float* Y, int T_out, int tstride, int layout, int elu_out,
                      float* Y2, int ksplit) {
   PTTS_REQUIRE(cin % 32 == 0, "conv cin must be a multiple of 32");
+  tile_override(name, layout, ksplit);
+  PTTS_REQUIRE(!(layout == 8 || layout == 15 || layout == 16) || cin % 64 == 0, "BK 64 tiles need cin % 64 == 0");
   // ksplit > 1: single-phase conv on an LDS-DMA tile, K split into ksplit partial slabs in the
   // back part's slab buffer; the caller adds the row-reduce epilogue
   PTTS_REQUIRE(ksplit == 1 || (phases == 1 && layout >= 6 && layout != 9 && layout != 10 && layout < 17),
@@ -794,11 +819,15 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     const Layout::TL& t = L_.mdec[l];
     const std::string p = "mimi.l" + std::to_string(l);
     KvStore kv{ring_ + (long)l * ring_layer_, ring_slot_, RING};
-    // fat GEMMs (B*16 rows): LDS-DMA tiles once there are enough rows to fill the chip
+    // fat GEMMs (B*16 rows): LDS-DMA tiles once there are enough rows to fill the chip. BK 64,
+    // 3 buffers alone on the chip (tools/gemm_bench.hip); BK 32, 2 buffers in pipelined stepping,
+    // whose lighter workgroups leave more room to the concurrent front part (qkv + ff1 at 6:
+    // steady step 0.6661 -> 0.6587 ms, tools/sweep_env.sh over PTTS_OVR)
     const bool fat = MR >= 256;
-    {  // QKV: one pass, 64x64 LDS-DMA BK 64 tiles once there are enough rows (tools/gemm_bench.hip c2.mimi.qkv)
+    const int fat_layout = pipeline_ ? 6 : 15;
+    {  // QKV: one pass, 64x64 LDS-DMA tiles once there are enough rows (tools/gemm_bench.hip c2.mimi.qkv)
       dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_,
-               fat ? 15 : 0);
+               fat ? fat_layout : 0);
       const float* qkv = mqkv_;
       float* Q = mq_;
       float* O = mo_;
@@ -816,7 +845,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       ops.push_back({p + ".ln2", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
     }
     dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
-             fat ? 15 : 0);
+             fat ? fat_layout : 0);
     if (fat) {  // K = 2048: 64x64 LDS-DMA tiles, 4-way split-K; LayerScale + residual in the reduce
       const int S = 4;
       GemmArgs a{};
@@ -871,12 +900,20 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   // 2-tap conv over rows (x[q-1], x[q]) whose output row q is the r time rows q*r .. q*r+r-1 of
   // the channels-last output, N = r * Cout (packed [r][Cout][2][Cin] = [r*Cout][2*Cin]).
   const bool big = B >= 16;
-  if (big) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the reduce
+  // Tiles: the tools/gemm_bench.hip choices (each launch alone on the chip, B = 32), except where
+  // the pipelined step (tools/sweep_env.sh over PTTS_OVR, steady step time) prefers lighter
+  // workgroups beside the concurrent front part: the register-blocked res_conv3 tiles of stages
+  // 0 and 1 (k_gemm_rb, 2x2 accumulators per wave) give way to the 64x64 LDS-DMA tile, steady
+  // step 0.6748 -> 0.6639 ms. Tiles that are faster alone under the per-CU cap (tools/
+  // back_tune.py: 32 us less back time in all) each made the pipelined step slower.
+  int l_c0 = 6, s_c0 = 8;  // conv0 tile / split-K (PTTS_OVR may change them)
+  tile_override("seanet.conv0", l_c0, s_c0);
+  if (big && s_c0 > 1) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the reduce
     conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
-            nullptr, 16, 1, 6, 0, nullptr, 8);
+            nullptr, 16, 1, l_c0, 0, nullptr, s_c0);
     RowReduceArgs r{};
     r.P = mpartial_;
-    r.S = 8;
+    r.S = s_c0;
     r.M = B * 16;
     r.N = 512;
     r.bias = W(L_.dc0_b);
@@ -886,23 +923,25 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     ops.push_back({"seanet.conv0_reduce", [r](hipStream_t s) { row_reduce(r, s); }});
   } else {
     conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, W(L_.dc0_b), nullptr,
-            a0_, 16, 1, 0, 1);
+            a0_, 16, 1, big ? l_c0 : 0, 1);
   }
   const float* cin_buf = a0_;
   int T = 16, ch = 512;
   for (int i = 0; i < 3; ++i) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
-    // per-stage tiles (tools/gemm_bench.hip, rb.* cases, B = 32)
+    // per-stage tiles (tools/gemm_bench.hip, rb.* cases, B = 32; see above for pipelined)
     const int l_tr = big ? (i == 0 ? 20 : (i == 1 ? 13 : 22)) : 0;
-    const int l_r3 = big ? (i == 0 ? 18 : (i == 1 ? 20 : 14)) : 0;
+    const int l_r3 = !big ? 0 : i == 2 ? 14 : pipeline_ ? 6 : (i == 0 ? 18 : 20);
     const int l_r1 = big ? 6 : 0;
-    if (big && i == 0) {  // M = 16 B rows only: 4-way split-K fills the chip; bias + dual store in the reduce
+    int l_t0 = 6, s_t0 = i == 0 ? 4 : 1;  // split-K of the first transposed conv (PTTS_OVR may change it)
+    if (i == 0) tile_override(p + ".convtr", l_t0, s_t0);
+    if (big && i == 0 && s_t0 > 1) {  // M = 16 B rows only: 4-way split-K fills the chip; bias + dual store in the reduce
       conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1], 1, 1, 0, W(L_.dtr_w[0]), r * (ch / 2), 2, 1, nullptr,
-              nullptr, nullptr, T, 1, 6, 0, nullptr, 4);
+              nullptr, nullptr, T, 1, l_t0, 0, nullptr, s_t0);
       RowReduceArgs rr{};
       rr.P = mpartial_;
-      rr.S = 4;
+      rr.S = s_t0;
       rr.M = B * T;
       rr.N = r * (ch / 2);
       rr.bias = trb_[0];
@@ -1084,9 +1123,15 @@ double Engine::time_op(int B, const std::string& name, int reps) {
   PTTS_HIP(hipSetDevice(dev_));
   std::vector<Op> ops = build_step(B);
   const Op* sel = nullptr;
-  for (const Op& op : ops)
-    if (op.name == name) sel = &op;
+  bool back = false, in_back = false;
+  for (const Op& op : ops) {
+    in_back = in_back || op.name == "mimi.quant_upsample";
+    if (op.name == name) sel = &op, back = in_back;
+  }
   PTTS_REQUIRE(sel != nullptr, "no op named " + name + " in the step plan");
+  // PTTS_TIME_CAP: time back-part ops with the per-CU cap of pipelined stepping
+  const bool capped = back && pipeline_ && getenv("PTTS_TIME_CAP");
+  set_wg_cap(capped ? back_cap_ : 0);
   hipEvent_t e0, e1;
   PTTS_HIP(hipEventCreate(&e0));
   PTTS_HIP(hipEventCreate(&e1));
@@ -1119,6 +1164,7 @@ double Engine::time_op(int B, const std::string& name, int reps) {
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  set_wg_cap(0);
   return 1000.0 * ms / reps;
 }
 
@@ -1175,21 +1221,26 @@ void Engine::overlap_probe(int B, int reps, double* us) {
     PTTS_HIP(hipEventElapsedTime(&ms, e0, e1));
     return 1000.0 * ms / reps;
   };
-  us[0] = timed(0);
-  us[1] = timed(1);
-  us[2] = timed(2);
-  us[3] = timed(3);
+  // PTTS_PROBE_MODES: digits of the measurements to run (default all: "0123456")
+  const std::string modes = getenv("PTTS_PROBE_MODES") ? getenv("PTTS_PROBE_MODES") : "0123456";
+  auto want = [&](int m) { return modes.find((char)('0' + m)) != std::string::npos; };
+  for (int m = 0; m < 7; ++m) us[m] = -1.0;
+  for (int m = 0; m < 4; ++m)
+    if (want(m)) us[m] = timed(m);
   // us[4..6]: front graph || back part launched op by op on a stream whose CU mask keeps
   // 8/8, 6/8, 4/8 of the CUs (graph launches do not honour a stream's CU mask)
   for (int v = 0; v < 3; ++v) {
+    if (!want(4 + v)) continue;
     const int keep = 8 - 2 * v;
     std::vector<uint32_t> mask(8, 0u);  // 256 CUs
     for (int cu = 0; cu < 256; ++cu)
       if ((cu % 8) < keep) mask[cu / 32] |= 1u << (cu % 32);
     hipStream_t sm = nullptr;
     PTTS_HIP(hipExtStreamCreateWithCUMask(&sm, (uint32_t)mask.size(), mask.data()));
-    auto back_eager = [&]() {
+    auto back_eager = [&]() {  // capped as in pipelined stepping: the persistent flow-head launch of
+      set_wg_cap(back_cap_);    // the concurrent front graph needs room for all its workgroups
       for (size_t i = cut; i < ops.size(); ++i) ops[i].fn(sm);
+      set_wg_cap(0);
     };
     for (int w = 0; w < 2; ++w) {
       PTTS_HIP(hipGraphLaunch(ge[0], stream_));
