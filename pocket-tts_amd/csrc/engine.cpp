@@ -847,10 +847,13 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
              fat ? fat_layout : 0);
     if (fat) {  // K = 2048: 64x64 LDS-DMA tiles, 4-way split-K; LayerScale + residual in the reduce
-      const int S = 4;
+      int S = 4, lay = 6;
+      tile_override(p + ".ff2_gemm", lay, S);
+      PTTS_REQUIRE(S >= 1 && S <= 16 && (lay == 6 || lay == 7 || lay == 11 || lay == 12 || lay == 13 || lay == 14),
+                   "mimi ff2: split-K 1..16 on a single-phase LDS-DMA tile");
       GemmArgs a{};
       a.mode = 0;
-      a.layout = 6;
+      a.layout = lay;
       a.M = MR;
       a.N = MD;
       a.K = MFF;
@@ -861,7 +864,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       a.S = S;
       a.partial = mpartial_;
       PTTS_REQUIRE((size_t)S * MR * MD <= mpcap_, "back split-K slab buffer too small");
-      ops.push_back({p + ".ff2_gemm", [a](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * MD * MFF,
+      ops.push_back({p + ".ff2_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * MD * MFF,
                      4.0 * ((double)MD * MFF + (double)MR * MFF + 2.0 * MR * MD)});
       RowReduceArgs r{};
       r.P = mpartial_;
