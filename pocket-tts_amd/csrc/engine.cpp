@@ -254,10 +254,53 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
   PTTS_HIP(hipMemcpy(blob_, host, n_bytes, hipMemcpyHostToDevice));
 }
 
+// The FlowLM step matrices as fragment-packed copies for the register-resident split-K GEMM
+// (PTTS_GEMV: bit mask of the matrices that use it, 1 qkv, 2 out, 4 linear1, 8 linear2): out on
+// 32x32 tiles with 8 K slices of 128 (4 waves splitting each), linear2 on 32x32 tiles with 16
+// slices of 256. Alone on the chip every matrix is faster this way (qkv 8.1 -> 4.9 us, out 4.5
+// -> 3.2, linear1 8.1 -> 5.2, linear2 7.9 -> 5.3); in the pipelined step only out + linear2 pay
+// (steady step 0.6595 -> 0.6326 ms, medians of 3), the qkv / linear1 versions on any tile
+// (PTTS_GEMV_WIDE) slow the concurrent back part more than they gain. Default mask: 2 | 8.
+void Engine::derive_gemv() {
+  const int mask = getenv("PTTS_GEMV") ? atoi(getenv("PTTS_GEMV")) : 10;
+  struct M {
+    const float* w;
+    int N, K, bit;
+    GemvShape g;
+  };
+  std::vector<M> mats;
+  GemvShape wide{4, 128};  // qkv / linear1 tile (PTTS_GEMV_WIDE="wn,kw")
+  if (getenv("PTTS_GEMV_WIDE")) sscanf(getenv("PTTS_GEMV_WIDE"), "%d,%d", &wide.wn, &wide.kw);
+  for (int l = 0; l < NL; ++l) {
+    const Layout::TL& t = L_.fl[l];
+    mats.push_back({W(t.in_proj), 3 * D, D, 1, wide});
+    mats.push_back({W(t.out_proj), D, D, 2, GemvShape{1, 32}});
+    mats.push_back({W(t.l1), FF, D, 4, wide});
+    mats.push_back({W(t.l2), D, FF, 8, GemvShape{1, 64}});
+  }
+  size_t total = 0;
+  for (const M& m : mats)
+    if ((mask & m.bit) && gemv_supported(m.g, m.N, m.K)) total += (size_t)m.N * m.K;
+  if (!total) return;
+  void* p = nullptr;
+  PTTS_HIP(hipMalloc(&p, sizeof(float) * total));  // every element is written by the packing
+  allocs_.push_back(p);
+  float* dst = (float*)p;
+  for (const M& m : mats) {
+    if (!(mask & m.bit) || !gemv_supported(m.g, m.N, m.K)) continue;
+    pack_gemv(m.w, m.N, m.K, m.g, dst, stream_);
+    gvmap_[m.w] = {dst, m.g};
+    dst += (size_t)m.N * m.K;
+  }
+  PTTS_HIP(hipGetLastError());
+  PTTS_HIP(hipStreamSynchronize(stream_));
+}
+
 void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   if (fp8_ && f8map_.empty()) derive_fp8();
+  if (wq_ == QUANT_NONE && !fp8_ && gvmap_.empty()) derive_gemv();
   if (!inw_t_) {  // every element is written by the transpose below: no (null-stream) memset
     void* p = nullptr;
     PTTS_HIP(hipMalloc(&p, sizeof(float) * LDIM * D));
@@ -384,6 +427,20 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   // large matrices (qkv, ff1, ff2, adaLN; >= 2M weights): below that the launch is latency-bound
   // and the f32 copy of the same values is as fast (tools/w8_probe.py). Prefill passes
   // (M >= 256) keep the f32 copy too: they are MFMA-bound.
+  auto gv = gvmap_.find(Wt);
+  if (gv != gvmap_.end() && M <= 32) {  // register-resident weights (derive_gemv)
+    const GemvShape g = gv->second.second;
+    const float* P = gv->second.first;
+    const int Sg = K / g.ks();
+    PTTS_REQUIRE((size_t)Sg * M * N <= pcap_, "split-K partial buffer too small");
+    float* part = partial_;
+    ops.push_back({name, [=](hipStream_t s) { gemv_splitk(X, ldx, M, N, K, P, g, part, s); }, 2.0 * M * N * K,
+                   4.0 * N * K + 4.0 * ((double)M * K + (double)Sg * M * N)});
+    last_split_ = GemmArgs{};
+    last_split_op_ = (size_t)-1;  // never folded into a reduce (push_rr)
+    *S_out = Sg;
+    return;
+  }
   auto f8 = f8map_.find(Wt);
   const bool wf8 = f8 != f8map_.end() && M <= 64;
   if (wf8) {  // fp8 W8A8 (k_gemm_fp8): 32x64 tiles, >= 256 workgroups, K slice <= FP8_KSLICE_MAX
@@ -401,6 +458,7 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
     S = 1;
     while (S < 16 && tiles * S < 256 && (K / 32) / (2 * S) >= 4) S *= 2;
   }
+  if (!w8 && !wf8) tile_override(name, layout, S);
   while (S > 1 && (size_t)S * M * N > pcap_) --S;
   PTTS_REQUIRE((size_t)S * M * N <= pcap_, "split-K partial buffer too small");
   GemmArgs a{};

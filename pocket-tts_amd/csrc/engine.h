@@ -98,6 +98,9 @@ class Engine {
   int fp8_ = 0;  // ptts_engine_config.fp8_gemm
   // e4m3 code matrices of the large FlowLM step GEMMs: f32 weight pointer -> (codes, row scales)
   std::map<const float*, std::pair<const uint8_t*, const float*>> f8map_;
+  // fragment-packed copies of the f32 FlowLM step matrices for gemv_splitk: weight -> (copy, shape)
+  std::map<const float*, std::pair<const float*, GemvShape>> gvmap_;
+  void derive_gemv();
   bool own_blob_ = true, ready_ = false;
   hipStream_t stream_ = nullptr;
   Layout L_{};

@@ -112,6 +112,21 @@ struct GemmArgs {
 };
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
 
+// Skinny split-K GEMM (M <= 32 rows, the FlowLM step) with register-resident weights: the
+// workgroup tile is 32 rows x 32*wn columns over a K slice of ks = kw * (4 / wn); wave w takes
+// 32 columns (w % wn) and kw of the slice's k ((w / wn) * kw ..). Its weight fragment (kw * 32
+// floats) comes from a copy packed in fragment order (pack_gemv: every load instruction reads 1
+// contiguous KB), all of it requested at the start; the slice of X is staged in LDS. Output:
+// partial slab z = blockIdx.y of P [S][M][N], S = K / ks.
+struct GemvShape {
+  int wn, kw;
+  int ks() const { return kw * (4 / wn); }
+};
+bool gemv_supported(GemvShape g, int N, int K);
+void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStream_t s);
+void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
+                 hipStream_t s);
+
 // int8 codes of a quantized weight matrix: q[n][k] = W[n][k] / s[n] (exact integers in
 // [-127, 127] for a blob packed by the quantizer); rows with s[n] == 0 get code 0. Any element
 // with float(q) * s[n] != W[n][k] (bitwise) increments *bad.

@@ -1305,6 +1305,131 @@ void gemm(const GemmArgs& a, int grid_z, hipStream_t s) {
 }
 
 // =============================================================================================
+// Skinny split-K GEMM with register-resident weights (see kernels.h). Packed layout, per
+// (tile t, slice z, wave w): NV = kw / 8 groups of 64 float4, group j lane l = W[n][k..k+3] with
+//   n = t * 32 * WN + (w % WN) * 32 + (l & 31),  k = z * ks + (w / WN) * kw + (l >> 5) * kw / 2 + 4 j,
+// so lane l holds the B operand of v_mfma_f32_32x32x2f32 for the steps s = 0 .. kw/2 - 1 of its
+// wave, k = base + (l >> 5) * kw / 2 + s (the two lane halves take the two k of a step from the two
+// halves of the wave's k range: the MFMA K order is a permutation of the sum). A (X's slice) is
+// read from LDS in the same order: lane l, row l & 31, the same k.
+// =============================================================================================
+__global__ void k_pack_gemv(const float* __restrict__ W, int N, int K, int wn, int kw, float* __restrict__ P) {
+  const long i4 = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index into P
+  const long total4 = (long)N * K / 4;
+  if (i4 >= total4) return;
+  const int nv = kw / 8, ks = kw * (4 / wn), S = K / ks;
+  const int lane = (int)(i4 & 63);
+  long r = i4 >> 6;
+  const int j = (int)(r % nv);
+  r /= nv;
+  const int w = (int)(r & 3);
+  r >>= 2;
+  const int z = (int)(r % S);
+  const int t = (int)(r / S);
+  const int n = t * 32 * wn + (w % wn) * 32 + (lane & 31);
+  const int k = z * ks + (w / wn) * kw + (lane >> 5) * (kw / 2) + 4 * j;
+  reinterpret_cast<float4*>(P)[i4] = *reinterpret_cast<const float4*>(W + (long)n * K + k);
+}
+
+template <int WN, int KW>
+__global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long ldx, int M, int N,
+                                              const float* __restrict__ P, float* __restrict__ partial) {
+  constexpr int WK = 4 / WN, KS = KW * WK, NV = KW / 8, LDA = KS + 4;  // +4: conflict-free b128 rows
+  __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
+  __shared__ __attribute__((aligned(16))) float red[WK > 1 ? 4 * 16 * 64 : 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t = blockIdx.x, z = blockIdx.y, S = gridDim.y;
+  // X's slice first (the LDS fill waits only for these loads), then every weight load
+  constexpr int AV = 32 * KS / 4 / 256;  // float4 of X per thread
+  float4 av[AV];
+#pragma unroll
+  for (int i = 0; i < AV; ++i) {
+    const int e = tid + 256 * i, row = e / (KS / 4), c4 = e % (KS / 4);
+    av[i] = row < M ? *reinterpret_cast<const float4*>(X + (long)row * ldx + (long)z * KS + 4 * c4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* wp = reinterpret_cast<const f4v*>(P) + (((long)t * S + z) * 4 + wave) * NV * 64 + lane;
+  f4v w[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) w[j] = __builtin_nontemporal_load(wp + j * 64);  // once-read weights
+#pragma unroll
+  for (int i = 0; i < AV; ++i) {
+    const int e = tid + 256 * i, row = e / (KS / 4), c4 = e % (KS / 4);
+    *reinterpret_cast<float4*>(&sA[row * LDA + 4 * c4]) = av[i];
+  }
+  __syncthreads();
+  const int m = lane & 31, h = lane >> 5, wn = wave % WN, wk = wave / WN;
+  const float* ar = &sA[m * LDA + wk * KW + h * (KW / 2)];
+  floatx16 acc;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float4 a = *reinterpret_cast<const float4*>(ar + 4 * j);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, w[j].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, w[j].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, w[j].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, w[j].w, acc, 0, 0, 0);
+  }
+  const int n = t * 32 * WN + wn * 32 + m;
+  float* out = partial + (long)z * M * N;
+  if (WK == 1) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
+      if (row < M) out[(long)row * N + n] = acc[g];
+    }
+    return;
+  }
+  // WK > 1: the WK waves of column block c (waves c, c + WN, ..) hold partials over their k
+  // ranges; the 16 * WN (block, register) outputs are dealt 4 * WN per wave and summed in k order
+#pragma unroll
+  for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[g];
+  __syncthreads();
+#pragma unroll
+  for (int ff = 0; ff < 4 * WN; ++ff) {
+    const int f = wave * 4 * WN + ff, c = f / 16, g = f % 16;
+    float v = red[(c * 16 + g) * 64 + lane];
+#pragma unroll
+    for (int kk = 1; kk < WK; ++kk) v += red[((kk * WN + c) * 16 + g) * 64 + lane];
+    const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
+    if (row < M) out[(long)row * N + t * 32 * WN + c * 32 + m] = v;
+  }
+}
+
+bool gemv_supported(GemvShape g, int N, int K) {
+  const bool shape = (g.wn == 4 && g.kw == 128) || (g.wn == 1 && g.kw == 32) || (g.wn == 1 && g.kw == 64) ||
+                     (g.wn == 2 && g.kw == 64);
+  return shape && N % (32 * g.wn) == 0 && K % g.ks() == 0 && K / g.ks() <= 16;
+}
+
+void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStream_t s) {
+  if (!gemv_supported(g, N, K)) throw std::runtime_error("pack_gemv: unsupported shape");
+  const long total4 = (long)N * K / 4;
+  hipLaunchKernelGGL(k_pack_gemv, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, W, N, K, g.wn, g.kw,
+                     packed);
+}
+
+void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
+                 hipStream_t s) {
+  if (M < 1 || M > 32 || !gemv_supported(g, N, K)) throw std::runtime_error("gemv_splitk: unsupported shape");
+  const dim3 grid((unsigned)(N / (32 * g.wn)), (unsigned)(K / g.ks()));
+#define PTTS_GEMV(WN_, KW_)                                                                              \
+  if (g.wn == WN_ && g.kw == KW_) {                                                                      \
+    hipLaunchKernelGGL((k_gemv<WN_, KW_>), grid, dim3(256), cap_lds(k_gemv<WN_, KW_>, g_wg_cap), s, X, ldx, M, N, \
+                       packed, partial);                                                                 \
+    return;                                                                                              \
+  }
+  PTTS_GEMV(4, 128)
+  PTTS_GEMV(2, 64)
+  PTTS_GEMV(1, 64)
+  PTTS_GEMV(1, 32)
+#undef PTTS_GEMV
+}
+
+// =============================================================================================
 // Row reduce + epilogue + LayerNorm/modulate. One workgroup per row.
 // =============================================================================================
 __device__ __forceinline__ float block_sum(float v, float* sh) {
