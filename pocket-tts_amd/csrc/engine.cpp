@@ -255,14 +255,15 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
 }
 
 // The FlowLM step matrices as fragment-packed copies for the register-resident split-K GEMM
-// (PTTS_GEMV: bit mask of the matrices that use it, 1 qkv, 2 out, 4 linear1, 8 linear2): out on
+// (PTTS_GEMV: bit mask of the matrices that use it, 1 qkv, 2 out, 4 linear1, 8 linear2, 16 the
+// flow head's adaLN matrix, M = lsd * B rows): out on
 // 32x32 tiles with 8 K slices of 128 (4 waves splitting each), linear2 on 32x32 tiles with 16
 // slices of 256. Alone on the chip every matrix is faster this way (qkv 8.1 -> 4.9 us, out 4.5
 // -> 3.2, linear1 8.1 -> 5.2, linear2 7.9 -> 5.3); in the pipelined step only out + linear2 pay
 // (steady step 0.6595 -> 0.6326 ms, medians of 3), the qkv / linear1 versions on any tile
-// (PTTS_GEMV_WIDE) slow the concurrent back part more than they gain. Default mask: 2 | 8.
+// (PTTS_GEMV_WIDE) slow the concurrent back part more than they gain. Default mask: 2 | 8 | 16.
 void Engine::derive_gemv() {
-  const int mask = getenv("PTTS_GEMV") ? atoi(getenv("PTTS_GEMV")) : 10;
+  const int mask = getenv("PTTS_GEMV") ? atoi(getenv("PTTS_GEMV")) : 26;
   struct M {
     const float* w;
     int N, K, bit;
@@ -278,6 +279,9 @@ void Engine::derive_gemv() {
     mats.push_back({W(t.l1), FF, D, 4, wide});
     mats.push_back({W(t.l2), D, FF, 8, GemvShape{1, 64}});
   }
+  GemvShape ada{4, 128};  // flow-head adaLN matrix (PTTS_GEMV_ADA="wn,kw"): 0.6365 -> 0.6315 ms
+  if (getenv("PTTS_GEMV_ADA")) sscanf(getenv("PTTS_GEMV_ADA"), "%d,%d", &ada.wn, &ada.kw);
+  mats.push_back({W(L_.ada_w), NADA, FD, 16, ada});
   size_t total = 0;
   for (const M& m : mats)
     if ((mask & m.bit) && gemv_supported(m.g, m.N, m.K)) total += (size_t)m.N * m.K;
