@@ -271,11 +271,13 @@ void Engine::derive_gemv() {
   };
   std::vector<M> mats;
   GemvShape wide{4, 128};  // qkv / linear1 tile (PTTS_GEMV_WIDE="wn,kw")
+  GemvShape outg{1, 32};   // out tile (PTTS_GEMV_OUT="wn,kw")
+  if (getenv("PTTS_GEMV_OUT")) sscanf(getenv("PTTS_GEMV_OUT"), "%d,%d", &outg.wn, &outg.kw);
   if (getenv("PTTS_GEMV_WIDE")) sscanf(getenv("PTTS_GEMV_WIDE"), "%d,%d", &wide.wn, &wide.kw);
   for (int l = 0; l < NL; ++l) {
     const Layout::TL& t = L_.fl[l];
     mats.push_back({W(t.in_proj), 3 * D, D, 1, wide});
-    mats.push_back({W(t.out_proj), D, D, 2, GemvShape{1, 32}});
+    mats.push_back({W(t.out_proj), D, D, 2, outg});
     mats.push_back({W(t.l1), FF, D, 4, wide});
     mats.push_back({W(t.l2), D, FF, 8, GemvShape{1, 64}});
   }
