@@ -8,6 +8,8 @@
 //   activations                row-major [rows][features]; Mimi/SEANet channels-last [slot][time][ch]
 #include "engine.h"
 
+#include <rocblas/rocblas.h>
+
 #include <hip/hip_ext.h>
 
 #include <algorithm>
@@ -78,6 +80,13 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_REQUIRE(dev_ >= 0 && dev_ < ndev, "HIP device ordinal out of range");
   PTTS_HIP(hipSetDevice(dev_));
   PTTS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  if (!getenv("PTTS_BLAS") || atoi(getenv("PTTS_BLAS")) != 0) {
+    rocblas_handle h = nullptr;
+    if (rocblas_create_handle(&h) == rocblas_status_success) {
+      (void)rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
+      blas_ = h;
+    }
+  }
 
   L_ = pack_weights(nullptr, nullptr);
   if (cfg.weight_blob) {
@@ -221,6 +230,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
 Engine::~Engine() {
   (void)hipSetDevice(dev_);
   if (stream_) (void)hipStreamSynchronize(stream_);
+  if (blas_) (void)rocblas_destroy_handle((rocblas_handle)blas_);
   if (stream_be_) (void)hipStreamSynchronize(stream_be_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
@@ -433,6 +443,26 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   // large matrices (qkv, ff1, ff2, adaLN; >= 2M weights): below that the launch is latency-bound
   // and the f32 copy of the same values is as fast (tools/w8_probe.py). Prefill passes
   // (M >= 256) keep the f32 copy too: they are MFMA-bound.
+  if (blas_ && M >= 256 && name.rfind("prefill", 0) == 0 && q8map_.find(Wt) == q8map_.end() &&
+      f8map_.find(Wt) == f8map_.end()) {
+    // row-major Y[M][N] = X[M][K] W[N][K]^T as column-major Y^T (N x M) = W^T(N x K) X^T(K x M)
+    PTTS_REQUIRE((size_t)M * N <= pcap_, "split-K partial buffer too small");
+    rocblas_handle h = (rocblas_handle)blas_;
+    float* part = partial_;
+    ops.push_back({name,
+                   [=](hipStream_t s) {
+                     const float one = 1.f, zero = 0.f;
+                     if (rocblas_set_stream(h, s) != rocblas_status_success ||
+                         rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &one, Wt, K,
+                                       X, (rocblas_int)ldx, &zero, part, N) != rocblas_status_success)
+                       throw Error(PTTS_ERR_HIP, "rocblas_sgemm failed");
+                   },
+                   2.0 * M * N * K, 4.0 * ((double)N * K + (double)M * K + (double)M * N)});
+    last_split_ = GemmArgs{};
+    last_split_op_ = (size_t)-1;
+    *S_out = 1;
+    return;
+  }
   auto gv = gvmap_.find(Wt);
   if (gv != gvmap_.end() && M <= 32) {  // register-resident weights (derive_gemv)
     const GemvShape g = gv->second.second;

@@ -101,6 +101,10 @@ class Engine {
   // fragment-packed copies of the f32 FlowLM step matrices for gemv_splitk: weight -> (copy, shape)
   std::map<const float*, std::pair<const float*, GemvShape>> gvmap_;
   void derive_gemv();
+  // rocBLAS handle for the plain fp32 GEMMs of the text / voice prefill passes (M >= 256 rows,
+  // eager, never captured): the library's tiles run at 117-149 TF/s on those shapes, twice the
+  // hand-written 64x64 tile; the step's GEMMs stay hand-written (PTTS_BLAS=0 disables it)
+  void* blas_ = nullptr;
   bool own_blob_ = true, ready_ = false;
   hipStream_t stream_ = nullptr;
   Layout L_{};

@@ -23,6 +23,8 @@ int main() {
                            {"mimi.out", 512, 512, 512},    {"mimi.ff1", 512, 2048, 512},
                            {"mimi.ff2", 512, 512, 2048},   {"conv0 (im2col)", 512, 512, 3584},
                            {"convtr2 (1 phase)", 3072, 128, 512}, {"res3a (im2col)", 61440, 32, 192},
+                           {"prefill.qkv", 1536, 3072, 1024}, {"prefill.out", 1536, 1024, 1024},
+                           {"prefill.ff1", 1536, 4096, 1024}, {"prefill.ff2", 1536, 1024, 4096},
                            {"big 4096^3", 4096, 4096, 4096}};
   float *X, *W, *Y;
   (void)hipMalloc(&X, sizeof(float) * 64 << 20);

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 REPS=${REPS:-1}
 for r in $(seq 1 "$REPS"); do
   for v in $VALUES; do
-    t=$(echo "$v" | tr '/' '_')
+    t=$(echo "$v" | tr '/' '_' | cut -c1-60)$(echo "$v" | md5sum | cut -c1-6)
     if [ "$v" = "-" ]; then
       timeout -k 10 200 python bench.py --no-cpu-baseline --no-quant-variant --no-op-times --no-latency \
           ${BENCH_ARGS:-} > gpurun_out/sweep_$t.log 2>&1 || { echo "$VAR unset failed"; tail -5 gpurun_out/sweep_$t.log; exit 1; }
@@ -19,9 +19,11 @@ for r in $(seq 1 "$REPS"); do
     python - "$VAR=$v" gpurun_out/sweep_$t.log <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(sys.argv[1], "value", d["value"], "steady_ms", d["steady_ms_per_step"], flush=True)
+import os
+key = os.environ.get("METRIC", "steady_ms_per_step")
+print(sys.argv[1][:60], "value", d["value"], "steady_ms", d["steady_ms_per_step"], "admit_ms", d["admit_ms"], flush=True)
 with open("gpurun_out/sweep_all.txt", "a") as f:
-    f.write(f"{sys.argv[1]} {d['steady_ms_per_step']}\n")
+    f.write(f"{sys.argv[1]} {d[key]}\n")
 PY
   done
 done
@@ -32,6 +34,6 @@ for line in open("gpurun_out/sweep_all.txt"):
     k, v = line.split()
     d[k].append(float(v))
 for k, v in d.items():
-    print(f"median {k}: {statistics.median(v):.4f} ms over {len(v)}")
+    print(f"median {k[:70]}: {statistics.median(v):.4f} over {len(v)}")
 PY
 rm -f gpurun_out/sweep_all.txt
