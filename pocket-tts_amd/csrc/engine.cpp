@@ -156,9 +156,11 @@ Engine::Engine(const ptts_engine_config& cfg) {
   // pipelined stepping: the back part's kernels run at most one workgroup per CU, so the
   // latency-bound front part always finds room on every CU (measured 0.735 -> 0.688 ms per step
   // for the GEMMs alone; tools/sweep_env.sh)
-  // two hand-off buffers by default: the step is front-bound, and letting the front part run two
-  // frames ahead (3 buffers) measured 0.5% slower (more front/back overlap, same front work)
-  nhb_ = getenv("PTTS_HANDOFF_BUFS") && atoi(getenv("PTTS_HANDOFF_BUFS")) == 3 ? 3 : 2;
+  // three hand-off buffers: the front part may run two frames ahead of the back part. With the
+  // back part now the longer of the two alone (498 vs 441 us), the front no longer idles behind
+  // it: steady step 0.6370 -> 0.6321 ms (medians of 4; when the front was the longer part, 3
+  // buffers measured 0.5% slower). PTTS_HANDOFF_BUFS=2 restores lockstep.
+  nhb_ = getenv("PTTS_HANDOFF_BUFS") && atoi(getenv("PTTS_HANDOFF_BUFS")) == 2 ? 2 : 3;
   mimi_attn_fused_ = !getenv("PTTS_MIMI_ATTN_UNFUSED");
   back_cap_ = getenv("PTTS_BACK_WG_CAP") ? atoi(getenv("PTTS_BACK_WG_CAP")) : 1;
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
@@ -1134,7 +1136,7 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
 //   sequential: front(k) then back(k) on one stream; the call's frame is frame k.
 //   pipelined:  front(k) on stream_ || back(k-1) on stream_be_ (the back part decodes the frame
 //               the previous call's front part produced); the call's frame is frame k-1. Frame
-//               k's hand-off buffer is k % nhb_ (2, or 3 with PTTS_HANDOFF_BUFS=3): front(k)
+//               k's hand-off buffer is k % nhb_ (3, or 2 with PTTS_HANDOFF_BUFS=2): front(k)
 //               waits only for back(k - nhb_), the last reader of its buffer, and back(k-1) for
 //               front(k-1).
 void Engine::step_async(int B) {

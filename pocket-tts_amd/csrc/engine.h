@@ -148,7 +148,7 @@ class Engine {
   // Up to three hand-off buffers: front(k) writes buffer k % nhb_ and waits only for back(k - nhb_)
   // (nhb_ = 3 lets front and back drift a step apart instead of running in lockstep).
   static constexpr int NHB = 3;
-  int nhb_ = 2;  // buffers in use (2 or 3)
+  int nhb_ = 3;  // buffers in use (2 or 3)
   bool mimi_attn_fused_ = true;  // Mimi step: RoPE + ring append inside the attention launch
   float* lat_out_[NHB] = {};
   float* eos_out_[NHB] = {};
