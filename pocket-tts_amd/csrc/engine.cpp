@@ -1032,7 +1032,10 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     // per-stage tiles (tools/gemm_bench.hip, rb.* cases, B = 32; see above for pipelined)
     const int l_tr = big ? (i == 0 ? 20 : (i == 1 ? 13 : 22)) : 0;
     const int l_r3 = !big ? 0 : i == 2 ? 14 : pipeline_ ? 6 : (i == 0 ? 18 : 20);
-    const int l_r1 = big ? 6 : 0;
+    // stage 2's k1 conv (M = 32 * 3840 rows, N = 64): 128x64 register-blocked LDS-DMA tile in
+    // pipelined stepping, steady step 0.6310 -> 0.6188 ms (medians of 4; its 64x64 / 128x128
+    // neighbours 22 / 21 measured 0.644 / 0.652)
+    const int l_r1 = !big ? 0 : (i == 2 && pipeline_) ? 23 : 6;
     int l_t0 = 6, s_t0 = i == 0 ? 4 : 1;  // split-K of the first transposed conv (PTTS_OVR may change it)
     if (i == 0) tile_override(p + ".convtr", l_t0, s_t0);
     if (big && i == 0 && s_t0 > 1) {  // M = 16 B rows only: 4-way split-K fills the chip; bias + dual store in the reduce
