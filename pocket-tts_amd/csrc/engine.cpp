@@ -1323,10 +1323,60 @@ void Engine::overlap_probe(int B, int reps, double* us) {
     PTTS_HIP(hipEventElapsedTime(&ms, e0, e1));
     return 1000.0 * ms / reps;
   };
+  // us[7]: front || Mimi transformer || SEANet decoder on three streams (a 3-stage pipeline)
+  if (getenv("PTTS_PROBE_MODES") && strchr(getenv("PTTS_PROBE_MODES"), '7')) {
+    size_t cut2 = cut;
+    while (cut2 < ops.size() && ops[cut2].name != "seanet.conv0") ++cut2;
+    hipGraphExec_t g3[2] = {};
+    hipGraph_t d3[2] = {};
+    for (int part = 0; part < 2; ++part) {
+      PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+      set_wg_cap(back_cap_);
+      for (size_t i = part ? cut2 : cut; i < (part ? ops.size() : cut2); ++i) ops[i].fn(stream_);
+      set_wg_cap(0);
+      PTTS_HIP(hipStreamEndCapture(stream_, &d3[part]));
+      PTTS_HIP(hipGraphInstantiate(&g3[part], d3[part], nullptr, nullptr, 0));
+    }
+    hipStream_t s3 = nullptr;
+    PTTS_HIP(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+    hipEvent_t a0, a1, a2, a3;
+    PTTS_HIP(hipEventCreate(&a0));
+    PTTS_HIP(hipEventCreate(&a1));
+    PTTS_HIP(hipEventCreate(&a2));
+    PTTS_HIP(hipEventCreate(&a3));
+    auto run3 = [&](int n) {
+      for (int r = 0; r < n; ++r) {
+        PTTS_HIP(hipGraphLaunch(ge[0], stream_));
+        PTTS_HIP(hipGraphLaunch(g3[0], s2));
+        PTTS_HIP(hipGraphLaunch(g3[1], s3));
+      }
+    };
+    run3(2);
+    PTTS_HIP(hipDeviceSynchronize());
+    PTTS_HIP(hipEventRecord(a0, stream_));
+    PTTS_HIP(hipStreamWaitEvent(s2, a0, 0));
+    PTTS_HIP(hipStreamWaitEvent(s3, a0, 0));
+    run3(reps);
+    PTTS_HIP(hipEventRecord(a2, s2));
+    PTTS_HIP(hipEventRecord(a3, s3));
+    PTTS_HIP(hipStreamWaitEvent(stream_, a2, 0));
+    PTTS_HIP(hipStreamWaitEvent(stream_, a3, 0));
+    PTTS_HIP(hipEventRecord(a1, stream_));
+    PTTS_HIP(hipEventSynchronize(a1));
+    float ms = 0.f;
+    PTTS_HIP(hipEventElapsedTime(&ms, a0, a1));
+    us[7] = 1000.0 * ms / reps;
+    for (hipEvent_t e : {a0, a1, a2, a3}) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(s3);
+    for (int part = 0; part < 2; ++part) {
+      (void)hipGraphExecDestroy(g3[part]);
+      (void)hipGraphDestroy(d3[part]);
+    }
+  }
   // PTTS_PROBE_MODES: digits of the measurements to run (default all: "0123456")
   const std::string modes = getenv("PTTS_PROBE_MODES") ? getenv("PTTS_PROBE_MODES") : "0123456";
   auto want = [&](int m) { return modes.find((char)('0' + m)) != std::string::npos; };
-  for (int m = 0; m < 7; ++m) us[m] = -1.0;
+  for (int m = 0; m < 7; ++m) us[m] = -1.0;  // us[7]: see above
   for (int m = 0; m < 4; ++m)
     if (want(m)) us[m] = timed(m);
   // us[4..6]: front graph || back part launched op by op on a stream whose CU mask keeps

@@ -33,3 +33,4 @@ print(f"front {us[0]:.1f} us, back {us[1]:.1f} us, both concurrently {us[2]:.1f}
       f"(sum {us[0] + us[1]:.1f}); front high-priority {us[3]:.1f} us")
 print(f"front graph || back op by op on a CU-masked stream: 8/8 {us[4]:.1f} us, 6/8 {us[5]:.1f} us, "
       f"4/8 {us[6]:.1f} us")
+print(f"front || Mimi transformer || SEANet on three streams: {us[7]:.1f} us")
