@@ -275,7 +275,9 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
 // (steady step 0.6595 -> 0.6326 ms, medians of 3), the qkv / linear1 versions on any tile
 // (PTTS_GEMV_WIDE) slow the concurrent back part more than they gain. Default mask: 2 | 8 | 16.
 void Engine::derive_gemv() {
-  const int mask = getenv("PTTS_GEMV") ? atoi(getenv("PTTS_GEMV")) : 26;
+  // sequential stepping (the B = 1 first-chunk path, no concurrent back part): every matrix
+  const int mask = getenv("PTTS_GEMV") ? atoi(getenv("PTTS_GEMV")) : pipeline_ ? 26 : 31;
+  gemv_mask_ = mask;
   struct M {
     const float* w;
     int N, K, bit;
@@ -307,7 +309,7 @@ void Engine::derive_gemv() {
   for (const M& m : mats) {
     if (!(mask & m.bit) || !gemv_supported(m.g, m.N, m.K)) continue;
     pack_gemv(m.w, m.N, m.K, m.g, dst, stream_);
-    gvmap_[m.w] = {dst, m.g};
+    gvmap_[m.w] = Gemv{dst, m.g, m.bit};
     dst += (size_t)m.N * m.K;
   }
   PTTS_HIP(hipGetLastError());
@@ -466,9 +468,9 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
     return;
   }
   auto gv = gvmap_.find(Wt);
-  if (gv != gvmap_.end() && M <= 32) {  // register-resident weights (derive_gemv)
-    const GemvShape g = gv->second.second;
-    const float* P = gv->second.first;
+  if (gv != gvmap_.end() && M <= 64 && (gemv_mask_ & gv->second.bit)) {  // register-resident weights (derive_gemv)
+    const GemvShape g = gv->second.g;
+    const float* P = gv->second.packed;
     const int Sg = K / g.ks();
     PTTS_REQUIRE((size_t)Sg * M * N <= pcap_, "split-K partial buffer too small");
     float* part = partial_;

@@ -99,7 +99,13 @@ class Engine {
   // e4m3 code matrices of the large FlowLM step GEMMs: f32 weight pointer -> (codes, row scales)
   std::map<const float*, std::pair<const uint8_t*, const float*>> f8map_;
   // fragment-packed copies of the f32 FlowLM step matrices for gemv_splitk: weight -> (copy, shape)
-  std::map<const float*, std::pair<const float*, GemvShape>> gvmap_;
+  struct Gemv {
+    const float* packed;
+    GemvShape g;
+    int bit;  // PTTS_GEMV mask bit of the matrix
+  };
+  std::map<const float*, Gemv> gvmap_;
+  int gemv_mask_ = 0;  // matrices that take the register-resident GEMM
   void derive_gemv();
   // rocBLAS handle for the plain fp32 GEMMs of the text / voice prefill passes (M >= 256 rows,
   // eager, never captured): the library's tiles run at 117-149 TF/s on those shapes, twice the

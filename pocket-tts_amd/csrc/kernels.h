@@ -112,7 +112,8 @@ struct GemmArgs {
 };
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
 
-// Skinny split-K GEMM (M <= 32 rows, the FlowLM step) with register-resident weights: the
+// Skinny split-K GEMM (M <= 64 rows: the FlowLM step, small prefills; one 32-row block per
+// grid z) with register-resident weights: the
 // workgroup tile is 32 rows x 32*wn columns over a K slice of ks = kw * (4 / wn); wave w takes
 // 32 columns (w % wn) and kw of the slice's k ((w / wn) * kw ..). Its weight fragment (kw * 32
 // floats) comes from a copy packed in fragment order (pack_gemv: every load instruction reads 1

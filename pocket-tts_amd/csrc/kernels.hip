@@ -1339,15 +1339,15 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   __shared__ __attribute__((aligned(16))) float red[WK > 1 ? 4 * 16 * 64 : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int t = blockIdx.x, z = blockIdx.y, S = gridDim.y;
+  const int t = blockIdx.x, z = blockIdx.y, S = gridDim.y, m0 = 32 * blockIdx.z;  // z: K slice; blockIdx.z: 32-row block
   // X's slice first (the LDS fill waits only for these loads), then every weight load
   constexpr int AV = 32 * KS / 4 / 256;  // float4 of X per thread
   float4 av[AV];
 #pragma unroll
   for (int i = 0; i < AV; ++i) {
     const int e = tid + 256 * i, row = e / (KS / 4), c4 = e % (KS / 4);
-    av[i] = row < M ? *reinterpret_cast<const float4*>(X + (long)row * ldx + (long)z * KS + 4 * c4)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    av[i] = m0 + row < M ? *reinterpret_cast<const float4*>(X + (long)(m0 + row) * ldx + (long)z * KS + 4 * c4)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   typedef float f4v __attribute__((ext_vector_type(4)));
   const f4v* wp = reinterpret_cast<const f4v*>(P) + (((long)t * S + z) * 4 + wave) * NV * 64 + lane;
@@ -1378,7 +1378,7 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   if (WK == 1) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
+      const int row = m0 + (g & 3) + 8 * (g >> 2) + 4 * h;
       if (row < M) out[(long)row * N + n] = acc[g];
     }
     return;
@@ -1394,7 +1394,7 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
     float v = red[(c * 16 + g) * 64 + lane];
 #pragma unroll
     for (int kk = 1; kk < WK; ++kk) v += red[((kk * WN + c) * 16 + g) * 64 + lane];
-    const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
+    const int row = m0 + (g & 3) + 8 * (g >> 2) + 4 * h;
     if (row < M) out[(long)row * N + t * 32 * WN + c * 32 + m] = v;
   }
 }
@@ -1414,8 +1414,8 @@ void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStre
 
 void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
                  hipStream_t s) {
-  if (M < 1 || M > 32 || !gemv_supported(g, N, K)) throw std::runtime_error("gemv_splitk: unsupported shape");
-  const dim3 grid((unsigned)(N / (32 * g.wn)), (unsigned)(K / g.ks()));
+  if (M < 1 || M > 64 || !gemv_supported(g, N, K)) throw std::runtime_error("gemv_splitk: unsupported shape");
+  const dim3 grid((unsigned)(N / (32 * g.wn)), (unsigned)(K / g.ks()), (unsigned)((M + 31) / 32));
 #define PTTS_GEMV(WN_, KW_)                                                                              \
   if (g.wn == WN_ && g.kw == KW_) {                                                                      \
     hipLaunchKernelGGL((k_gemv<WN_, KW_>), grid, dim3(256), cap_lds(k_gemv<WN_, KW_>, g_wg_cap), s, X, ldx, M, N, \
