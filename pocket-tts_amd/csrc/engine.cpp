@@ -944,11 +944,14 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     }
     dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
              fat ? fat_layout : 0);
-    if (fat) {  // K = 2048: 64x64 LDS-DMA tiles, 4-way split-K; LayerScale + residual in the reduce
-      int S = 4, lay = 6;
+    {  // K = 2048, split-K; LayerScale + residual (+ the next layer's norm1) in the reduce. Fat:
+       // 64x64 LDS-DMA tiles, 4 slices; few rows (B < 16, the first-chunk path): 32x32 tiles, 8
+       // slices (16 -> 128 workgroups: 18.2 -> ~7 us at B = 1, and no separate norm1 launch)
+      int S = fat ? 4 : 8, lay = fat ? 6 : 0;
       tile_override(p + ".ff2_gemm", lay, S);
-      PTTS_REQUIRE(S >= 1 && S <= 16 && (lay == 6 || lay == 7 || lay == 11 || lay == 12 || lay == 13 || lay == 14),
-                   "mimi ff2: split-K 1..16 on a single-phase LDS-DMA tile");
+      PTTS_REQUIRE(S >= 1 && S <= 16 &&
+                       (lay == 0 || lay == 6 || lay == 7 || lay == 11 || lay == 12 || lay == 13 || lay == 14),
+                   "mimi ff2: split-K 1..16 on a single-phase tile");
       GemmArgs a{};
       a.mode = 0;
       a.layout = lay;
@@ -984,13 +987,6 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
         r.ldh = MD;
       }
       ops.push_back({p + ".ff2_reduce", [r](hipStream_t s) { row_reduce(r, s); }});
-    } else {
-      dense_op(ops, p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, nullptr, ACT_NONE, W(t.ls2), mx_, mx_);
-    }
-    if (l + 1 < MNL && !fat) {
-      const float *x = mx_, *w = W(L_.mdec[l + 1].n1w), *b = W(L_.mdec[l + 1].n1b);
-      float* h = mh_;
-      ops.push_back({p + ".ln1_next", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
     }
   }
   // SEANetDecoder (seanet.rs:396-402): conv0 -> [ELU, convtr(r), resblock] x3 -> ELU, conv(64->1).
@@ -1009,7 +1005,8 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   // back_tune.py: 32 us less back time in all) each made the pipelined step slower.
   int l_c0 = 6, s_c0 = 8;  // conv0 tile / split-K (PTTS_OVR may change them)
   tile_override("seanet.conv0", l_c0, s_c0);
-  if (big && s_c0 > 1) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the reduce
+  if (s_c0 > 1) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the reduce (every B:
+                   // at B = 1 the unsplit launch had 16 workgroups, 27.4 us)
     conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
             nullptr, 16, 1, l_c0, 0, nullptr, s_c0);
     RowReduceArgs r{};
