@@ -2826,39 +2826,50 @@ __device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, floa
 }
 
 // LayerNorm (eps 1e-6, optional affine) + adaLN modulate (mlp.rs:29-58,135-137) of this lane's
-// 16 values of row c; row statistics combine the 4 lane groups and the 8 waves in a fixed order.
+// 16 values of row c. Row statistics in ONE workgroup barrier: each wave contributes its 64
+// values' sum and squared deviations about their own mean, combined as M2 = sum_w [M2_w +
+// 64 (mean_w - mean)^2] (Chan et al.'s pairwise update; the same two-pass variance, summed in a
+// different order), in a fixed wave order.
+// The affines (lnw, lnb: LDS, this lane's k range; nullptr for none) are read after the barrier,
+// so the prologue's LDS fill needs no barrier of its own.
 __device__ __forceinline__ void fh_ln(float4 (&v)[4], float (*s_st)[FH_WAVES][16], int wave, int c, int G,
-                                      const float4 (&lw)[4], const float4 (&lb)[4], bool affine,
-                                      const float4 (&sc)[4], const float4 (&sf)[4]) {
+                                      const float* lnw, const float* lnb, const float4 (&sc)[4],
+                                      const float4 (&sf)[4]) {
   float s1 = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) s1 += (v[j].x + v[j].y) + (v[j].z + v[j].w);
   s1 += __shfl_xor(s1, 16, 64);
   s1 += __shfl_xor(s1, 32, 64);
-  if (G == 0) s_st[0][wave][c] = s1;
+  const float mw = s1 * (1.0f / 64.0f);
+  float m2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = v[j].x - mw, b = v[j].y - mw, d = v[j].z - mw, e = v[j].w - mw;
+    m2 += (a * a + b * b) + (d * d + e * e);
+  }
+  m2 += __shfl_xor(m2, 16, 64);
+  m2 += __shfl_xor(m2, 32, 64);
+  if (G == 0) {
+    s_st[0][wave][c] = s1;
+    s_st[1][wave][c] = m2;
+  }
   __syncthreads();
   float tot = 0.f;
 #pragma unroll
   for (int w = 0; w < FH_WAVES; ++w) tot += s_st[0][w][c];
   const float mean = tot / (float)FH_D;
-  float s2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    v[j] = make_float4(v[j].x - mean, v[j].y - mean, v[j].z - mean, v[j].w - mean);
-    s2 += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
-  }
-  s2 += __shfl_xor(s2, 16, 64);
-  s2 += __shfl_xor(s2, 32, 64);
-  if (G == 0) s_st[1][wave][c] = s2;
-  __syncthreads();
   float q = 0.f;
 #pragma unroll
-  for (int w = 0; w < FH_WAVES; ++w) q += s_st[1][w][c];
+  for (int w = 0; w < FH_WAVES; ++w) {
+    const float dm = s_st[0][w][c] * (1.0f / 64.0f) - mean;
+    q += s_st[1][w][c] + 64.0f * dm * dm;
+  }
   const float rden = 1.0f / sqrtf(q / (float)FH_D + 1e-6f);  // one divide, then multiplies (<= 1 ulp apart)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float4 h = make_float4(v[j].x * rden, v[j].y * rden, v[j].z * rden, v[j].w * rden);
-    if (affine) h = f4add(f4mul(h, lw[j]), lb[j]);
+    float4 h = make_float4((v[j].x - mean) * rden, (v[j].y - mean) * rden, (v[j].z - mean) * rden,
+                           (v[j].w - mean) * rden);
+    if (lnw) h = f4add(f4mul(h, f4ld(lnw + 4 * j)), f4ld(lnb + 4 * j));
     v[j] = make_float4(h.x * (1.0f + sc[j].x) + sf[j].x, h.y * (1.0f + sc[j].y) + sf[j].y,
                        h.z * (1.0f + sc[j].z) + sf[j].z, h.w * (1.0f + sc[j].w) + sf[j].w);
   }
@@ -2869,16 +2880,18 @@ __device__ __forceinline__ void fh_ln(float4 (&v)[4], float (*s_st)[FH_WAVES][16
 // reads of one and the other waves' writes of the next)
 __device__ __forceinline__ float4 fh_gemm(const float4 (&a)[4], const float4 (&b)[4], float (*s_red)[16][16],
                                           int wave, int c, int G, int lane) {
-  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  // four independent accumulator chains (one per float4 of the lane's k range), summed after:
+  // the dependent chain of 16 MFMAs was the phase's longest serial step
+  floatx4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].x, b[j].x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].y, b[j].y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].z, b[j].z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].w, b[j].w, acc, 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].x, b[j].x, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].y, b[j].y, acc[j], 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].z, b[j].z, acc[j], 0, 0, 0);
+    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j].w, b[j].w, acc[j], 0, 0, 0);
   }
 #pragma unroll
-  for (int g = 0; g < 4; ++g) s_red[wave][4 * G + g][c] = acc[g];
+  for (int g = 0; g < 4; ++g) s_red[wave][4 * G + g][c] = (acc[0][g] + acc[1][g]) + (acc[2][g] + acc[3][g]);
   __syncthreads();
   float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
   if (wave == 0) {
@@ -2922,19 +2935,10 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   int gi = 0;  // GEMMs done (s_red buffer parity)
   bool dead = false;
   float4 xo = make_float4(0.f, 0.f, 0.f, 0.f);  // wave 0: residual tile x[orow][ocol..+3]
-  const float4 zero4[4] = {};
   int sk = 0;
 #define FH_STAMP()                                                                     \
   if (a.dbg && tid == 0 && blockIdx.x < 4 && sk < 120) a.dbg[blockIdx.x * 128 + sk++] = __builtin_amdgcn_s_memrealtime()
 
-#pragma unroll
-  for (int i = 0; i < FH_DEPTH; ++i)
-    if (tid < FH_D / 2) {  // threads 0..255: float4 (tid & 127) of lnw (tid < 128) or lnb
-      const float* src = (tid < FH_D / 4 ? a.lnw : a.lnb) + (long)i * a.blk;
-      reinterpret_cast<float4*>(&s_ln[i][tid < FH_D / 4 ? 0 : 1][0])[tid & (FH_D / 4 - 1)] =
-          f4ld(src + 4 * (tid & (FH_D / 4 - 1)));
-    }
-  __syncthreads();  // s_ln before the first LayerNorm (the sweeps have no barrier)
   // operand loaders (i: ResBlock, or FH_DEPTH for the FinalLayer)
   auto load_ln_ops = [&](FhOps& o, const float* mods, int i) {
     if (i == FH_DEPTH && !fin) return;
@@ -2958,12 +2962,11 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
     }
   };
   FhOps p0, p2;  // operands of the next LayerNorm phase and the next mlp2 phase
-  load_ln_ops(p0, a.mods, 0);
-  load_mlp2_ops(p2, a.mods, 0);
 
   for (int st = 0; st < a.lsd; ++st) {
     const float* mods = a.mods + (long)st * a.B * a.ldm;
-    // ---- input projection x = cur W_in^T + b_in (K = 32), one wave
+    // ---- input projection x = cur W_in^T + b_in (K = 32), one wave. At st = 0 it comes first:
+    // its hand-off starts the chain, so its loads are not queued behind the prologue's
     if (st > 0) fh_wait(cc, 2 * st, a.err, dead);
     if (wave == 0) {
       float4 cv[8];
@@ -2985,6 +2988,19 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       if (ostore) fh_put(hr, q * rstride + ooff, xo);
     }
     ++q;
+    if (st == 0) {
+      // the first phases' operands, then the ResBlock LayerNorm affines into LDS (first read
+      // after the first LayerNorm's barrier)
+      load_ln_ops(p0, mods, 0);
+      load_mlp2_ops(p2, mods, 0);
+#pragma unroll
+      for (int i = 0; i < FH_DEPTH; ++i)
+        if (tid < FH_D / 2) {  // threads 0..255: float4 (tid & 127) of lnw (tid < 128) or lnb
+          const float* src = (tid < FH_D / 4 ? a.lnw : a.lnb) + (long)i * a.blk;
+          reinterpret_cast<float4*>(&s_ln[i][tid < FH_D / 4 ? 0 : 1][0])[tid & (FH_D / 4 - 1)] =
+              f4ld(src + 4 * (tid & (FH_D / 4 - 1)));
+        }
+    }
 #pragma unroll 1
     for (int i = 0; i < FH_DEPTH; ++i) {
       // ---- h = modulate(LN(x)), u = silu(h W0^T + b0)
@@ -2992,13 +3008,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       FH_STAMP();
       fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
       FH_STAMP();
-      float4 lw[4], lb[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        lw[j] = f4ld(&s_ln[i][0][k0 + 4 * j]);
-        lb[j] = f4ld(&s_ln[i][1][k0 + 4 * j]);
-      }
-      fh_ln(v, s_st, wave, c, G, lw, lb, true, p0.sc, p0.sf);
+      fh_ln(v, s_st, wave, c, G, &s_ln[i][0][k0], &s_ln[i][1][k0], p0.sc, p0.sf);
       FH_STAMP();
       float4 r = fh_gemm(v, p0.w, s_red2[gi++ & 1], wave, c, G, lane);
       FH_STAMP();
@@ -3013,32 +3023,36 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       ++q;
       // ---- x += gate * (u W2^T + b2)
       fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
+      FH_STAMP();
       r = fh_gemm(v, p2.w, s_red2[gi++ & 1], wave, c, G, lane);
+      FH_STAMP();
       if (wave != 0 && i + 1 < FH_DEPTH) load_mlp2_ops(p2, mods, i + 1);
       if (wave == 0) {
         xo = f4add(xo, f4mul(p2.e0, f4add(r, p2.e1)));
         if (ostore) fh_put(hr, q * rstride + ooff, xo);
         if (i + 1 < FH_DEPTH) load_mlp2_ops(p2, mods, i + 1);
       }
+      FH_STAMP();
       ++q;
     }
     // ---- FinalLayer (mlp.rs:182-213): modulate(LN_noaffine(x)) W_f^T + b_f, Euler x += v / N
     const float* nmods = mods + (long)a.B * a.ldm;  // next Euler step's modulations
     const bool more = st + 1 < a.lsd;
     if (fin) {
+      const int off = (crow * FH_L + ocol) * 4;
+      float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (wave == 0) cv = fh_ld(cr, off);  // latent before this Euler step (read ahead of the sweep)
       float4 v[4];
       fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
       if (wave != 0 && more) load_mlp2_ops(p2, nmods, 0);
-      fh_ln(v, s_st, wave, c, G, zero4, zero4, false, p0.sc, p0.sf);
+      fh_ln(v, s_st, wave, c, G, nullptr, nullptr, p0.sc, p0.sf);
       const float4 r = fh_gemm(v, p0.w, s_red2[gi++ & 1], wave, c, G, lane);
       if (wave != 0 && more) load_ln_ops(p0, nmods, 0);
       if (wave == 0) {
-        const int off = (crow * FH_L + ocol) * 4;
-        const float4 cv = fh_ld(cr, off);
         const float e = a.euler_scale;
         const float4 o = f4add(r, p0.e0);
         if (ostore) fh_st(cr, off, make_float4(cv.x + o.x * e, cv.y + o.y * e, cv.z + o.z * e, cv.w + o.w * e));
-        fh_publish(cc);
+        if (more) fh_publish(cc);
         if (more) {
           load_ln_ops(p0, nmods, 0);
           load_mlp2_ops(p2, nmods, 0);
@@ -3049,8 +3063,9 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       load_mlp2_ops(p2, nmods, 0);
     }
   }
-  // re-arm: the last workgroup to finish zeroes every counter (all waits are behind it)
-  if (tid == 0) {
+  // re-arm: the last workgroup to finish zeroes every counter (all waits are behind it); with one
+  // Euler step no counter is used
+  if (a.lsd > 1 && tid == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int* done = a.ctr + 4 * RG;
     if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
