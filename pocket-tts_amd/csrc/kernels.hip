@@ -2753,10 +2753,15 @@ void resample(const float* x, int n_in, const float* taps, const ResamplePlan& p
 // counter (sc1 stores, drain, agent-scope add); counters are zeroed at allocation and re-armed by
 // the last workgroup to finish.
 // v_mfma_f32_16x16x4_f32 fragments as in k_attn16: lane (c = l & 15, G = l >> 4) supplies
-// A[row c][k] and B[k][col c] for k = 64*wave + 16*G + s at step s; D reg g -> row 4G+g, col c.
+// A[row c][k] and B[k][col c] for k = 64*wave + FH_KJ*(s/4) + 4*G + s%4 at step s (FH_KJ below); D reg g -> row 4G+g, col c.
 // =============================================================================================
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int FH_WAVES = 8;  // FH_D, FH_L, FH_DEPTH: kernels.h
+// k layout of a lane's 16 values: float4 j of lane group G holds k = 64 wave + FH_KJ j + 4 G ..+3,
+// so the 4 lane groups of a row read 64 contiguous bytes per load instruction (16 rows x 64 B
+// per instruction instead of 16 rows x four 16-B pieces 64 B apart). A and B use the same k
+// order, so the MFMA sum is over the same products.
+constexpr int FH_KJ = 16;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t fh_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
@@ -2807,7 +2812,7 @@ __device__ __forceinline__ bool fh_empty(float4 v) {
 // launch (the frame is poisoned, fetch() reports it).
 __device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, float4 (&v)[4], int* err, bool& dead) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = fh_ld(r, off + 16 * j);
+  for (int j = 0; j < 4; ++j) v[j] = fh_ld(r, off + FH_KJ * 4 * j);
   unsigned spins = 0;
   while (!dead) {
     bool ok = true;
@@ -2817,7 +2822,7 @@ __device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, floa
     __builtin_amdgcn_s_sleep(1);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (fh_empty(v[j])) v[j] = fh_ld(r, off + 16 * j);
+      if (fh_empty(v[j])) v[j] = fh_ld(r, off + FH_KJ * 4 * j);
     if (++spins > (1u << 20)) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       dead = true;
@@ -2869,7 +2874,7 @@ __device__ __forceinline__ void fh_ln(float4 (&v)[4], float (*s_st)[FH_WAVES][16
   for (int j = 0; j < 4; ++j) {
     float4 h = make_float4((v[j].x - mean) * rden, (v[j].y - mean) * rden, (v[j].z - mean) * rden,
                            (v[j].w - mean) * rden);
-    if (lnw) h = f4add(f4mul(h, f4ld(lnw + 4 * j)), f4ld(lnb + 4 * j));
+    if (lnw) h = f4add(f4mul(h, f4ld(lnw + FH_KJ * j)), f4ld(lnb + FH_KJ * j));
     v[j] = make_float4(h.x * (1.0f + sc[j].x) + sf[j].x, h.y * (1.0f + sc[j].y) + sf[j].y,
                        h.z * (1.0f + sc[j].z) + sf[j].z, h.w * (1.0f + sc[j].w) + sf[j].w);
   }
@@ -2921,7 +2926,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;
   const int col0 = 16 * cg;
   const int arow = min(16 * rg + c, a.B - 1);  // A-operand row of this lane (clamped; rows >= B unused)
-  const int k0 = 64 * wave + 16 * G;           // this lane's 16 k
+  const int k0 = 64 * wave + 4 * G;            // this lane's 16 k: k0 + FH_KJ j + 0..3, j < 4
   const int orow = 16 * rg + (lane >> 2);      // epilogue (wave 0): row, columns ocol..ocol+3
   const int ocol = col0 + 4 * (lane & 3);
   const int crow = min(orow, a.B - 1);
@@ -2946,16 +2951,16 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
     const float* mr = mods + (long)arow * a.ldm + (long)i * 3 * FH_D + k0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      o.w[j] = f4ld(W + 4 * j);
-      o.sf[j] = f4ld(mr + 4 * j);
-      o.sc[j] = f4ld(mr + FH_D + 4 * j);
+      o.w[j] = f4ld(W + FH_KJ * j);
+      o.sf[j] = f4ld(mr + FH_KJ * j);
+      o.sc[j] = f4ld(mr + FH_D + FH_KJ * j);
     }
     if (wave == 0) o.e0 = f4ld((i < FH_DEPTH ? a.b0 + (long)i * a.blk : a.fin_b) + ocol);
   };
   auto load_mlp2_ops = [&](FhOps& o, const float* mods, int i) {
     const float* W = a.w2 + (long)i * a.blk + (long)(col0 + c) * FH_D + k0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o.w[j] = f4ld(W + 4 * j);
+    for (int j = 0; j < 4; ++j) o.w[j] = f4ld(W + FH_KJ * j);
     if (wave == 0) {
       o.e0 = f4ld(mods + (long)crow * a.ldm + (long)i * 3 * FH_D + 2 * FH_D + ocol);  // gate
       o.e1 = f4ld(a.b2 + (long)i * a.blk + ocol);
