@@ -328,6 +328,14 @@ void Engine::finalize() {
     inw_t_ = (float*)p;
   }
   transpose(W(L_.input_linear), D, LDIM, inw_t_, stream_);
+  const bool wpack = !(getenv("PTTS_FH_WPACK") && !atoi(getenv("PTTS_FH_WPACK")));
+  if (!fhw_ && wpack && head_uniform_stride()) {  // every element is written by the packing below
+    void* p = nullptr;
+    PTTS_HIP(hipMalloc(&p, sizeof(float) * flow_head_packed_floats()));
+    allocs_.push_back(p);
+    fhw_ = (float*)p;
+  }
+  if (fhw_) pack_flow_head(W(L_.rb_w0[0]), W(L_.rb_w2[0]), (long)(L_.rb_w0[1] - L_.rb_w0[0]), W(L_.fin_w), fhw_, stream_);
   TimeEmbedWeights tw;
   for (int i = 0; i < 2; ++i) {
     tw.l1w[i] = W(L_.te_l1w[i]);
@@ -714,6 +722,10 @@ bool Engine::use_head_chain(int B) const {
   if (!head_chain_ || !flow_head_fits(B)) return false;
   // every workgroup spins on counters the others bump: all of them must be resident at once
   if (flow_head_grid(B) > head_resident_) return false;
+  return head_uniform_stride();
+}
+
+bool Engine::head_uniform_stride() const {
   const long s = (long)(L_.rb_w0[1] - L_.rb_w0[0]);
   for (int i = 1; i < FDEPTH; ++i)
     if ((long)(L_.rb_lnw[i] - L_.rb_lnw[i - 1]) != s || (long)(L_.rb_lnb[i] - L_.rb_lnb[i - 1]) != s ||
@@ -784,7 +796,9 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     f.blk = (long)(L_.rb_w0[1] - L_.rb_w0[0]);
     f.fin_w = W(L_.fin_w);
     f.fin_b = W(L_.fin_b);
+    f.wp = fhw_;
     f.hx = hx_;
+    f.hx_rows = getenv("PTTS_FH_HX_ROWS") ? atoi(getenv("PTTS_FH_HX_ROWS")) : 0;
     f.ctr = hctr_;
     f.err = herr_;
     f.dbg = getenv("PTTS_HEAD_DBG") ? (unsigned long long*)strtoull(getenv("PTTS_HEAD_DBG"), nullptr, 0) : nullptr;

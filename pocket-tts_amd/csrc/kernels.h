@@ -221,9 +221,14 @@ struct FlowHeadArgs {
   const float *lnw, *lnb, *w0, *b0, *w2, *b2;
   long blk;
   const float *fin_w, *fin_b;
+  // the 13 chain matrices (w0 / w2 of each ResBlock, then fin_w) in fragment order
+  // (pack_flow_head): every operand load instruction reads one contiguous KB
+  const float* wp;
   // hand-off regions: 13 per Euler step (x0, then u_i, x_{i+1} per ResBlock), each
-  // [ceil(B/16) * 16][512], all 0xFFFFFFFF (empty) at launch
+  // [ceil(B/16)][32 column groups][16 rows][16 columns] (one producer tile = one contiguous KB),
+  // all 0xFFFFFFFF (empty) at launch
   float* hx;
+  int hx_rows;  // 1: row-major [ceil(B/16) * 16][512] regions instead (PTTS_FH_HX_ROWS, A/B only)
   int* ctr;
   int* err;
   unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr
@@ -232,6 +237,9 @@ struct FlowHeadArgs {
 // each kernel share a CU (0 = no cap). Process-wide; the engine sets it around graph capture.
 void set_wg_cap(int cap);
 bool flow_head_fits(int B);
+// fragment-order copy of the chain's matrices for FlowHeadArgs::wp: 12 * 512 * 512 + 32 * 512 floats
+size_t flow_head_packed_floats();
+void pack_flow_head(const float* w0, const float* w2, long blk, const float* fin_w, float* dst, hipStream_t s);
 int flow_head_grid(int B);             // workgroups of one k_flow_head launch
 int flow_head_max_resident(int dev);   // co-resident k_flow_head workgroups (occupancy x CUs)
 // FlowLM input_linear (32 -> 1024, no bias) + layer-0 norm1: x = lat W^T, h = LN(x) (eps 1e-5).

@@ -2762,6 +2762,9 @@ constexpr int FH_WAVES = 8;  // FH_D, FH_L, FH_DEPTH: kernels.h
 // per instruction instead of 16 rows x four 16-B pieces 64 B apart). A and B use the same k
 // order, so the MFMA sum is over the same products.
 constexpr int FH_KJ = 16;
+// consumer offsets of float4 j in a hand-off region: the 16 columns of j sit in the next column
+// group's 16x16 tile, 1 KB on
+constexpr int FH_SJ = 16 * 16 * 4;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t fh_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
@@ -2810,9 +2813,10 @@ __device__ __forceinline__ bool fh_empty(float4 v) {
 // consumer: this lane's 16 values of a region (byte offset `off`), re-read until none is empty.
 // The loop condition is wave-uniform; a timeout sets *err and stops waiting for the rest of the
 // launch (the frame is poisoned, fetch() reports it).
-__device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, float4 (&v)[4], int* err, bool& dead) {
+__device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, int sj, float4 (&v)[4], int* err,
+                                         bool& dead) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = fh_ld(r, off + FH_KJ * 4 * j);
+  for (int j = 0; j < 4; ++j) v[j] = fh_ld(r, off + sj * j);
   unsigned spins = 0;
   while (!dead) {
     bool ok = true;
@@ -2822,7 +2826,7 @@ __device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, floa
     __builtin_amdgcn_s_sleep(1);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (fh_empty(v[j])) v[j] = fh_ld(r, off + FH_KJ * 4 * j);
+      if (fh_empty(v[j])) v[j] = fh_ld(r, off + sj * j);
     if (++spins > (1u << 20)) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       dead = true;
@@ -2935,7 +2939,13 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   const __amdgpu_buffer_rsrc_t hr = fh_rsrc(a.hx), cr = fh_rsrc(a.cur);
   int* cc = a.ctr + 4 * rg + 2;  // cur published (lsd > 1)
   const int rstride = RG * 16 * FH_D * 4;  // bytes per hand-off region
-  const int aoff = (arow * FH_D + k0) * 4, ooff = (orow * FH_D + ocol) * 4;  // sweep / store offsets
+  // sweep / store byte offsets in a hand-off region ([RG][32][16][16]: tile (rg, cg) is one KB):
+  // lane (c, G) of wave w reads row c, columns 16 (4w + j) + 4G..+3 of its row group; wave 0 lane
+  // t stores its tile's row t/4, columns 4(t%4)..+3 at tile offset 16 t bytes
+  // (a.hx_rows: row-major [RG * 16][512] regions instead, 64 B per row and load)
+  const int aoff = a.hx_rows ? (arow * FH_D + k0) * 4 : (((rg * 32 + 4 * wave) * 16 + (arow - 16 * rg)) * 16 + 4 * G) * 4;
+  const int ooff = a.hx_rows ? (orow * FH_D + ocol) * 4 : ((rg * 32 + cg) * 256 + 4 * lane) * 4;
+  const int sj = a.hx_rows ? FH_KJ * 4 : FH_SJ;
   int q = 0;   // next hand-off region
   int gi = 0;  // GEMMs done (s_red buffer parity)
   bool dead = false;
@@ -2945,22 +2955,29 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   if (a.dbg && tid == 0 && blockIdx.x < 4 && sk < 120) a.dbg[blockIdx.x * 128 + sk++] = __builtin_amdgcn_s_memrealtime()
 
   // operand loaders (i: ResBlock, or FH_DEPTH for the FinalLayer)
+  // fragment-packed matrix m (2i: w0 of ResBlock i, 2i + 1: its w2, 12: fin_w), this lane's float4 j
+  const float* wpl = a.wp ? a.wp + ((long)cg * FH_WAVES + wave) * 4 * 256 + 4 * lane : nullptr;
+  auto wfrag = [&](int m, int j) {
+    if (!a.wp) {  // row-major matrices of the blob (PTTS_FH_WPACK=0)
+      const float* W = (m == 2 * FH_DEPTH ? a.fin_w : (m & 1 ? a.w2 : a.w0) + (long)(m >> 1) * a.blk);
+      return f4ld(W + (long)(col0 + c) * FH_D + k0 + FH_KJ * j);
+    }
+    return f4ld(wpl + (long)m * (32 * FH_WAVES * 4 * 256) + j * 256);
+  };
   auto load_ln_ops = [&](FhOps& o, const float* mods, int i) {
     if (i == FH_DEPTH && !fin) return;
-    const float* W = (i < FH_DEPTH ? a.w0 + (long)i * a.blk : a.fin_w) + (long)(col0 + c) * FH_D + k0;
     const float* mr = mods + (long)arow * a.ldm + (long)i * 3 * FH_D + k0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      o.w[j] = f4ld(W + FH_KJ * j);
+      o.w[j] = wfrag(2 * i, j);
       o.sf[j] = f4ld(mr + FH_KJ * j);
       o.sc[j] = f4ld(mr + FH_D + FH_KJ * j);
     }
     if (wave == 0) o.e0 = f4ld((i < FH_DEPTH ? a.b0 + (long)i * a.blk : a.fin_b) + ocol);
   };
   auto load_mlp2_ops = [&](FhOps& o, const float* mods, int i) {
-    const float* W = a.w2 + (long)i * a.blk + (long)(col0 + c) * FH_D + k0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o.w[j] = f4ld(W + FH_KJ * j);
+    for (int j = 0; j < 4; ++j) o.w[j] = wfrag(2 * i + 1, j);
     if (wave == 0) {
       o.e0 = f4ld(mods + (long)crow * a.ldm + (long)i * 3 * FH_D + 2 * FH_D + ocol);  // gate
       o.e1 = f4ld(a.b2 + (long)i * a.blk + ocol);
@@ -3011,7 +3028,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       // ---- h = modulate(LN(x)), u = silu(h W0^T + b0)
       float4 v[4];
       FH_STAMP();
-      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
+      fh_sweep(hr, (q - 1) * rstride + aoff, sj, v, a.err, dead);
       FH_STAMP();
       fh_ln(v, s_st, wave, c, G, &s_ln[i][0][k0], &s_ln[i][1][k0], p0.sc, p0.sf);
       FH_STAMP();
@@ -3027,7 +3044,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       FH_STAMP();
       ++q;
       // ---- x += gate * (u W2^T + b2)
-      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
+      fh_sweep(hr, (q - 1) * rstride + aoff, sj, v, a.err, dead);
       FH_STAMP();
       r = fh_gemm(v, p2.w, s_red2[gi++ & 1], wave, c, G, lane);
       FH_STAMP();
@@ -3048,7 +3065,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
       if (wave == 0) cv = fh_ld(cr, off);  // latent before this Euler step (read ahead of the sweep)
       float4 v[4];
-      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
+      fh_sweep(hr, (q - 1) * rstride + aoff, sj, v, a.err, dead);
       if (wave != 0 && more) load_mlp2_ops(p2, nmods, 0);
       fh_ln(v, s_st, wave, c, G, nullptr, nullptr, p0.sc, p0.sf);
       const float4 r = fh_gemm(v, p0.w, s_red2[gi++ & 1], wave, c, G, lane);
@@ -3136,6 +3153,26 @@ void transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) 
 }
 
 bool flow_head_fits(int B) { return B >= 1 && B <= 128; }
+
+size_t flow_head_packed_floats() { return (size_t)2 * FH_DEPTH * FH_D * FH_D + (size_t)FH_L * FH_D; }
+
+// dst float4 (((m * 32 + cg) * 8 + w) * 4 + j) * 64 + l = W_m[16 cg + (l & 15)][64 w + FH_KJ j +
+// 4 (l >> 4) ..+3], W_m = w0 / w2 of ResBlock m / 2, or fin_w (m = 12, column groups 0-1)
+__global__ void k_pack_flow_head(const float* w0, const float* w2, long blk, const float* fin_w, float4* dst,
+                                 long n4) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n4) return;
+  const int l = (int)(e & 63), j = (int)((e >> 6) & 3), w = (int)((e >> 8) & 7), cg = (int)((e >> 11) & 31);
+  const int m = (int)(e >> 16);
+  const float* W = m == 2 * FH_DEPTH ? fin_w : (m & 1 ? w2 : w0) + (long)(m >> 1) * blk;
+  dst[e] = *reinterpret_cast<const float4*>(W + (long)(16 * cg + (l & 15)) * FH_D + 64 * w + FH_KJ * j + 4 * (l >> 4));
+}
+
+void pack_flow_head(const float* w0, const float* w2, long blk, const float* fin_w, float* dst, hipStream_t s) {
+  const long n4 = (long)flow_head_packed_floats() / 4;
+  hipLaunchKernelGGL(k_pack_flow_head, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, w0, w2, blk, fin_w,
+                     reinterpret_cast<float4*>(dst), n4);
+}
 
 int flow_head_grid(int B) { return (B + 15) / 16 * (FH_D / 16); }
 
