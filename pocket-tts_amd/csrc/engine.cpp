@@ -171,6 +171,9 @@ Engine::Engine(const ptts_engine_config& cfg) {
   head_chain_ = !getenv("PTTS_HEAD_CHAIN_OFF");
   PTTS_REQUIRE(hx_floats(B) * 4 < (1ull << 31), "flow-head hand-off regions exceed 2 GB (lsd_decode_steps too large)");
   hx_ = dalloc(hx_floats(B));
+  // adaLN shift / scale in the chain's fragment order (written by the adaLN reduce), zeroed:
+  // rows past B in the last row group read finite values and are never stored
+  fhm_ = dalloc((size_t)lsd_ * ((B + 15) / 16) * (FDEPTH + 1) * 2 * 16 * FD);
   PTTS_HIP(hipMemset(hx_, 0xFF, hx_floats(B) * 4));  // empty (the launch ahead re-arms the used part)
   PTTS_HIP(hipDeviceSynchronize());                    // null-stream memset: see dalloc
   hctr_ = (int*)dalloc(4 * ((B + 15) / 16) + 4);
@@ -328,8 +331,7 @@ void Engine::finalize() {
     inw_t_ = (float*)p;
   }
   transpose(W(L_.input_linear), D, LDIM, inw_t_, stream_);
-  const bool wpack = !(getenv("PTTS_FH_WPACK") && !atoi(getenv("PTTS_FH_WPACK")));
-  if (!fhw_ && wpack && head_uniform_stride()) {  // every element is written by the packing below
+  if (!fhw_ && head_uniform_stride()) {  // every element is written by the packing below
     void* p = nullptr;
     PTTS_HIP(hipMalloc(&p, sizeof(float) * flow_head_packed_floats()));
     allocs_.push_back(p);
@@ -772,6 +774,8 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     if (use_head_chain(B)) {  // side job: empty the hand-off regions k_flow_head uses next
       a.fill = hx_;
       a.fill_n4 = (long)(hx_floats(B) / 4);
+      a.fhm = fhm_;
+      a.fhm_B = B;
     }
     push_rr(ops, "head.ada_reduce", a);
   }
@@ -797,8 +801,8 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     f.fin_w = W(L_.fin_w);
     f.fin_b = W(L_.fin_b);
     f.wp = fhw_;
+    f.fhm = fhm_;
     f.hx = hx_;
-    f.hx_rows = getenv("PTTS_FH_HX_ROWS") ? atoi(getenv("PTTS_FH_HX_ROWS")) : 0;
     f.ctr = hctr_;
     f.err = herr_;
     f.dbg = getenv("PTTS_HEAD_DBG") ? (unsigned long long*)strtoull(getenv("PTTS_HEAD_DBG"), nullptr, 0) : nullptr;

@@ -51,6 +51,10 @@ struct RowReduceArgs {
   // launch just ahead of k_flow_head), or nullptr
   float* fill;
   long fill_n4;
+  // the adaLN reduce's second copy of the ResBlock / final shift and scale columns in k_flow_head's
+  // fragment order (FlowHeadArgs::fhm) for a batch of fhm_B rows, or nullptr
+  float* fhm;
+  int fhm_B;
 };
 struct GemmArgs {
   int mode;    // 0 dense, 1 conv
@@ -224,11 +228,14 @@ struct FlowHeadArgs {
   // the 13 chain matrices (w0 / w2 of each ResBlock, then fin_w) in fragment order
   // (pack_flow_head): every operand load instruction reads one contiguous KB
   const float* wp;
+  // adaLN shift / scale in fragment order, float4 ((((((st RG + rg) 7 + i) 2 + t) 8 + w) 4 + j) 64 +
+  // lane) for Euler step st, row group rg, ResBlock i (6: final layer), t 0 shift / 1 scale
+  // (written by the adaLN reduce: RowReduceArgs::fhm); mods itself is read for the gates
+  const float* fhm;
   // hand-off regions: 13 per Euler step (x0, then u_i, x_{i+1} per ResBlock), each
   // [ceil(B/16)][32 column groups][16 rows][16 columns] (one producer tile = one contiguous KB),
   // all 0xFFFFFFFF (empty) at launch
   float* hx;
-  int hx_rows;  // 1: row-major [ceil(B/16) * 16][512] regions instead (PTTS_FH_HX_ROWS, A/B only)
   int* ctr;
   int* err;
   unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr

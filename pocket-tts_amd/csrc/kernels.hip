@@ -1479,6 +1479,16 @@ __device__ __forceinline__ float4 rr_value(const RowReduceArgs& a, int m, int n)
 }
 __device__ __forceinline__ void rr_store(const RowReduceArgs& a, int m, int n, float4 v) {
   if (a.Y) *reinterpret_cast<float4*>(a.Y + (long)m * a.ldy + n) = v;
+  if (a.fhm) {  // adaLN columns [shift | scale | gate] x 6 ResBlocks, then [shift | scale] (final)
+    const int st = m / a.fhm_B, b = m - st * a.fhm_B, RG = (a.fhm_B + 15) / 16;
+    const int i = min(n / (3 * FH_D), FH_DEPTH), rem = n - i * 3 * FH_D;
+    const int t = rem / FH_D, k = rem - t * FH_D;
+    if (t < 2) {
+      const long idx = (((((long)(st * RG + b / 16) * (FH_DEPTH + 1) + i) * 2 + t) * 8 + (k >> 6)) * 4 + ((k >> 4) & 3)) * 64 +
+                       (b & 15) + 16 * ((k >> 2) & 3);
+      reinterpret_cast<float4*>(a.fhm)[idx] = v;
+    }
+  }
   if (a.Y2) *reinterpret_cast<float4*>(a.Y2 + (long)m * a.ldy + n) = make_float4(elu1(v.x), elu1(v.y), elu1(v.z), elu1(v.w));
   if (a.euler) {
     float4* e = reinterpret_cast<float4*>(a.euler + (long)m * 32 + n);
@@ -2813,10 +2823,9 @@ __device__ __forceinline__ bool fh_empty(float4 v) {
 // consumer: this lane's 16 values of a region (byte offset `off`), re-read until none is empty.
 // The loop condition is wave-uniform; a timeout sets *err and stops waiting for the rest of the
 // launch (the frame is poisoned, fetch() reports it).
-__device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, int sj, float4 (&v)[4], int* err,
-                                         bool& dead) {
+__device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, float4 (&v)[4], int* err, bool& dead) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = fh_ld(r, off + sj * j);
+  for (int j = 0; j < 4; ++j) v[j] = fh_ld(r, off + FH_SJ * j);
   unsigned spins = 0;
   while (!dead) {
     bool ok = true;
@@ -2826,7 +2835,7 @@ __device__ __forceinline__ void fh_sweep(__amdgpu_buffer_rsrc_t r, int off, int 
     __builtin_amdgcn_s_sleep(1);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (fh_empty(v[j])) v[j] = fh_ld(r, off + sj * j);
+      if (fh_empty(v[j])) v[j] = fh_ld(r, off + FH_SJ * j);
     if (++spins > (1u << 20)) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       dead = true;
@@ -2942,10 +2951,8 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   // sweep / store byte offsets in a hand-off region ([RG][32][16][16]: tile (rg, cg) is one KB):
   // lane (c, G) of wave w reads row c, columns 16 (4w + j) + 4G..+3 of its row group; wave 0 lane
   // t stores its tile's row t/4, columns 4(t%4)..+3 at tile offset 16 t bytes
-  // (a.hx_rows: row-major [RG * 16][512] regions instead, 64 B per row and load)
-  const int aoff = a.hx_rows ? (arow * FH_D + k0) * 4 : (((rg * 32 + 4 * wave) * 16 + (arow - 16 * rg)) * 16 + 4 * G) * 4;
-  const int ooff = a.hx_rows ? (orow * FH_D + ocol) * 4 : ((rg * 32 + cg) * 256 + 4 * lane) * 4;
-  const int sj = a.hx_rows ? FH_KJ * 4 : FH_SJ;
+  const int aoff = (((rg * 32 + 4 * wave) * 16 + (arow - 16 * rg)) * 16 + 4 * G) * 4;
+  const int ooff = ((rg * 32 + cg) * 256 + 4 * lane) * 4;
   int q = 0;   // next hand-off region
   int gi = 0;  // GEMMs done (s_red buffer parity)
   bool dead = false;
@@ -2956,22 +2963,16 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
 
   // operand loaders (i: ResBlock, or FH_DEPTH for the FinalLayer)
   // fragment-packed matrix m (2i: w0 of ResBlock i, 2i + 1: its w2, 12: fin_w), this lane's float4 j
-  const float* wpl = a.wp ? a.wp + ((long)cg * FH_WAVES + wave) * 4 * 256 + 4 * lane : nullptr;
-  auto wfrag = [&](int m, int j) {
-    if (!a.wp) {  // row-major matrices of the blob (PTTS_FH_WPACK=0)
-      const float* W = (m == 2 * FH_DEPTH ? a.fin_w : (m & 1 ? a.w2 : a.w0) + (long)(m >> 1) * a.blk);
-      return f4ld(W + (long)(col0 + c) * FH_D + k0 + FH_KJ * j);
-    }
-    return f4ld(wpl + (long)m * (32 * FH_WAVES * 4 * 256) + j * 256);
-  };
-  auto load_ln_ops = [&](FhOps& o, const float* mods, int i) {
+  const float* wpl = a.wp + ((long)cg * FH_WAVES + wave) * 4 * 256 + 4 * lane;
+  auto wfrag = [&](int m, int j) { return f4ld(wpl + (long)m * (32 * FH_WAVES * 4 * 256) + j * 256); };
+  auto load_ln_ops = [&](FhOps& o, const float* mods, int i, int stp) {
     if (i == FH_DEPTH && !fin) return;
-    const float* mr = mods + (long)arow * a.ldm + (long)i * 3 * FH_D + k0;
+    const float* mp = a.fhm + (((((long)(stp * RG + rg) * (FH_DEPTH + 1) + i) * 2) * 8 + wave) * 4 * 64 + lane) * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       o.w[j] = wfrag(2 * i, j);
-      o.sf[j] = f4ld(mr + FH_KJ * j);
-      o.sc[j] = f4ld(mr + FH_D + FH_KJ * j);
+      o.sf[j] = f4ld(mp + j * 256);
+      o.sc[j] = f4ld(mp + 8 * 4 * 256 + j * 256);
     }
     if (wave == 0) o.e0 = f4ld((i < FH_DEPTH ? a.b0 + (long)i * a.blk : a.fin_b) + ocol);
   };
@@ -3013,7 +3014,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
     if (st == 0) {
       // the first phases' operands, then the ResBlock LayerNorm affines into LDS (first read
       // after the first LayerNorm's barrier)
-      load_ln_ops(p0, mods, 0);
+      load_ln_ops(p0, mods, 0, st);
       load_mlp2_ops(p2, mods, 0);
 #pragma unroll
       for (int i = 0; i < FH_DEPTH; ++i)
@@ -3028,23 +3029,23 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       // ---- h = modulate(LN(x)), u = silu(h W0^T + b0)
       float4 v[4];
       FH_STAMP();
-      fh_sweep(hr, (q - 1) * rstride + aoff, sj, v, a.err, dead);
+      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
       FH_STAMP();
       fh_ln(v, s_st, wave, c, G, &s_ln[i][0][k0], &s_ln[i][1][k0], p0.sc, p0.sf);
       FH_STAMP();
       float4 r = fh_gemm(v, p0.w, s_red2[gi++ & 1], wave, c, G, lane);
       FH_STAMP();
-      if (wave != 0) load_ln_ops(p0, mods, i + 1);
+      if (wave != 0) load_ln_ops(p0, mods, i + 1, st);
       if (wave == 0) {
         const float4 bb = p0.e0;
         const float4 u = make_float4(silu(r.x + bb.x), silu(r.y + bb.y), silu(r.z + bb.z), silu(r.w + bb.w));
         if (ostore) fh_put(hr, q * rstride + ooff, u);
-        load_ln_ops(p0, mods, i + 1);
+        load_ln_ops(p0, mods, i + 1, st);
       }
       FH_STAMP();
       ++q;
       // ---- x += gate * (u W2^T + b2)
-      fh_sweep(hr, (q - 1) * rstride + aoff, sj, v, a.err, dead);
+      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
       FH_STAMP();
       r = fh_gemm(v, p2.w, s_red2[gi++ & 1], wave, c, G, lane);
       FH_STAMP();
@@ -3065,23 +3066,23 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
       if (wave == 0) cv = fh_ld(cr, off);  // latent before this Euler step (read ahead of the sweep)
       float4 v[4];
-      fh_sweep(hr, (q - 1) * rstride + aoff, sj, v, a.err, dead);
+      fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
       if (wave != 0 && more) load_mlp2_ops(p2, nmods, 0);
       fh_ln(v, s_st, wave, c, G, nullptr, nullptr, p0.sc, p0.sf);
       const float4 r = fh_gemm(v, p0.w, s_red2[gi++ & 1], wave, c, G, lane);
-      if (wave != 0 && more) load_ln_ops(p0, nmods, 0);
+      if (wave != 0 && more) load_ln_ops(p0, nmods, 0, st + 1);
       if (wave == 0) {
         const float e = a.euler_scale;
         const float4 o = f4add(r, p0.e0);
         if (ostore) fh_st(cr, off, make_float4(cv.x + o.x * e, cv.y + o.y * e, cv.z + o.z * e, cv.w + o.w * e));
         if (more) fh_publish(cc);
         if (more) {
-          load_ln_ops(p0, nmods, 0);
+          load_ln_ops(p0, nmods, 0, st + 1);
           load_mlp2_ops(p2, nmods, 0);
         }
       }
     } else if (more) {
-      load_ln_ops(p0, nmods, 0);
+      load_ln_ops(p0, nmods, 0, st + 1);
       load_mlp2_ops(p2, nmods, 0);
     }
   }
