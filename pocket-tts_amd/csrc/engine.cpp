@@ -1017,10 +1017,10 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   const bool big = B >= 16;
   // Tiles: the tools/gemm_bench.hip choices (each launch alone on the chip, B = 32), except where
   // the pipelined step (tools/sweep_env.sh over PTTS_OVR, steady step time) prefers lighter
-  // workgroups beside the concurrent front part: the register-blocked res_conv3 tiles of stages
-  // 0 and 1 (k_gemm_rb, 2x2 accumulators per wave) give way to the 64x64 LDS-DMA tile, steady
-  // step 0.6748 -> 0.6639 ms. Tiles that are faster alone under the per-CU cap (tools/
-  // back_tune.py: 32 us less back time in all) each made the pipelined step slower.
+  // workgroups beside the concurrent front part (the choices move with the front/back balance:
+  // see the res_conv3 note below). Tiles that were faster alone under the per-CU cap (tools/
+  // back_tune.py: 32 us less back time in all) each made the pipelined step slower while the
+  // front part was the longer one.
   int l_c0 = 6, s_c0 = 8;  // conv0 tile / split-K (PTTS_OVR may change them)
   tile_override("seanet.conv0", l_c0, s_c0);
   if (s_c0 > 1) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the reduce (every B:
@@ -1048,7 +1048,10 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     const std::string p = "seanet.up" + std::to_string(i);
     // per-stage tiles (tools/gemm_bench.hip, rb.* cases, B = 32; see above for pipelined)
     const int l_tr = big ? (i == 0 ? 20 : (i == 1 ? 13 : 22)) : 0;
-    const int l_r3 = !big ? 0 : i == 2 ? 14 : pipeline_ ? 6 : (i == 0 ? 18 : 20);
+    // stages 0-1 k3 convs: the register-blocked tiles in pipelined stepping too since the front
+    // part got shorter (flow-head chain 74 -> 47 us): steady step 0.626 -> 0.608 ms (medians of 3);
+    // while the front was the longer part, the 64x64 LDS-DMA tile (6) was 1.6 % faster
+    const int l_r3 = !big ? 0 : i == 2 ? 14 : (i == 0 ? 18 : 20);
     // stage 2's k1 conv (M = 32 * 3840 rows, N = 64): 128x64 register-blocked LDS-DMA tile in
     // pipelined stepping, steady step 0.6310 -> 0.6188 ms (medians of 4; its 64x64 / 128x128
     // neighbours 22 / 21 measured 0.644 / 0.652)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Bench sweep over environment combinations, interleaved repeats:
-#   COMBOS="A=1,B=0 A=0,B=1 -" [REPS=3] bash tools/sweep_combo.sh   ("-" = nothing set)
+#   COMBOS="A=1+B=0 A=0+B=1 -" [REPS=3] bash tools/sweep_combo.sh   ("-" = nothing set)
 # One line per run, then the median steady ms per combination. Also records head.chain (isolated).
 set -u
 cd "$(dirname "$0")/.."
@@ -9,7 +9,7 @@ rm -f gpurun_out/combo_all.txt
 for r in $(seq 1 "${REPS:-3}"); do
   for c in $COMBOS; do
     envs=()
-    [ "$c" != "-" ] && IFS=',' read -ra envs <<< "$c"
+    [ "$c" != "-" ] && IFS='+' read -ra envs <<< "$c"
     env "${envs[@]}" timeout -k 10 200 python bench.py --no-cpu-baseline --no-quant-variant --no-latency \
         ${BENCH_ARGS:-} > gpurun_out/combo.log 2>&1 || { echo "$c failed"; tail -5 gpurun_out/combo.log; exit 1; }
     python - "$c" gpurun_out/combo.log <<'PY'
