@@ -568,6 +568,22 @@ void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowRed
   ops.push_back({name, [r](hipStream_t s) { row_reduce(r, s); }});
 }
 
+// Y[M][N] = X[M][K] W[N][K]^T through rocBLAS (row-major as column-major Y^T = W^T X^T)
+void Engine::blas_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,
+                     int K, float* Y) {
+  PTTS_REQUIRE(blas_ != nullptr, "rocBLAS handle unavailable");
+  rocblas_handle h = (rocblas_handle)blas_;
+  ops.push_back({name,
+                 [=](hipStream_t s) {
+                   const float one = 1.f, zero = 0.f;
+                   if (rocblas_set_stream(h, s) != rocblas_status_success ||
+                       rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &one, Wt, K, X, K,
+                                     &zero, Y, N) != rocblas_status_success)
+                     throw Error(PTTS_ERR_HIP, "rocblas_sgemm failed");
+                 },
+                 2.0 * M * N * K, 4.0 * ((double)N * K + (double)M * K + (double)M * N)});
+}
+
 void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,
                       int K, const float* bias, int act, const float* rscale, const float* R, float* Y, int layout) {
   PTTS_REQUIRE(K % 32 == 0, "GEMM K must be a multiple of 32");
@@ -941,9 +957,16 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     // steady step 0.6661 -> 0.6587 ms, tools/sweep_env.sh over PTTS_OVR)
     const bool fat = MR >= 256;
     const int fat_layout = pipeline_ ? 6 : 15;
+    // Mimi GEMMs through rocBLAS (fat shapes only), PTTS_BACK_BLAS bits: 1 qkv, 2 ff1 (+ a GELU
+    // pass), 4 ff2 (one unsplit product into the existing reduce). Pipelined default 4: once the
+    // back part bounded the step, ff2 on rocBLAS measured 0.6205 -> 0.6028 and 0.6124 -> 0.6070
+    // ms (medians of 3-4, two boxes); qkv +0.7 % / -0.4 %, ff1 slower, all three 0.6103
+    const int bb = !(fat && blas_) ? 0 : getenv("PTTS_BACK_BLAS") ? atoi(getenv("PTTS_BACK_BLAS")) : pipeline_ ? 4 : 0;
     {  // QKV: one pass, 64x64 LDS-DMA tiles once there are enough rows (tools/gemm_bench.hip c2.mimi.qkv)
-      dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_,
-               fat ? fat_layout : 0);
+      if (bb & 1) blas_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, mqkv_);
+      else
+        dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_,
+                 fat ? fat_layout : 0);
       const float* qkv = mqkv_;
       float* Q = mq_;
       float* O = mo_;
@@ -960,8 +983,22 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       float* h = mh_;
       ops.push_back({p + ".ln2", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
     }
-    dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
-             fat ? fat_layout : 0);
+    if (bb & 2) {
+      PTTS_REQUIRE((size_t)MR * MFF <= mpcap_, "back split-K slab buffer too small");
+      blas_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, mpartial_);
+      RowReduceArgs g{};
+      g.P = mpartial_;
+      g.S = 1;
+      g.M = MR;
+      g.N = MFF;
+      g.act = ACT_GELU;
+      g.Y = mu_;
+      g.ldy = MFF;
+      ops.push_back({p + ".ff1_gelu", [g](hipStream_t s) { row_reduce(g, s); }});
+    } else {
+      dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
+               fat ? fat_layout : 0);
+    }
     {  // K = 2048, split-K; LayerScale + residual (+ the next layer's norm1) in the reduce. Fat:
        // 64x64 LDS-DMA tiles, 4 slices; few rows (B < 16, the first-chunk path): 32x32 tiles, 8
        // slices (16 -> 128 workgroups: 18.2 -> ~7 us at B = 1, and no separate norm1 launch)
@@ -982,9 +1019,12 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       a.W = W(t.l2);
       a.S = S;
       a.partial = mpartial_;
+      if (bb & 4) S = 1;
       PTTS_REQUIRE((size_t)S * MR * MD <= mpcap_, "back split-K slab buffer too small");
-      ops.push_back({p + ".ff2_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * MD * MFF,
-                     4.0 * ((double)MD * MFF + (double)MR * MFF + 2.0 * MR * MD)});
+      if (bb & 4) blas_op(ops, p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, mpartial_);
+      else
+        ops.push_back({p + ".ff2_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * MD * MFF,
+                       4.0 * ((double)MD * MFF + (double)MR * MFF + 2.0 * MR * MD)});
       RowReduceArgs r{};
       r.P = mpartial_;
       r.S = S;

@@ -84,6 +84,8 @@ class Engine {
                int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases, const float* bias,
                const float* R, float* Y, int T_out, int tstride, int layout = 0, int elu_out = 0,
                float* Y2 = nullptr, int ksplit = 1);
+  void blas_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N, int K,
+               float* Y);
   void dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N, int K,
                 const float* bias, int act, const float* rscale, const float* R, float* Y,
                 int layout = 0);
