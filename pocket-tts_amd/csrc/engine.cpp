@@ -120,7 +120,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
     pcm_[q] = dalloc((size_t)B * FRAME);
   }
   // back part's own split-K slabs: Mimi QKV (2 slabs), Mimi ff2 (4), SEANet conv0 (8), convtr0 (4)
-  mpcap_ = std::max({(size_t)2 * B * UP * 3 * MD, (size_t)8 * B * UP * MD, (size_t)4 * B * UP * RATIOS[0] * (MD / 2)});
+  mpcap_ = std::max({(size_t)2 * B * UP * 3 * MD, (size_t)8 * B * UP * MD, (size_t)4 * B * UP * RATIOS[0] * (MD / 2),
+                     (size_t)B * FRAME * 64});  // the last: stage-2 k1 conv as one rocBLAS product
   mpartial_ = dalloc(mpcap_);
 
   // streaming conv histories (SEANetDecoder, seanet.rs:307-402): source T, channels, rows kept
@@ -960,7 +961,9 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     // Mimi GEMMs through rocBLAS (fat shapes only), PTTS_BACK_BLAS bits: 1 qkv, 2 ff1 (+ a GELU
     // pass), 4 ff2 (one unsplit product into the existing reduce). Pipelined default 4: once the
     // back part bounded the step, ff2 on rocBLAS measured 0.6205 -> 0.6028 and 0.6124 -> 0.6070
-    // ms (medians of 3-4, two boxes); qkv +0.7 % / -0.4 %, ff1 slower, all three 0.6103
+    // ms (medians of 3-4, two boxes); qkv +0.7 % / -0.4 %, ff1 slower, all three 0.6103; bit 8
+    // (out + LayerScale/residual reduce) 0.6146 against 0.6121. Bits 16 / 32 (SEANet k1 convs,
+    // below) measured 0.842 / 0.683 ms: those skinny products stay on the hand-written tiles
     const int bb = !(fat && blas_) ? 0 : getenv("PTTS_BACK_BLAS") ? atoi(getenv("PTTS_BACK_BLAS")) : pipeline_ ? 4 : 0;
     {  // QKV: one pass, 64x64 LDS-DMA tiles once there are enough rows (tools/gemm_bench.hip c2.mimi.qkv)
       if (bb & 1) blas_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, mqkv_);
@@ -977,7 +980,23 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
         ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, MR, MNH, mmap, kv, MCTX, UP, O, s); }});
       }
     }
-    dense_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, nullptr, ACT_NONE, W(t.ls1), mx_, mx_);
+    if (bb & 8) {  // out + LayerScale + residual: one rocBLAS product, the epilogue in a reduce
+      blas_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, mpartial_);
+      RowReduceArgs g{};
+      g.P = mpartial_;
+      g.S = 1;
+      g.M = MR;
+      g.N = MD;
+      g.gate = W(t.ls1);
+      g.ldg = 0;
+      g.R = mx_;
+      g.ldr = MD;
+      g.Y = mx_;
+      g.ldy = MD;
+      ops.push_back({p + ".out_reduce", [g](hipStream_t s) { row_reduce(g, s); }});
+    } else {
+      dense_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, nullptr, ACT_NONE, W(t.ls1), mx_, mx_);
+    }
     {
       const float *x = mx_, *w = W(t.n2w), *b = W(t.n2b);
       float* h = mh_;
@@ -1055,6 +1074,8 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   // 2-tap conv over rows (x[q-1], x[q]) whose output row q is the r time rows q*r .. q*r+r-1 of
   // the channels-last output, N = r * Cout (packed [r][Cout][2][Cin] = [r*Cout][2*Cin]).
   const bool big = B >= 16;
+  // PTTS_BACK_BLAS bits for the SEANet k1 convs (rocBLAS product + reduce): 16 stage 2, 32 stages 0-1
+  const int bbs = getenv("PTTS_BACK_BLAS") ? atoi(getenv("PTTS_BACK_BLAS")) : 0;
   // Tiles: the tools/gemm_bench.hip choices (each launch alone on the chip, B = 32), except where
   // the pipelined step (tools/sweep_env.sh over PTTS_OVR, steady step time) prefers lighter
   // workgroups beside the concurrent front part (the choices move with the front/back balance:
@@ -1119,8 +1140,24 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     ch /= 2;
     conv_op(ops, p + ".res_conv3", ce_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 0, W(L_.dra_w[i]), ch / 2, 3, 1,
             W(L_.dra_b[i]), nullptr, cv_[i], T, 1, l_r3, 1);
-    conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 0, W(L_.drb_w[i]), ch, 1, 1, W(L_.drb_b[i]),
-            cb_[i], ca_[i], T, 1, l_r1, 1);
+    if (big && blas_ && (bbs & (i == 2 ? 16 : 32))) {  // k1 conv = plain GEMM: rocBLAS, then bias + skip + ELU
+      PTTS_REQUIRE((size_t)B * T * ch <= mpcap_, "back split-K slab buffer too small");
+      blas_op(ops, p + ".res_conv1", cv_[i], B * T, W(L_.drb_w[i]), ch, ch / 2, mpartial_);
+      RowReduceArgs g{};
+      g.P = mpartial_;
+      g.S = 1;
+      g.M = B * T;
+      g.N = ch;
+      g.bias = W(L_.drb_b[i]);
+      g.R = cb_[i];
+      g.ldr = ch;
+      g.Y2 = ca_[i];
+      g.ldy = ch;
+      ops.push_back({p + ".res_conv1_reduce", [g](hipStream_t s) { row_reduce(g, s); }});
+    } else {
+      conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 0, W(L_.drb_w[i]), ch, 1, 1,
+              W(L_.drb_b[i]), cb_[i], ca_[i], T, 1, l_r1, 1);
+    }
     cin_buf = ca_[i];
   }
   {
