@@ -2936,7 +2936,11 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, G = lane >> 4;
   const int RG = (a.B + 15) / 16;
-  const int rg = blockIdx.x % RG, cg = blockIdx.x / RG;
+  // XCD-aware placement (speed only: blocks b and b + 8 are observed to share an XCD's L2): the
+  // RG row groups of a column group sit on one XCD, so each weight fragment is fetched into that
+  // L2 once and read by all RG of them (column groups 4x .. 4x+3 on XCD slot x)
+  const int xs = blockIdx.x & 7, xr = blockIdx.x >> 3;
+  const int rg = xr % RG, cg = 4 * xs + xr / RG;
   const int col0 = 16 * cg;
   const int arow = min(16 * rg + c, a.B - 1);  // A-operand row of this lane (clamped; rows >= B unused)
   const int k0 = 64 * wave + 4 * G;            // this lane's 16 k: k0 + FH_KJ j + 0..3, j < 4

@@ -11,7 +11,7 @@ for r in $(seq 1 "${REPS:-3}"); do
     envs=()
     [ "$c" != "-" ] && IFS='+' read -ra envs <<< "$c"
     env "${envs[@]}" timeout -k 10 200 python bench.py --no-cpu-baseline --no-quant-variant --no-latency \
-        ${BENCH_ARGS:-} > gpurun_out/combo.log 2>&1 || { echo "$c failed"; tail -5 gpurun_out/combo.log; exit 1; }
+        ${BENCH_ARGS:-} > gpurun_out/combo.log 2>&1 || { echo "$c failed"; tail -2 gpurun_out/combo.log; continue; }
     python - "$c" gpurun_out/combo.log <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
