@@ -66,6 +66,12 @@ typedef struct ptts_engine_config {
                                (row, K slice). Not a reference numeric (the reference has no fp8;
                                BASELINE configs[4]): gated on accuracy vs the f32 path. Requires
                                weight_quant = PTTS_QUANT_NONE. 0 = f32 (default). */
+  const char* cfg_yaml;     /* the reference's model config (config/b6369a24.yaml; TTSModel::load's
+                               config, config.rs:111-115), or NULL. The kernels implement the
+                               b6369a24 dimensions; when given, every hot-path key of the file must
+                               be present and equal them, or creation fails (PTTS_ERR_INVALID,
+                               naming the key): another variant is a rebuild. Checked, not read
+                               for shapes. ptts_config_check() is the same check alone. */
 } ptts_engine_config;
 
 #define PTTS_QUANT_NONE 0
@@ -115,6 +121,9 @@ int ptts_engine_fp8_matrices(ptts_engine* e);
 
 /* TTSModel::load / load_with_params_device (tts_model.rs:59-106,182-236). */
 int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out);
+/* The cfg_yaml check of ptts_engine_create without an engine (no GPU needed): 0 if the model
+ * config at `cfg_yaml` states the dimensions this build implements (config.rs:1-124 keys). */
+int ptts_config_check(const char* cfg_yaml);
 /* Second half of create when cfg->defer_weights = 1 (derived tables, time embeddings). */
 int ptts_engine_finalize(ptts_engine* e);
 void ptts_engine_destroy(ptts_engine* e);

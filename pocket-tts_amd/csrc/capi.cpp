@@ -109,6 +109,13 @@ int ptts_quant_applies(const char* name, size_t numel, int weight_quant) {
 int ptts_engine_int8_matrices(ptts_engine* e) { return (e && e->impl) ? e->impl->int8_matrices() : 0; }
 int ptts_engine_fp8_matrices(ptts_engine* e) { return (e && e->impl) ? e->impl->fp8_matrices() : 0; }
 
+int ptts_config_check(const char* cfg_yaml) {
+  return guard([&] {
+    if (!cfg_yaml || !*cfg_yaml) throw ptts::Error(PTTS_ERR_INVALID, "null model config path");
+    ptts::check_model_config(cfg_yaml);
+  });
+}
+
 int ptts_engine_create(const ptts_engine_config* cfg, ptts_engine** out) {
   return guard([&] {
     if (!cfg || !out) throw ptts::Error(PTTS_ERR_INVALID, "null argument");

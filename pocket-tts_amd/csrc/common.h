@@ -27,4 +27,8 @@ struct Error : std::runtime_error {
     if (!(cond)) throw ::ptts::Error(PTTS_ERR_INVALID, std::string(msg)); \
   } while (0)
 
+// model-config check (config.cpp): throws Error(PTTS_ERR_INVALID) naming the first key that
+// differs from the compiled b6369a24 dimensions; a null or empty path is accepted
+void check_model_config(const char* path);
+
 }  // namespace ptts

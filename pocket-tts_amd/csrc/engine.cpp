@@ -63,6 +63,7 @@ float* Engine::dalloc(size_t n) {
 }
 
 Engine::Engine(const ptts_engine_config& cfg) {
+  check_model_config(cfg.cfg_yaml);  // before any device work
   PTTS_REQUIRE(cfg.max_slots >= 1 && cfg.max_slots <= 256, "max_slots must be in [1, 256]");
   PTTS_REQUIRE(cfg.max_ctx >= 16 && cfg.max_ctx <= 8192, "max_ctx must be in [16, 8192]");
   PTTS_REQUIRE(cfg.lsd_decode_steps >= 1 && cfg.lsd_decode_steps <= 64, "lsd_decode_steps must be in [1, 64]");

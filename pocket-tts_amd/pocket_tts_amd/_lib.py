@@ -36,6 +36,7 @@ class EngineConfig(C.Structure):
         ("pipeline", C.c_int),
         ("weight_quant", C.c_int),
         ("fp8_gemm", C.c_int),
+        ("cfg_yaml", C.c_char_p),
     ]
 
 
@@ -61,6 +62,7 @@ SIGNATURES = [
     ("ptts_engine_int8_matrices", C.c_int, [C.c_void_p]),
     ("ptts_engine_fp8_matrices", C.c_int, [C.c_void_p]),
     ("ptts_engine_create", C.c_int, [C.POINTER(EngineConfig), C.POINTER(C.c_void_p)]),
+    ("ptts_config_check", C.c_int, [C.c_char_p]),
     ("ptts_engine_finalize", C.c_int, [C.c_void_p]),
     ("ptts_engine_load_blob", C.c_int, [C.c_void_p, F32P, C.c_size_t]),
     ("ptts_engine_destroy", None, [C.c_void_p]),

@@ -67,16 +67,18 @@ class StepResult:
 class Engine:
     def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
                  seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
-                 defer_weights: bool = False, pipeline: bool = False, weight_quant: int = 0, fp8_gemm: bool = False):
+                 defer_weights: bool = False, pipeline: bool = False, weight_quant: int = 0, fp8_gemm: bool = False,
+                 cfg_yaml: str | None = None):
         """pipeline=True: overlapped stepping, each step() returns the frame produced by the
         previous call (see ptts_engine_config.pipeline). weight_quant: QUANT_NONE / QUANT_FLOW_LM /
         QUANT_ALL, the reference's simulated int8 weight quantization (quantize.rs), with the
         FlowLM step GEMMs streaming int8 codes. fp8_gemm=True: the large FlowLM step GEMMs run as
-        fp8 W8A8 MFMA (accuracy-gated; see ptts_engine_config.fp8_gemm)."""
+        fp8 W8A8 MFMA (accuracy-gated; see ptts_engine_config.fp8_gemm). cfg_yaml: the reference's
+        model config (config/b6369a24.yaml), checked against the compiled dimensions."""
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
                            weight_blob or None, int(defer_weights), int(pipeline), int(weight_quant),
-                           int(fp8_gemm))
+                           int(fp8_gemm), cfg_yaml.encode() if cfg_yaml else None)
         h = C.c_void_p()
         check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
         self.handle = h
@@ -85,6 +87,12 @@ class Engine:
         self.max_ctx = max_ctx
         self.lsd_decode_steps = lsd_decode_steps
         self.pipeline = bool(pipeline)
+
+    @staticmethod
+    def check_config(cfg_yaml: str) -> None:
+        """Raise PocketTTSError unless the reference model config at `cfg_yaml` states the
+        dimensions this build implements (b6369a24); no GPU needed (ptts_config_check)."""
+        check(lib().ptts_config_check(cfg_yaml.encode()))
 
     @staticmethod
     def weight_blob_bytes() -> int:
