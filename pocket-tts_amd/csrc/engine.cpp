@@ -124,6 +124,9 @@ Engine::Engine(const ptts_engine_config& cfg) {
   mpcap_ = std::max({(size_t)2 * B * UP * 3 * MD, (size_t)8 * B * UP * MD, (size_t)4 * B * UP * RATIOS[0] * (MD / 2),
                      (size_t)B * FRAME * 64});  // the last: stage-2 k1 conv as one rocBLAS product
   mpartial_ = dalloc(mpcap_);
+  // explicit conv operands for the rocBLAS convs (PTTS_BACK_BLAS 64 / 128): the largest is the
+  // stage-2 transposed conv's [B * 480][2 * 128]
+  mcol_ = dalloc((size_t)B * 480 * 2 * 128);
 
   // streaming conv histories (SEANetDecoder, seanet.rs:307-402): source T, channels, rows kept
   const int hT[8] = {16, 16, 96, 96, 480, 480, 1920, 1920};
@@ -1075,7 +1078,10 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   // 2-tap conv over rows (x[q-1], x[q]) whose output row q is the r time rows q*r .. q*r+r-1 of
   // the channels-last output, N = r * Cout (packed [r][Cout][2][Cin] = [r*Cout][2*Cin]).
   const bool big = B >= 16;
-  // PTTS_BACK_BLAS bits for the SEANet k1 convs (rocBLAS product + reduce): 16 stage 2, 32 stages 0-1
+  // PTTS_BACK_BLAS bits for SEANet convs as rocBLAS products (+ reduce): 16 stage-2 k1 conv, 32
+  // stage-0/1 k1 convs, 64 transposed convs and 128 conv0 (both on an explicit im2col operand).
+  // All measured slower in the pipelined step (0.842 / 0.683 / 0.667 / 0.622 against 0.603-0.612
+  // ms): the hand-written implicit-GEMM tiles stay.
   const int bbs = getenv("PTTS_BACK_BLAS") ? atoi(getenv("PTTS_BACK_BLAS")) : 0;
   // Tiles: the tools/gemm_bench.hip choices (each launch alone on the chip, B = 32), except where
   // the pipelined step (tools/sweep_env.sh over PTTS_OVR, steady step time) prefers lighter
@@ -1085,10 +1091,19 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   // front part was the longer one.
   int l_c0 = 6, s_c0 = 8;  // conv0 tile / split-K (PTTS_OVR may change them)
   tile_override("seanet.conv0", l_c0, s_c0);
-  if (s_c0 > 1) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the reduce (every B:
-                   // at B = 1 the unsplit launch had 16 workgroups, 27.4 us)
-    conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
-            nullptr, 16, 1, l_c0, 0, nullptr, s_c0);
+  const bool conv_blas = big && blas_ && (bbs & 128);
+  if (s_c0 > 1 || conv_blas) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the
+                                // reduce (every B: at B = 1 the unsplit launch had 16 workgroups, 27.4 us)
+    if (conv_blas) {  // explicit operand + one rocBLAS product
+      s_c0 = 1;
+      const float *X = mx_, *H = hist_[0];
+      float* A = mcol_;
+      ops.push_back({"seanet.conv0_im2col", [=](hipStream_t s) { im2col(X, H, B, 16, 1, 6, 512, 7, A, s); }});
+      blas_op(ops, "seanet.conv0", mcol_, B * 16, W(L_.dc0_w), 512, 7 * 512, mpartial_);
+    } else {
+      conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
+              nullptr, 16, 1, l_c0, 0, nullptr, s_c0);
+    }
     RowReduceArgs r{};
     r.P = mpartial_;
     r.S = s_c0;
@@ -1120,7 +1135,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     const int l_r1 = !big ? 0 : (i == 2 && pipeline_) ? 23 : 6;
     int l_t0 = 6, s_t0 = i == 0 ? 4 : 1;  // split-K of the first transposed conv (PTTS_OVR may change it)
     if (i == 0) tile_override(p + ".convtr", l_t0, s_t0);
-    if (big && i == 0 && s_t0 > 1) {  // M = 16 B rows only: 4-way split-K fills the chip; bias + dual store in the reduce
+    if (big && i == 0 && s_t0 > 1 && !(blas_ && (bbs & 64))) {  // M = 16 B rows only: 4-way split-K fills the chip; bias + dual store in the reduce
       conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1], 1, 1, 0, W(L_.dtr_w[0]), r * (ch / 2), 2, 1, nullptr,
               nullptr, nullptr, T, 1, l_t0, 0, nullptr, s_t0);
       RowReduceArgs rr{};
@@ -1131,6 +1146,23 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       rr.bias = trb_[0];
       rr.Y = cb_[0];
       rr.Y2 = ce_[0];
+      rr.ldy = r * (ch / 2);
+      ops.push_back({p + ".convtr_reduce", [rr](hipStream_t s) { row_reduce(rr, s); }});
+    } else if (big && blas_ && (bbs & 64)) {  // explicit [x(q-1) | x(q)] rows + one rocBLAS product
+      const float *X = cin_buf, *H = hist_[1 + 2 * i];
+      float* A = mcol_;
+      const int Tc = T, cc = ch;
+      PTTS_REQUIRE((size_t)B * T * r * (ch / 2) <= mpcap_, "back split-K slab buffer too small");
+      ops.push_back({p + ".convtr_im2col", [=](hipStream_t s) { im2col(X, H, B, Tc, 1, 1, cc, 2, A, s); }});
+      blas_op(ops, p + ".convtr", mcol_, B * T, W(L_.dtr_w[i]), r * (ch / 2), 2 * ch, mpartial_);
+      RowReduceArgs rr{};
+      rr.P = mpartial_;
+      rr.S = 1;
+      rr.M = B * T;
+      rr.N = r * (ch / 2);
+      rr.bias = trb_[i];
+      rr.Y = cb_[i];
+      rr.Y2 = ce_[i];
       rr.ldy = r * (ch / 2);
       ops.push_back({p + ".convtr_reduce", [rr](hipStream_t s) { row_reduce(rr, s); }});
     } else {

@@ -243,6 +243,9 @@ struct FlowHeadArgs {
 // Launches issued while a cap > 0 is set reserve dynamic LDS so that at most `cap` workgroups of
 // each kernel share a CU (0 = no cap). Process-wide; the engine sets it around graph capture.
 void set_wg_cap(int cap);
+// conv operand rows as an explicit [B * T_in / stride][taps * cin] matrix (cin % 4 == 0)
+void im2col(const float* X, const float* H, int B, int T_in, int stride, int P, int cin, int taps, float* A,
+            hipStream_t s);
 bool flow_head_fits(int B);
 // fragment-order copy of the chain's matrices for FlowHeadArgs::wp: 12 * 512 * 512 + 32 * 512 floats
 size_t flow_head_packed_floats();

@@ -3157,6 +3157,30 @@ void transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) 
   hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, cols, dst);
 }
 
+// Implicit-GEMM conv operand made explicit (for a library GEMM): A[m][j cin + c] with m = b Tq + q
+// is input time t = q stride + j - P of utterance b: X[b T_in + t][c] for t >= 0, else the
+// history H[b][P + t][c] (the same rule as k_gemm_glds's MODE 1 operand loader).
+__global__ void k_im2col(const float* __restrict__ X, const float* __restrict__ H, int T_in, int Tq, int stride, int P,
+                         int cin, int taps, long n4, float4* __restrict__ A) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n4) return;
+  const int K4 = taps * cin / 4;
+  const long m = e / K4;
+  const int k = (int)(e - m * K4) * 4;
+  const int j = k / cin, c = k - j * cin;
+  const int b = (int)(m / Tq), q = (int)(m - (long)b * Tq);
+  const int t = q * stride + j - P;
+  const float* src = t >= 0 ? X + ((long)b * T_in + t) * cin + c : H + ((long)b * P + (P + t)) * cin + c;
+  A[e] = *reinterpret_cast<const float4*>(src);
+}
+
+void im2col(const float* X, const float* H, int B, int T_in, int stride, int P, int cin, int taps, float* A,
+            hipStream_t s) {
+  const long n4 = (long)B * (T_in / stride) * taps * cin / 4;
+  hipLaunchKernelGGL(k_im2col, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, X, H, T_in, T_in / stride, stride,
+                     P, cin, taps, n4, reinterpret_cast<float4*>(A));
+}
+
 bool flow_head_fits(int B) { return B >= 1 && B <= 128; }
 
 size_t flow_head_packed_floats() { return (size_t)2 * FH_DEPTH * FH_D * FH_D + (size_t)FH_L * FH_D; }
