@@ -1242,8 +1242,19 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
   PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   // back part of a pipelined step: its launches leave room for the concurrent front part
   set_wg_cap(part == 1 && pipeline_ ? back_cap_ : 0);
+  // per-op cap override for back-part launches: PTTS_OP_CAP="name=cap,..." (tuning)
+  const char* opcap = part == 1 && pipeline_ ? getenv("PTTS_OP_CAP") : nullptr;
   try {
-    for (const Op& op : ops) op.fn(stream_);
+    for (const Op& op : ops) {
+      if (opcap) {
+        int cap = back_cap_;
+        const std::string e(opcap), key = op.name + "=";
+        const size_t at = e.find(key);
+        if (at != std::string::npos && (at == 0 || e[at - 1] == ',')) cap = atoi(e.c_str() + at + key.size());
+        set_wg_cap(cap);
+      }
+      op.fn(stream_);
+    }
     if (part == 0) {  // the hand-off timeout word, read by fetch() without a device round trip
       PTTS_HIP(hipMemcpyAsync(h_err_, herr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
     } else {  // the frame of this buffer leaves HBM inside the step (fetch() reads host memory)
