@@ -348,33 +348,39 @@ def test_batch_scheduler_matches_oracle(oracle):
         eng.close()
 
 
-@pytest.mark.parametrize("lsd", [1, 3])
-def test_flow_head_chain_two_row_groups(oracle, lsd):
+@pytest.mark.parametrize("B,lsd", [(20, 1), (20, 3), (45, 1), (128, 1)])
+def test_flow_head_chain_two_row_groups(oracle, B, lsd):
     """B = 20: the persistent flow-head launch (k_flow_head) runs two 16-row groups, the second
-    ragged (4 valid rows). The launch is first replayed alone in a timing loop, which must leave
-    its hand-off counters re-armed; then every row of every step equals its oracle run."""
+    ragged (4 valid rows); B = 45 three (the XCD-aware block -> (row group, column group) map with
+    an odd group count, 13 valid rows in the last), B = 128 its largest grid (8 groups, 256
+    workgroups; sampled rows). The launch is first replayed alone in a timing loop, which must
+    leave its hand-off counters re-armed; then every checked row of every step equals its oracle
+    run."""
     import pocket_tts_amd as pt
     d = load_golden("e2e_lsd1.safetensors")
     rng = np.random.default_rng(11)
-    B, steps = 20, 3
+    steps = 3
+    rows = range(B) if B <= 48 else [0, 15, 16, 63, 64, 100, 127]
     eng = pt.Engine(device=0, max_slots=B, max_ctx=64, lsd_decode_steps=lsd, seed=0x5EED)
     try:
         assert "head.chain" in eng.plan_ops(B)
-        orc = []
+        orc = {}
         for b in range(B):
             F = 3 + (b % 5)
             prompt = (d["prompt"][:F] * (1.0 + 0.05 * b)).astype(np.float32)
             ids = rng.integers(0, 4000, size=2 + b % 3).astype(np.int32)
             eng.open(b, eng.voice_from_prompt(prompt), ids, params(max_frames=steps))
-            s = oracle.new_state(64)
-            s.prefill(prompt)
-            s.prefill_tokens(ids)
-            orc.append(s)
+            if b in rows:
+                s = oracle.new_state(64)
+                s.prefill(prompt)
+                s.prefill_tokens(ids)
+                orc[b] = s
         assert eng.time_kernel(B, "head.chain", reps=20) > 0
         lat = [None] * B
         for i in range(steps):
             r = eng.step(B)
-            for b in range(B):
+            assert r.valid.all()
+            for b in rows:
                 o = orc[b].step(lat[b], lsd_steps=lsd)
                 lat[b] = o["latent"]
                 assert r.valid[b]
