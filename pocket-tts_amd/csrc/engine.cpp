@@ -792,9 +792,15 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     a.bias = W(L_.ada_b);
     a.Y = mods_;
     a.ldy = NADA;
-    if (use_head_chain(B)) {  // side job: empty the hand-off regions k_flow_head uses next
-      a.fill = hx_;
-      a.fill_n4 = (long)(hx_floats(B) / 4);
+    if (use_head_chain(B)) {  // side jobs: x0 into hand-off region 0, empty the other regions
+      const size_t r0 = (size_t)((B + 15) / 16 * 16) * FD;  // floats per hand-off region
+      a.fill = hx_ + r0;
+      a.fill_n4 = (long)((hx_floats(B) - r0) / 4);
+      a.x0_cur = cur_;
+      a.x0_w = W(L_.inproj_w);
+      a.x0_b = W(L_.inproj_b);
+      a.x0_hx = hx_;
+      a.x0_B = B;
       a.fhm = fhm_;
       a.fhm_B = B;
     }
@@ -824,16 +830,22 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     f.wp = fhw_;
     f.fhm = fhm_;
     f.hx = hx_;
+    f.x0_ready = 1;
     f.ctr = hctr_;
     f.err = herr_;
     f.dbg = getenv("PTTS_HEAD_DBG") ? (unsigned long long*)strtoull(getenv("PTTS_HEAD_DBG"), nullptr, 0) : nullptr;
     const double fl = 2.0 * lsd_ * B * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD);
     const double by = 4.0 * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD) +
                       4.0 * lsd_ * B * ((double)FDEPTH * 3 * FD + 2 * FD);
+    // isolated replays: re-empty the regions and recompute x0 (the adaLN reduce's side jobs)
     float* hx = hx_;
     const size_t nhx = hx_floats(B);
+    const float *cur = cur_, *iw = W(L_.inproj_w), *ib = W(L_.inproj_b);
     Op op{"head.chain", [f](hipStream_t s) { flow_head(f, s); }, fl, by};
-    op.prep = [hx, nhx](hipStream_t s) { PTTS_HIP(hipMemsetD32Async(hx, 0xFFFFFFFFu, nhx, s)); };
+    op.prep = [hx, nhx, cur, iw, ib, B](hipStream_t s) {
+      PTTS_HIP(hipMemsetD32Async(hx, 0xFFFFFFFFu, nhx, s));
+      flow_head_x0(cur, iw, ib, hx, B, s);
+    };
     ops.push_back(op);
   }
   for (int st = 0; st < lsd_ && !use_head_chain(B); ++st) {

@@ -55,6 +55,11 @@ struct RowReduceArgs {
   // fragment order (FlowHeadArgs::fhm) for a batch of fhm_B rows, or nullptr
   float* fhm;
   int fhm_B;
+  // side job for k_flow_head's first hand-off: x0 = cur W_in^T + b_in (flow-head input projection,
+  // mlp.rs:375) for x0_B rows, stored into hand-off region 0 in its tile layout, or nullptr
+  const float *x0_cur, *x0_w, *x0_b;
+  float* x0_hx;
+  int x0_B;
 };
 struct GemmArgs {
   int mode;    // 0 dense, 1 conv
@@ -236,6 +241,7 @@ struct FlowHeadArgs {
   // [ceil(B/16)][32 column groups][16 rows][16 columns] (one producer tile = one contiguous KB),
   // all 0xFFFFFFFF (empty) at launch
   float* hx;
+  int x0_ready;  // 1: hand-off region 0 already holds x0 of Euler step 0 (the adaLN reduce's side job)
   int* ctr;
   int* err;
   unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr
@@ -247,6 +253,9 @@ void set_wg_cap(int cap);
 void im2col(const float* X, const float* H, int B, int T_in, int stride, int P, int cin, int taps, float* A,
             hipStream_t s);
 bool flow_head_fits(int B);
+// x0 = cur W_in^T + b_in into hand-off region 0 as its own launch (the adaLN reduce's side job,
+// for replaying k_flow_head alone)
+void flow_head_x0(const float* cur, const float* w, const float* bias, float* hx, int B, hipStream_t s);
 // fragment-order copy of the chain's matrices for FlowHeadArgs::wp: 12 * 512 * 512 + 32 * 512 floats
 size_t flow_head_packed_floats();
 void pack_flow_head(const float* w0, const float* w2, long blk, const float* fin_w, float* dst, hipStream_t s);

@@ -1511,6 +1511,48 @@ __device__ __forceinline__ float4 rr_ln(const RowReduceArgs& a, int m, int n, fl
   return hh;
 }
 
+// Flow-head input projection of 4 columns n..n+3 of one row (cv: the row's 32 latent values),
+// in one summation order for both of its callers (k_row_reduce's x0 side job, k_flow_head's
+// later Euler steps); a NaN result is stored canonical (never the hand-off's empty pattern).
+__device__ __forceinline__ float4 fh_inproj4(const float4 (&cv)[8], const float* in_w, const float* in_b, int n) {
+  float acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float* w = in_w + (long)(n + q) * FH_L;
+    float t = in_b[n + q];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 wv = *reinterpret_cast<const float4*>(w + 4 * j);
+      t += (cv[j].x * wv.x + cv[j].y * wv.y) + (cv[j].z * wv.z + cv[j].w * wv.w);
+    }
+    acc[q] = t;
+  }
+  return make_float4(acc[0], acc[1], acc[2], acc[3]);
+}
+
+// x0 of Euler step 0 into hand-off region 0 ([RG][32][16][16] tiles; plain stores, read by the
+// next launch), threads i0, i0 + nthr, ... of the caller's grid
+__device__ __forceinline__ void fh_x0_job(const float* cur, const float* w, const float* bias, float* hx, int B, long i0,
+                                          long nthr) {
+  for (long i = i0; i < (long)B * (FH_D / 4); i += nthr) {
+    const int b = (int)(i / (FH_D / 4)), n = (int)(i % (FH_D / 4)) * 4;
+    float4 cv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cv[j] = *reinterpret_cast<const float4*>(cur + (long)b * FH_L + 4 * j);
+    float4 x = fh_inproj4(cv, w, bias, n);
+    const unsigned qn = 0x7FC00000u;
+    x = make_float4(x.x != x.x ? __uint_as_float(qn) : x.x, x.y != x.y ? __uint_as_float(qn) : x.y,
+                    x.z != x.z ? __uint_as_float(qn) : x.z, x.w != x.w ? __uint_as_float(qn) : x.w);
+    *reinterpret_cast<float4*>(hx + ((long)((b >> 4) * 32 + (n >> 4)) * 256 + (b & 15) * 16 + (n & 15))) = x;
+  }
+}
+__global__ void k_fh_x0(const float* cur, const float* w, const float* bias, float* hx, int B) {
+  fh_x0_job(cur, w, bias, hx, B, (long)blockIdx.x * 256 + threadIdx.x, (long)gridDim.x * 256);
+}
+void flow_head_x0(const float* cur, const float* w, const float* bias, float* hx, int B, hipStream_t s) {
+  hipLaunchKernelGGL(k_fh_x0, dim3((B * (FH_D / 4) + 255) / 256), dim3(256), 0, s, cur, w, bias, hx, B);
+}
+
 template <int SMAX>
 __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   __shared__ float sh[4];
@@ -1519,6 +1561,9 @@ __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
     for (long i = ((long)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x; i < a.fill_n4; i += nthr)
       reinterpret_cast<uint4*>(a.fill)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
   }
+  if (a.x0_hx)
+    fh_x0_job(a.x0_cur, a.x0_w, a.x0_b, a.x0_hx, a.x0_B, ((long)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x,
+              (long)gridDim.x * gridDim.y * 256);
   const int m = blockIdx.x;
   const int n0 = blockIdx.y * 1024 + 4 * threadIdx.x;
   const bool ok = n0 < a.N;
@@ -2964,6 +3009,8 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   int sk = 0;
 #define FH_STAMP()                                                                     \
   if (a.dbg && tid == 0 && blockIdx.x < 4 && sk < 120) a.dbg[blockIdx.x * 128 + sk++] = __builtin_amdgcn_s_memrealtime()
+  // probe layout: [entry, x0 published, 6 x 8 ResBlock stamps, final: swept, done]
+  FH_STAMP();
 
   // operand loaders (i: ResBlock, or FH_DEPTH for the FinalLayer)
   // fragment-packed matrix m (2i: w0 of ResBlock i, 2i + 1: its w2, 12: fin_w), this lane's float4 j
@@ -2994,27 +3041,20 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
     const float* mods = a.mods + (long)st * a.B * a.ldm;
     // ---- input projection x = cur W_in^T + b_in (K = 32), one wave. At st = 0 it comes first:
     // its hand-off starts the chain, so its loads are not queued behind the prologue's
+    // At st = 0 with x0_ready the launch ahead (the adaLN reduce) has stored x0 already: wave 0
+    // only reads its residual tile back (the chain's prologue was 3.5-3.9 us of cold loads).
     if (st > 0) fh_wait(cc, 2 * st, a.err, dead);
-    if (wave == 0) {
+    if (wave == 0 && st == 0 && a.x0_ready) {
+      xo = fh_ld(hr, ooff);
+    } else if (wave == 0) {
       float4 cv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) cv[j] = fh_ld(cr, (crow * FH_L + 4 * j) * 4);
-      float acc[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float* w = a.in_w + (long)(ocol + q) * FH_L;
-        float t = a.in_b[ocol + q];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float4 wv = f4ld(w + 4 * j);
-          t += (cv[j].x * wv.x + cv[j].y * wv.y) + (cv[j].z * wv.z + cv[j].w * wv.w);
-        }
-        acc[q] = t;
-      }
-      xo = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      xo = fh_inproj4(cv, a.in_w, a.in_b, ocol);
       if (ostore) fh_put(hr, q * rstride + ooff, xo);
     }
     ++q;
+    FH_STAMP();
     if (st == 0) {
       // the first phases' operands, then the ResBlock LayerNorm affines into LDS (first read
       // after the first LayerNorm's barrier)
@@ -3071,6 +3111,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
       if (wave == 0) cv = fh_ld(cr, off);  // latent before this Euler step (read ahead of the sweep)
       float4 v[4];
       fh_sweep(hr, (q - 1) * rstride + aoff, v, a.err, dead);
+      FH_STAMP();
       if (wave != 0 && more) load_mlp2_ops(p2, nmods, 0);
       fh_ln(v, s_st, wave, c, G, nullptr, nullptr, p0.sc, p0.sf);
       const float4 r = fh_gemm(v, p0.w, s_red2[gi++ & 1], wave, c, G, lane);
@@ -3080,6 +3121,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
         const float4 o = f4add(r, p0.e0);
         if (ostore) fh_st(cr, off, make_float4(cv.x + o.x * e, cv.y + o.y * e, cv.z + o.z * e, cv.w + o.w * e));
         if (more) fh_publish(cc);
+        FH_STAMP();
         if (more) {
           load_ln_ops(p0, nmods, 0, st + 1);
           load_mlp2_ops(p2, nmods, 0);

@@ -26,15 +26,17 @@ print("chain_us (isolated, HIP events)", round(eng.time_kernel(B, "head.chain", 
 eng.sync()
 torch.cuda.synchronize()
 names = ["sweep1", "ln", "gemm1", "store_u", "sweep2", "gemm2", "store_x", "next"]
+# stamps: [entry, x0 published] + 6 x 8 ResBlock stamps + (final layer WGs 0-3: [swept, done])
 s = buf.cpu().numpy().reshape(4, 128)
 for wg in range(4):
     t = s[wg]
     n = int(np.count_nonzero(t))
     t = t[:n].astype(np.int64)
     d = np.diff(t) * 10 / 1000.0  # us
-    print(f"wg{wg}: {n} stamps, total {(t[-1] - t[0]) * 10 / 1000:.2f} us")
+    print(f"wg{wg}: {n} stamps, total {(t[-1] - t[0]) * 10 / 1000:.2f} us; prologue {d[0]:.2f} us (entry -> x0 "
+          f"published), x0 -> block 0 {d[1]:.2f}" + (f"; final layer: sweep {d[-2]:.2f}, rest {d[-1]:.2f}" if n > 51 else ""))
     per = {k: [] for k in names}
-    for i, x in enumerate(d):
+    for i, x in enumerate(d[2:2 + 47]):
         per[names[i % len(names)]].append(x)
     print("  " + "  ".join(f"{k} {np.mean(val):.2f}" for k, val in per.items() if val))
 eng.close()
