@@ -336,6 +336,13 @@ void Engine::finalize() {
     inw_t_ = (float*)p;
   }
   transpose(W(L_.input_linear), D, LDIM, inw_t_, stream_);
+  if (!fh_inw_t_) {  // flow-head input projection transposed ([32][512], the x0 side job)
+    void* p = nullptr;
+    PTTS_HIP(hipMalloc(&p, sizeof(float) * LDIM * FD));
+    allocs_.push_back(p);
+    fh_inw_t_ = (float*)p;
+  }
+  transpose(W(L_.inproj_w), FD, LDIM, fh_inw_t_, stream_);
   if (!fhw_ && head_uniform_stride()) {  // every element is written by the packing below
     void* p = nullptr;
     PTTS_HIP(hipMalloc(&p, sizeof(float) * flow_head_packed_floats()));
@@ -797,7 +804,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
       a.fill = hx_ + r0;
       a.fill_n4 = (long)((hx_floats(B) - r0) / 4);
       a.x0_cur = cur_;
-      a.x0_w = W(L_.inproj_w);
+      a.x0_w = fh_inw_t_;
       a.x0_b = W(L_.inproj_b);
       a.x0_hx = hx_;
       a.x0_B = B;
@@ -840,7 +847,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     // isolated replays: re-empty the regions and recompute x0 (the adaLN reduce's side jobs)
     float* hx = hx_;
     const size_t nhx = hx_floats(B);
-    const float *cur = cur_, *iw = W(L_.inproj_w), *ib = W(L_.inproj_b);
+    const float *cur = cur_, *iw = fh_inw_t_, *ib = W(L_.inproj_b);
     Op op{"head.chain", [f](hipStream_t s) { flow_head(f, s); }, fl, by};
     op.prep = [hx, nhx, cur, iw, ib, B](hipStream_t s) {
       PTTS_HIP(hipMemsetD32Async(hx, 0xFFFFFFFFu, nhx, s));

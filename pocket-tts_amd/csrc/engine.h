@@ -148,6 +148,7 @@ class Engine {
   float* fhw_ = nullptr;  // the chain's matrices in fragment order (pack_flow_head, at finalize)
   float* hx_ = nullptr;
   float* fhm_ = nullptr;
+  float* fh_inw_t_ = nullptr;  // flow-head input projection transposed [32][512] (x0 side job)
   float* mcol_ = nullptr;  // explicit conv operands for rocBLAS convs (PTTS_BACK_BLAS 64 / 128)  // adaLN shift / scale in k_flow_head's fragment order (FlowHeadArgs::fhm)  // flow-head hand-off regions [lsd * 13][roundup(B, 16)][512] (k_flow_head)
   size_t hx_floats(int B) const { return (size_t)lsd_ * 13 * ((B + 15) / 16 * 16) * FD; }
   float* inw_t_ = nullptr;  // input_linear weight transposed, [32][1024] (k_input_ln)

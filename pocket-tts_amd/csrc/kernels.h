@@ -56,7 +56,8 @@ struct RowReduceArgs {
   float* fhm;
   int fhm_B;
   // side job for k_flow_head's first hand-off: x0 = cur W_in^T + b_in (flow-head input projection,
-  // mlp.rs:375) for x0_B rows, stored into hand-off region 0 in its tile layout, or nullptr
+  // mlp.rs:375) for x0_B rows, stored into hand-off region 0 in its tile layout, or nullptr;
+  // x0_w is W_in transposed, [32][512]
   const float *x0_cur, *x0_w, *x0_b;
   float* x0_hx;
   int x0_B;
@@ -255,7 +256,7 @@ void im2col(const float* X, const float* H, int B, int T_in, int stride, int P, 
 bool flow_head_fits(int B);
 // x0 = cur W_in^T + b_in into hand-off region 0 as its own launch (the adaLN reduce's side job,
 // for replaying k_flow_head alone)
-void flow_head_x0(const float* cur, const float* w, const float* bias, float* hx, int B, hipStream_t s);
+void flow_head_x0(const float* cur, const float* w_t, const float* bias, float* hx, int B, hipStream_t s);
 // fragment-order copy of the chain's matrices for FlowHeadArgs::wp: 12 * 512 * 512 + 32 * 512 floats
 size_t flow_head_packed_floats();
 void pack_flow_head(const float* w0, const float* w2, long blk, const float* fin_w, float* dst, hipStream_t s);

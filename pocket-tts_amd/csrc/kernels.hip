@@ -1514,6 +1514,7 @@ __device__ __forceinline__ float4 rr_ln(const RowReduceArgs& a, int m, int n, fl
 // Flow-head input projection of 4 columns n..n+3 of one row (cv: the row's 32 latent values),
 // in one summation order for both of its callers (k_row_reduce's x0 side job, k_flow_head's
 // later Euler steps); a NaN result is stored canonical (never the hand-off's empty pattern).
+__device__ __forceinline__ float fh_dot4(float4 c, float4 w) { return (c.x * w.x + c.y * w.y) + (c.z * w.z + c.w * w.w); }
 __device__ __forceinline__ float4 fh_inproj4(const float4 (&cv)[8], const float* in_w, const float* in_b, int n) {
   float acc[4];
 #pragma unroll
@@ -1521,36 +1522,35 @@ __device__ __forceinline__ float4 fh_inproj4(const float4 (&cv)[8], const float*
     const float* w = in_w + (long)(n + q) * FH_L;
     float t = in_b[n + q];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float4 wv = *reinterpret_cast<const float4*>(w + 4 * j);
-      t += (cv[j].x * wv.x + cv[j].y * wv.y) + (cv[j].z * wv.z + cv[j].w * wv.w);
-    }
+    for (int j = 0; j < 8; ++j) t += fh_dot4(cv[j], *reinterpret_cast<const float4*>(w + 4 * j));
     acc[q] = t;
   }
   return make_float4(acc[0], acc[1], acc[2], acc[3]);
 }
 
 // x0 of Euler step 0 into hand-off region 0 ([RG][32][16][16] tiles; plain stores, read by the
-// next launch), threads i0, i0 + nthr, ... of the caller's grid
-__device__ __forceinline__ void fh_x0_job(const float* cur, const float* w, const float* bias, float* hx, int B, long i0,
-                                          long nthr) {
-  for (long i = i0; i < (long)B * (FH_D / 4); i += nthr) {
-    const int b = (int)(i / (FH_D / 4)), n = (int)(i % (FH_D / 4)) * 4;
-    float4 cv[8];
+// next launch), one output per thread i0, i0 + nthr, ...; the weight is read transposed (w_t
+// [32][512], made at finalize) so each load instruction of a wave is one contiguous 256-B run
+__device__ __forceinline__ void fh_x0_job(const float* cur, const float* w_t, const float* bias, float* hx, int B,
+                                          long i0, long nthr) {
+  for (long i = i0; i < (long)B * FH_D; i += nthr) {
+    const int b = (int)(i / FH_D), n = (int)(i % FH_D);
+    float t = bias[n];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) cv[j] = *reinterpret_cast<const float4*>(cur + (long)b * FH_L + 4 * j);
-    float4 x = fh_inproj4(cv, w, bias, n);
-    const unsigned qn = 0x7FC00000u;
-    x = make_float4(x.x != x.x ? __uint_as_float(qn) : x.x, x.y != x.y ? __uint_as_float(qn) : x.y,
-                    x.z != x.z ? __uint_as_float(qn) : x.z, x.w != x.w ? __uint_as_float(qn) : x.w);
-    *reinterpret_cast<float4*>(hx + ((long)((b >> 4) * 32 + (n >> 4)) * 256 + (b & 15) * 16 + (n & 15))) = x;
+    for (int j = 0; j < 8; ++j) {
+      const float4 c = *reinterpret_cast<const float4*>(cur + (long)b * FH_L + 4 * j);
+      const float* w = w_t + (long)(4 * j) * FH_D + n;
+      t += fh_dot4(c, make_float4(w[0], w[FH_D], w[2 * FH_D], w[3 * FH_D]));
+    }
+    if (t != t) t = __uint_as_float(0x7FC00000u);  // never the hand-off's empty pattern
+    hx[((long)((b >> 4) * 32 + (n >> 4))) * 256 + (b & 15) * 16 + (n & 15)] = t;
   }
 }
 __global__ void k_fh_x0(const float* cur, const float* w, const float* bias, float* hx, int B) {
   fh_x0_job(cur, w, bias, hx, B, (long)blockIdx.x * 256 + threadIdx.x, (long)gridDim.x * 256);
 }
-void flow_head_x0(const float* cur, const float* w, const float* bias, float* hx, int B, hipStream_t s) {
-  hipLaunchKernelGGL(k_fh_x0, dim3((B * (FH_D / 4) + 255) / 256), dim3(256), 0, s, cur, w, bias, hx, B);
+void flow_head_x0(const float* cur, const float* w_t, const float* bias, float* hx, int B, hipStream_t s) {
+  hipLaunchKernelGGL(k_fh_x0, dim3((B * FH_D + 255) / 256), dim3(256), 0, s, cur, w_t, bias, hx, B);
 }
 
 template <int SMAX>
