@@ -11,10 +11,17 @@ memory inside the step (the graphs end in async D2H copies; fetch() reads host m
 
 The utterance length is fixed at 125 frames whatever --steps says: a timed job is the admission of
 all B utterances (voice-KV copy + 40-token text prefill per row) followed by the 125 batched steps
-that deliver their 10 s of audio. --steps K times ceil(K / 125) such jobs back to back (at least
-one); `steps` in the output is the number of steps actually timed (`steps_requested` = K).
-value = audio seconds produced by all ranks / max-over-ranks wall time of the timed jobs. The voice
-state is precomputed (as in configs[1]); warmup = one short job of W steps on the same rows.
+that deliver their 10 s of audio. --steps K times max(MIN_JOBS, ceil(K / 125)) such jobs back to
+back (MIN_JOBS = 16, >= 1 s of GPU work, so one scheduling hiccup cannot move the line by
+percent); `steps` in the output is the number of steps actually timed (`steps_requested` = K).
+value = audio seconds produced by all ranks / max-over-ranks wall time of all timed jobs;
+`per_job` gives the median, min and max of the per-job values (each job's time max over ranks).
+The voice state is precomputed (as in configs[1]); warmup = one short job of W steps on the same
+rows.
+
+Any PTTS_* environment variable, or a library whose build id differs from the checked-out
+sources (a stale binary or a -DPTTS_PROBES measurement build), marks the line "NOT A PRODUCT RUN"
+and lists them under `tuned`.
 
 Multi-GPU (--gpus N): replicas (independent utterances per GPU, no per-step collective). Without
 a torch.distributed environment the process re-launches itself as N ranks under
@@ -41,6 +48,7 @@ METRIC = "audio-sec/wall-sec (RTF) per GPU at batch=32 + p50 first-chunk latency
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8 TB/s spec
 F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix/vector peak
 BATCH, PROMPT_FRAMES, TEXT_TOKENS, UTT_FRAMES = 32, 125, 40, 125  # 125 frames = 10 s per utterance
+MIN_JOBS = 16  # timed jobs per run whatever --steps says (~1.3 s of GPU work at B = 32)
 
 
 def measured_traffic(op):
@@ -244,7 +252,7 @@ def main():
 
     B, W = args.batch, args.warmup
     K = args.profile_frames if args.profile_frames > 0 else UTT_FRAMES
-    jobs = max(1, -(-args.steps // K)) if args.profile_frames <= 0 else 1
+    jobs = max(MIN_JOBS, -(-args.steps // K)) if args.profile_frames <= 0 else 1
     pipeline = not args.no_pipeline
     calls = K + (1 if pipeline else 0)  # overlapped stepping returns each frame one call later
     max_ctx = PROMPT_FRAMES + TEXT_TOKENS + K + 8
@@ -298,6 +306,7 @@ def main():
         barrier()
         eng.sync()
         admit_s = 0.0
+        job_s = []
         t0 = time.perf_counter()
         for j in range(jobs):
             ta0 = time.perf_counter()
@@ -309,19 +318,23 @@ def main():
             eng.sync()
             r = eng.fetch(B)  # the last frame of every row, from pinned host memory
             assert r.valid.all() and r.last.all(), "bench produced invalid frames"
-            assert np.isfinite(r.pcm).all() or os.environ.get("PTTS_BACK_PROBE"), "bench produced non-finite PCM"
+            assert np.isfinite(r.pcm).all(), "bench produced non-finite PCM"
+            job_s.append(time.perf_counter() - ta0)
         t1 = time.perf_counter()
         barrier()
         elapsed = t1 - t0
         if dist is not None:
-            elapsed, admit_s = max_over_ranks(dist, [elapsed, admit_s], dev)
-        return elapsed, admit_s
+            elapsed, admit_s, *job_s = max_over_ranks(dist, [elapsed, admit_s, *job_s], dev)
+        return elapsed, admit_s, job_s
 
-    elapsed, admit_s = timed_job(eng)
+    elapsed, admit_s, job_s = timed_job(eng)
     steps = jobs * K
 
     audio_sec = world * jobs * B * K * 1920 / 24000.0
     value = audio_sec / elapsed
+    job_vals = sorted(world * B * K * 1920 / 24000.0 / t for t in job_s)
+    per_job = {"jobs": jobs, "median": round(float(np.median(job_vals)), 2), "min": round(job_vals[0], 2),
+               "max": round(job_vals[-1], 2)}
 
     if rank != 0:
         if dist is not None:
@@ -394,7 +407,7 @@ def main():
     if not args.no_quant_variant and world == 1:
         eq = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                        pipeline=pipeline, weight_quant=pt.QUANT_FLOW_LM)
-        q_el, q_ad = timed_job(eq)
+        q_el, q_ad, _ = timed_job(eq)
         quant = {"value": round(jobs * B * K * 1920 / 24000.0 / q_el, 2), "unit": "audio-sec/wall-sec",
                  "ms_per_step": round(1000.0 * q_el / steps, 4),
                  "steady_ms_per_step": round(1000.0 * (q_el - q_ad) / steps, 4),
@@ -403,7 +416,7 @@ def main():
         eq.close()
         ef = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                        pipeline=pipeline, fp8_gemm=True)
-        f_el, f_ad = timed_job(ef)
+        f_el, f_ad, _ = timed_job(ef)
         fp8 = {"value": round(jobs * B * K * 1920 / 24000.0 / f_el, 2), "unit": "audio-sec/wall-sec",
                "ms_per_step": round(1000.0 * f_el / steps, 4),
                "steady_ms_per_step": round(1000.0 * (f_el - f_ad) / steps, 4),
@@ -417,6 +430,19 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline_leg(args.cpu_procs)
+
+    # ---- what was measured: the product library built from these sources, no PTTS_* knobs
+    tuned = {k: v for k, v in os.environ.items() if k.startswith("PTTS_")}
+    build = None
+    if not selftest:
+        build = pt.build_id()
+        if build != pt.source_build_id():
+            tuned["build_id"] = f"{build} (sources: {pt.source_build_id()})"
+    data = ("launcher selftest (CPU stand-in engine, nothing computed)" if selftest else
+            f"PROFILING RUN ({K}-frame utterances, not configs[2])" if args.profile_frames > 0 else
+            "synthetic (seeded weights and prompts; real checkpoints are gated offline)")
+    if tuned:
+        data = "NOT A PRODUCT RUN (PTTS_* knobs or a non-matching build; see tuned): " + data
 
     out = {
         "metric": METRIC,
@@ -433,9 +459,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "launcher selftest (CPU stand-in engine, nothing computed)" if selftest else
-                f"PROFILING RUN ({K}-frame utterances, not configs[2])" if args.profile_frames > 0 else
-                "synthetic (seeded weights and prompts; real checkpoints are gated offline)",
+        "data": data,
         "config": {"workload": f"b6369a24 batch={B} concurrent 10 s utterances per GPU (125 frames, voice prompt "
                                f"{PROMPT_FRAMES} frames, {TEXT_TOKENS} text tokens), lsd_decode_steps=1 "
                                "(BASELINE configs[2])",
@@ -444,6 +468,9 @@ def main():
                    "stepping": "pipelined (Mimi decode of frame k overlaps FlowLM step k+1)" if pipeline
                    else "sequential",
                    "pcm_to_host": "every frame, async D2H into pinned memory inside the step graphs"},
+        "per_job": per_job,
+        "build_id": build,
+        "tuned": tuned or None,
         "p50_first_chunk_ms": None if p50 is None else round(p50, 3),
         "int8_flowlm_variant": quant,
         "fp8_flowlm_variant": fp8,

@@ -30,6 +30,16 @@ extern "C" {
 #define PTTS_ERR_STATE 3   /* call not valid in the current slot/engine state */
 #define PTTS_ERR_IO 4      /* weights file missing or malformed */
 
+/* ABI version of this header. Bumped whenever a struct below changes layout (3: cfg_yaml was
+ * appended to ptts_engine_config). A caller checks ptts_abi_version() == PTTS_ABI_VERSION before
+ * passing any struct: a library built from another header reads a different layout. */
+#define PTTS_ABI_VERSION 3
+int ptts_abi_version(void);
+/* Build id of the loaded library: the first 16 hex digits of the sha256 over the sources it was
+ * built from (pocket-tts_amd/Makefile, BUILD_ID), with "+probes" appended for a measurement build
+ * (-DPTTS_PROBES). Lets a test harness refuse a stale prebuilt binary. */
+const char* ptts_build_id(void);
+
 #define PTTS_FRAME_SAMPLES 1920 /* 24 kHz / 12.5 Hz (config/b6369a24.yaml:24-27) */
 #define PTTS_LATENT_DIM 32
 #define PTTS_MODEL_DIM 1024

@@ -37,6 +37,8 @@ ptts::Engine& eng(ptts_engine* e) {
 
 extern "C" {
 
+int ptts_abi_version(void) { return PTTS_ABI_VERSION; }
+
 size_t ptts_weight_blob_bytes(void) { return ptts::pack_weights(nullptr, nullptr).total * sizeof(float); }
 
 int ptts_pack_weights(uint64_t synth_seed, const char* weights_path, float* host_out, size_t n_bytes) {

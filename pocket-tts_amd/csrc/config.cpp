@@ -25,6 +25,23 @@ std::string trim(const std::string& s) {
   return s.substr(a, b - a + 1);
 }
 
+// A '#' starts a comment only at the start of the line or after whitespace, and never inside a
+// quoted scalar ('...' or "..."): "tok#1" and "'a # b'" keep their '#'.
+std::string strip_comment(const std::string& line) {
+  char quote = 0;
+  for (size_t i = 0; i < line.size(); ++i) {
+    const char ch = line[i];
+    if (quote) {
+      if (ch == quote) quote = 0;
+    } else if (ch == '\'' || ch == '"') {
+      quote = ch;
+    } else if (ch == '#' && (i == 0 || line[i - 1] == ' ' || line[i - 1] == '\t')) {
+      return line.substr(0, i);
+    }
+  }
+  return line;
+}
+
 // flattened "a.b.c" -> scalar, sequences joined with ','
 std::map<std::string, std::string> read_yaml(const std::string& path) {
   std::ifstream f(path);
@@ -35,8 +52,7 @@ std::map<std::string, std::string> read_yaml(const std::string& path) {
   int seq_indent = -1, lineno = 0;
   while (std::getline(f, line)) {
     ++lineno;
-    const size_t h = line.find('#');
-    if (h != std::string::npos) line = line.substr(0, h);
+    line = strip_comment(line);
     if (trim(line).empty()) continue;
     const int ind = (int)line.find_first_not_of(' ');
     const std::string body = trim(line);
@@ -99,6 +115,7 @@ void check_model_config(const char* path) {
       {"mimi.seanet.last_kernel_size", "3"},
       {"mimi.seanet.dilation_base", "2"},
       {"mimi.seanet.compress", "2"},
+      {"mimi.seanet.pad_mode", "constant"},  // the convs' zero left padding is compiled in
       {"mimi.transformer.d_model", "512"},
       {"mimi.transformer.num_heads", "8"},
       {"mimi.transformer.num_layers", "2"},

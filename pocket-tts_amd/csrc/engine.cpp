@@ -240,10 +240,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
 Engine::~Engine() {
   (void)hipSetDevice(dev_);
   if (stream_) (void)hipStreamSynchronize(stream_);
-  if (blas_) (void)rocblas_destroy_handle((rocblas_handle)blas_);
   if (stream_be_) (void)hipStreamSynchronize(stream_be_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
+  if (blas_) (void)rocblas_destroy_handle((rocblas_handle)blas_);  // after every graph that recorded it
   for (int q = 0; q < NHB; ++q) {
     if (ev_front_[q]) (void)hipEventDestroy(ev_front_[q]);
     if (ev_back_[q]) (void)hipEventDestroy(ev_back_[q]);

@@ -248,7 +248,7 @@ struct FlowHeadArgs {
   unsigned long long* dbg;  // probe only: s_memrealtime stamps of workgroups 0-3, or nullptr
 };
 // Launches issued while a cap > 0 is set reserve dynamic LDS so that at most `cap` workgroups of
-// each kernel share a CU (0 = no cap). Process-wide; the engine sets it around graph capture.
+// each kernel share a CU (0 = no cap). Per host thread; the engine sets it around graph capture.
 void set_wg_cap(int cap);
 // conv operand rows as an explicit [B * T_in / stride][taps * cin] matrix (cin % 4 == 0)
 void im2col(const float* X, const float* H, int B, int T_in, int stride, int P, int cin, int taps, float* A,

@@ -16,7 +16,8 @@ namespace ptts {
 // Workgroups-per-CU cap of the launches issued while it is set (set_wg_cap; the engine sets it
 // while capturing the back part of a pipelined step): dynamic LDS is reserved so that at most
 // `cap` workgroups of a kernel share a CU, leaving room for the concurrently running front part.
-static int g_wg_cap = 0;
+// Per host thread: engines of one process (serve --gpus N threads) capture graphs concurrently.
+static thread_local int g_wg_cap = 0;
 void set_wg_cap(int cap) { g_wg_cap = cap; }
 template <typename K>
 static size_t cap_lds(K kernel, int cap) {

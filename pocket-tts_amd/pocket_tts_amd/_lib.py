@@ -4,6 +4,7 @@ if the HIP library is missing or no GPU is visible, every entry point raises."""
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 from pathlib import Path
 
@@ -17,6 +18,7 @@ LDIM = 32
 DIM = 1024
 SAMPLE_RATE = 24000
 QUANT_NONE, QUANT_FLOW_LM, QUANT_ALL = 0, 1, 2
+ABI_VERSION = 3  # PTTS_ABI_VERSION of include/pocket_tts.h that the structs below mirror
 
 F32P = C.POINTER(C.c_float)
 U8P = C.POINTER(C.c_uint8)
@@ -53,6 +55,8 @@ class GenParams(C.Structure):
 
 # (name, restype, argtypes) for every symbol include/pocket_tts.h declares
 SIGNATURES = [
+    ("ptts_abi_version", C.c_int, []),
+    ("ptts_build_id", C.c_char_p, []),
     ("ptts_weight_blob_bytes", C.c_size_t, []),
     ("ptts_pack_weights", C.c_int, [C.c_uint64, C.c_char_p, F32P, C.c_size_t]),
     ("ptts_pack_weights_ex", C.c_int, [C.c_uint64, C.c_char_p, C.c_int, F32P, C.c_size_t]),
@@ -114,8 +118,38 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        abi = L.ptts_abi_version()
+        if abi != ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH} has C ABI version {abi}, these bindings mirror {ABI_VERSION}: rebuild it")
         _LIB = L
     return _LIB
+
+
+def build_id() -> str:
+    """Build id compiled into the loaded library (ptts_build_id)."""
+    return lib().ptts_build_id().decode()
+
+
+def source_build_id() -> str:
+    """The build id the checked-out sources produce (the Makefile's BUILD_ID rule: sha256 over the
+    sorted csrc/*.{hip,cpp,h}, include/pocket_tts.h and the Makefile, first 16 hex digits)."""
+    csrc = PKG_ROOT / "csrc"
+    files = sorted(p for ext in ("*.hip", "*.cpp", "*.h") for p in csrc.glob(ext))
+    files += [PKG_ROOT.parent / "include" / "pocket_tts.h", PKG_ROOT / "Makefile"]
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def check_build_id() -> str:
+    """Raise unless the loaded library was built from the checked-out sources (a stale prebuilt
+    binary, or a -DPTTS_PROBES measurement build, fails loudly). Returns the id."""
+    got, want = build_id(), source_build_id()
+    if got != want:
+        raise RuntimeError(f"{LIB_PATH} was built from other sources (build id {got}, sources {want}): "
+                           "run `make -C pocket-tts_amd`")
+    return got
 
 
 def check(rc: int) -> None:

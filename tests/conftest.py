@@ -21,6 +21,16 @@ def load_golden(name: str) -> dict:
     return load_file(str(GOLDEN / name))
 
 
+@pytest.fixture(autouse=True, scope="session")
+def _native_build_is_current(request):
+    """A GPU session runs only against a library built from these sources (ptts_build_id vs the
+    source hash): a stale prebuilt .so pushed to the box fails every GPU test loudly."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import pocket_tts_amd as pt
+
+        pt.check_build_id()
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from _oracle import Oracle

@@ -78,3 +78,15 @@ def test_generation_params_marshalling():
     p = GenerationParams(temp=0.5, eos_threshold=float("inf"), noise_clamp=None, frames_after_eos=5, max_frames=7,
                          seed=2**64 - 1).to_c()
     assert p.noise_clamp == 0.0 and p.max_frames == 7 and p.seed == 2**64 - 1 and np.isinf(p.eos_threshold)
+
+
+def test_library_is_built_from_these_sources():
+    """The .so carries the hash of the sources it was built from (Makefile BUILD_ID): a stale
+    prebuilt binary (or a -DPTTS_PROBES measurement build) is refused by every GPU session."""
+    import pocket_tts_amd as pt
+    from pocket_tts_amd import _lib
+
+    assert _lib.lib().ptts_abi_version() == _lib.ABI_VERSION == 3
+    assert len(pt.source_build_id()) == 16
+    assert pt.build_id() == pt.source_build_id()
+    assert pt.check_build_id() == pt.build_id()

@@ -31,6 +31,7 @@ def test_reference_config_matches_build():
     ("    context: 250", "    context: 500", "mimi.transformer.context"),
     ("  frame_rate: 12.5", "  frame_rate: 25", "mimi.frame_rate"),
     ("  dtype: float32\n  flow:", "  dtype: bfloat16\n  flow:", "flow_lm.dtype"),
+    ("    pad_mode: constant", "    pad_mode: reflect", "mimi.seanet.pad_mode"),
 ])
 def test_other_variant_is_rejected_naming_the_key(tmp_path, old, new, key):
     with pytest.raises(pt.PocketTTSError, match=key.replace(".", r"\.")):
@@ -40,6 +41,15 @@ def test_other_variant_is_rejected_naming_the_key(tmp_path, old, new, key):
 def test_equal_values_in_other_spellings_pass(tmp_path):
     pt.Engine.check_config(_variant(tmp_path, "  frame_rate: 12.5", "  frame_rate: 12.50  # Hz"))
     pt.Engine.check_config(_variant(tmp_path, "    max_period: 10000", "    max_period: 1e4"))
+
+
+def test_hash_inside_a_value_is_not_a_comment(tmp_path):
+    """'#' opens a comment only after whitespace and outside quotes."""
+    with pytest.raises(pt.PocketTTSError, match=r"pad_mode = constant#x"):
+        pt.Engine.check_config(_variant(tmp_path, "    pad_mode: constant", "    pad_mode: constant#x"))
+    with pytest.raises(pt.PocketTTSError, match=r"mimi\.dtype = 'float32 # x'"):
+        pt.Engine.check_config(_variant(tmp_path, "  dtype: float32\n  sample_rate", "  dtype: 'float32 # x'\n  sample_rate"))
+    pt.Engine.check_config(_variant(tmp_path, "    pad_mode: constant", "    pad_mode: constant   # zeros"))
 
 
 def test_missing_key_and_file_fail(tmp_path):

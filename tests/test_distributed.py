@@ -77,8 +77,8 @@ def test_replicas_gloo_world2():
 def test_bench_gpus_flag_launches_replica_ranks():
     """`bench.py --gpus 2` outside a torch.distributed environment re-launches itself as 2 ranks
     under torch.distributed.run (a child process, never exec), each rank runs its replica, rank 0
-    reports the whole job: n_gpus 2, "replicas x2", global batch 2 x 32, 125-frame utterances
-    whatever --steps asks. CPU only: --launcher-selftest swaps in a stand-in engine and gloo."""
+    reports the whole job: n_gpus 2, "replicas x2", global batch 2 x 32, 125-frame utterances and
+    at least MIN_JOBS (16) timed jobs whatever --steps asks, with the per-job median / min / max. CPU only: --launcher-selftest swaps in a stand-in engine and gloo."""
     import json
     import subprocess
     import sys
@@ -91,4 +91,6 @@ def test_bench_gpus_flag_launches_replica_ranks():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "replicas x2"
     assert out["config"]["global_batch"] == 64 and out["config"]["utterance_frames"] == 125
-    assert out["steps"] == 125 and out["steps_requested"] == 20 and out["scaling"] == "weak"
+    assert out["steps"] == 16 * 125 and out["steps_requested"] == 20 and out["scaling"] == "weak"
+    pj = out["per_job"]
+    assert pj["jobs"] == 16 and pj["min"] <= pj["median"] <= pj["max"]

@@ -4,11 +4,13 @@ bench's mode). The FlowLM context of every row grows 165 -> 297 positions, so th
 (k_attn_decode_qkv) takes its second 256-key round for the last 40 frames, and the Mimi decoder's
 250-key window slides over 2,112 ring positions (four wraps of the 512-slot ring).
 
-Checked every frame:
-  row 0  (the golden `e2e_long` prompt and text) against the reference's own outputs for its
-         first 100 frames (tests/golden/gen_golden.py long), and against the C oracle for all 132;
-  rows 15, 16, 31 (their own prompts and texts; rows 15/16 straddle a 16-row group boundary of
-         the flow-head launch and the attention tiles) against their own oracle runs.
+Checked every frame of EVERY row (an indexing fault confined to one row group, tile or XCD
+block cannot pass):
+  row 0     (the golden `e2e_long` prompt and text) against the reference's own outputs for its
+            first 100 frames (tests/golden/gen_golden.py long);
+  rows 0-31 (each its own prompt and text) against their own C-oracle runs for all 132 frames.
+The 32 oracle runs are single-threaded each (OpenMP team size 1 per worker thread) on a pool of
+min(16, cpus) threads (the GPU box's CPU share), started before the engine so that they overlap it.
 The oracle is pinned to the reference at this shape by tests/test_oracle.py
 (test_oracle_long_context_matches_reference).
 
@@ -16,6 +18,7 @@ Gates (all fp32; differences are reduction order only): EOS logit and latent <= 
 PCM <= 2e-6 max abs per frame (the golden PCM RMS is 0.035, so 6e-5 of the signal). The worst
 errors seen are printed."""
 
+import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -24,7 +27,7 @@ from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 
-FRAMES, PROBE = 132, (0, 15, 16, 31)
+FRAMES, B = 132, 32
 LAT_TOL, PCM_TOL = 5e-5, 2e-6
 
 
@@ -37,6 +40,9 @@ def _row_inputs(d, b):
 
 
 def _oracle_run(oracle, prompt, ids, n):
+    from _oracle import lib as oracle_lib
+
+    oracle_lib().omp_set_num_threads(1)  # this worker thread's OpenMP team: one thread
     s = oracle.new_state(320)
     s.prefill(prompt)
     s.prefill_tokens(ids)
@@ -52,10 +58,10 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
     import pocket_tts_amd as pt
 
     d = load_golden("e2e_long.safetensors")
-    B = 32
     inputs = [_row_inputs(d, b) for b in range(B)]
-    with ThreadPoolExecutor(len(PROBE)) as ex:  # the oracle runs free (temp 0): precompute them
-        futs = {b: ex.submit(_oracle_run, oracle, *inputs[b], FRAMES) for b in PROBE}
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    with ThreadPoolExecutor(workers) as ex:  # the oracle runs free (temp 0): precompute them
+        futs = {b: ex.submit(_oracle_run, oracle, *inputs[b], FRAMES) for b in range(B)}
         eng = pt.Engine(device=0, max_slots=B, max_ctx=320, lsd_decode_steps=1, seed=0x5EED, pipeline=True)
         try:
             voices = [eng.voice_from_prompt(p) for p, _ in inputs]
@@ -69,7 +75,7 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
                 r = eng.step(B)
                 assert r.valid.all(), i
                 assert bool(r.last.all()) == (i == FRAMES - 1) and not (r.last.any() and i < FRAMES - 1), i
-                frames.append({b: (float(r.eos_logits[b]), r.latents[b].copy(), r.pcm[b].copy()) for b in PROBE})
+                frames.append([(float(r.eos_logits[b]), r.latents[b].copy(), r.pcm[b].copy()) for b in range(B)])
             assert not eng.step(B).valid.any()
         finally:
             eng.close()
@@ -83,7 +89,7 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
         assert e[0] <= LAT_TOL and e[1] <= LAT_TOL and e[2] <= PCM_TOL, (kind, where, e)
 
     for i in range(FRAMES):
-        for b in PROBE:
+        for b in range(B):
             cmp("oracle", frames[i][b], ref[b][i], (i, b))
         if i < d["latent"].shape[0]:
             cmp("golden", frames[i][0], (d["eos_logit"][i], d["latent"][i], d["pcm"][i]), (i, 0))

@@ -12,7 +12,7 @@ fatal() { # exit codes that mean the GPU or process died: stop everything
   case $1 in 124|134|137|139) return 0 ;; *) return 1 ;; esac
 }
 
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -rfP --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v -rfP --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
 echo "pytest-gpu rc=$rc"; tail -n 30 "$OUT/pytest_gpu.log"
 if fatal $rc; then exit $rc; fi
@@ -36,19 +36,22 @@ if [ "${SEQ:-0}" = "1" ]; then
 fi
 
 if [ "${PROFILE:-1}" = "1" ]; then
+  # the MEASURED configuration: pipelined engine, full 125-frame jobs (front / back graphs on two
+  # streams; tools/prof_ops.py piped attributes each hardware queue to its part of the plan)
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-      -- python "$ROOT/bench.py" --profile-frames 30 --warmup 5 --no-cpu-baseline --no-latency --no-pipeline --no-quant-variant \
+      -- python "$ROOT/bench.py" --warmup 5 --no-cpu-baseline --no-latency --no-quant-variant \
       --ops-out "$OUT/prof_ops.json" > "$OUT/prof.log" 2>&1)
   rc=$?
-  echo "rocprof rc=$rc"; tail -n 2 "$OUT/prof.log"
+  echo "rocprof rc=$rc"; tail -n 2 "$OUT/prof.log" | cut -c1-300
   if [ $rc -ne 0 ]; then exit $rc; fi
-  python tools/prof_ops.py trace "$OUT/prof/run_kernel_trace.csv" "$OUT/prof_ops.json" "$OUT/op_stats.csv"
+  python tools/prof_ops.py piped "$OUT/prof/run_kernel_trace.csv" "$OUT/prof_ops.json" "$OUT/op_stats.csv" \
+      "$OUT/piped_steps.json"
 fi
 
 if [ "${PMC:-0}" = "1" ]; then
   for C in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -d "$OUT/pmc_$C" -o run --output-format csv \
-        -- python "$ROOT/bench.py" --profile-frames 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-pipeline --no-quant-variant \
+        -- python "$ROOT/bench.py" --profile-frames 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-quant-variant \
         > "$OUT/pmc_$C.log" 2>&1)
     rc=$?
     echo "pmc $C rc=$rc"; tail -n 2 "$OUT/pmc_$C.log"
@@ -60,7 +63,7 @@ if [ "${PMC:-0}" = "1" ]; then
   # MFMA utilisation: one pass with both counters (1 SQ_ + 1 GRBM_ counter: within one pass's limits)
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmc_mfma" \
       -o run --output-format csv \
-      -- python "$ROOT/bench.py" --profile-frames 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-pipeline --no-quant-variant \
+      -- python "$ROOT/bench.py" --profile-frames 6 --warmup 2 --no-cpu-baseline --no-latency --no-op-times --no-quant-variant \
       > "$OUT/pmc_mfma.log" 2>&1)
   rc=$?
   echo "pmc mfma rc=$rc"; tail -n 2 "$OUT/pmc_mfma.log"

@@ -8,6 +8,12 @@ k_commit dispatch whose kernel-name sequence equals the most common such window 
   prof_ops.py trace    <run_kernel_trace.csv> <bench_ops.json> <out.csv>
       per-op kernel durations next to the bench's own HIP-event timings (the cross-check of
       the bench's roofline kernel duration)
+  prof_ops.py piped    <run_kernel_trace.csv> <bench_ops.json> <out.csv> [<out_steps.json>]
+      the same for a PIPELINED run (the bench's own configuration): the front graph (FlowLM + flow
+      head, ending in k_front_commit) and the back graph (Mimi decode, ending in k_commit) run on
+      two streams (two hardware queues), so their dispatches interleave in time. Each queue's
+      dispatches are matched against its part of the plan; per step the front span, the back
+      span, their overlap and the interval between consecutive back ends (the steady step)
   prof_ops.py counters <run_counter_collection.csv> <bench_ops.json> <COUNTER> <out.json>
       per-op average of one PMC counter per launch
   prof_ops.py traffic  <fetch.json> <write.json> <out.json>
@@ -70,27 +76,122 @@ def cmd_trace(trace_path, ops_path, out_path):
           f"first-start to last-end {sum(span) / len(span):.1f} us/step")
 
 
+def part_windows(names, part, closer):
+    """Windows of len(part) dispatches ending at `closer` whose kernel names match the most common
+    such window (one per replay of that part's graph)."""
+    n = len(part)
+    ends = [i for i, nm in enumerate(names) if closer in nm and i + 1 >= n]
+    seqs = collections.Counter(tuple(names[i + 1 - n:i + 1]) for i in ends)
+    if not seqs:
+        return None, []
+    ref, _ = seqs.most_common(1)[0]
+    return ref, [i + 1 - n for i in ends if tuple(names[i + 1 - n:i + 1]) == ref]
+
+
+def split_plan(plan):
+    cut = plan.index("mimi.quant_upsample")
+    return plan[:cut], plan[cut:]
+
+
+def piped_attribution(rows, plan, queue_key):
+    """{op: [row, ...]} over every replay of the front and back graphs, grouped by hardware queue;
+    plus the per-part window lists [(part, [rows of one replay]), ...]."""
+    front, back = split_plan(plan)
+    byq = collections.defaultdict(list)
+    for r in rows:
+        byq[r[queue_key]].append(r)
+    per = collections.defaultdict(list)
+    reps = {"front": [], "back": []}
+    for q, rs in byq.items():
+        names = [r["Kernel_Name"] for r in rs]
+        for label, part, closer in (("front", front, "k_front_commit"), ("back", back, "k_commit")):
+            _, wins = part_windows(names, part, closer)
+            for w in wins:
+                win = rs[w:w + len(part)]
+                reps[label].append(win)
+                for j, op in enumerate(part):
+                    per[op].append(win[j])
+    return per, reps
+
+
+def cmd_piped(trace_path, ops_path, out_path, steps_path=None):
+    ops = json.load(open(ops_path))
+    plan = ops["plan"]
+    event_us = {o["op"]: o for o in ops["ops"]}
+    rows = [r for r in csv.DictReader(open(trace_path)) if is_engine(r["Kernel_Name"])]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    per, reps = piped_attribution(rows, plan, "Queue_Id")
+    if not reps["front"] or not reps["back"]:
+        raise SystemExit("no front/back windows found")
+
+    def dur(r):
+        return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
+
+    with open(out_path, "w", newline="") as f:
+        wr = csv.writer(f)
+        wr.writerow(["op", "kernel", "calls", "rocprof_avg_us", "bench_event_avg_us", "flops", "bytes"])
+        seen = set()
+        for op in plan:
+            if op in seen or op not in per:
+                continue
+            seen.add(op)
+            d = [dur(r) for r in per[op]]
+            e = event_us.get(op, {})
+            wr.writerow([op, per[op][0]["Kernel_Name"].split("(")[0], len(d), round(sum(d) / len(d), 3),
+                         round(e.get("avg_us", float("nan")), 3), e.get("flops", 0), e.get("bytes", 0)])
+
+    def span(win):
+        return int(win[0]["Start_Timestamp"]), int(win[-1]["End_Timestamp"])
+
+    fr = sorted(span(w) for w in reps["front"])
+    bk = sorted(span(w) for w in reps["back"])
+    med = lambda v: sorted(v)[len(v) // 2] if v else None
+    f_us = [(b - a) / 1000.0 for a, b in fr]
+    b_us = [(b - a) / 1000.0 for a, b in bk]
+    step = [(bk[i + 1][1] - bk[i][1]) / 1000.0 for i in range(len(bk) - 1)]
+    ov = []
+    for a, b in bk:  # overlap of each back replay with the front replays
+        ov.append(sum(max(0, min(b, fb) - max(a, fa)) for fa, fb in fr) / 1000.0)
+    busy_f = [sum(dur(r) for r in w) for w in reps["front"]]
+    busy_b = [sum(dur(r) for r in w) for w in reps["back"]]
+    out = {"front_replays": len(fr), "back_replays": len(bk),
+           "front_span_us_median": med(f_us), "back_span_us_median": med(b_us),
+           "front_kernel_busy_us_median": med(busy_f), "back_kernel_busy_us_median": med(busy_b),
+           "back_overlapped_by_front_us_median": med(ov),
+           "steady_step_us_median (back end to back end)": med(step)}
+    print(json.dumps(out))
+    if steps_path:
+        json.dump(out, open(steps_path, "w"), indent=1)
+
+
 def cmd_counters(cc_path, ops_path, counter, out_path):
     plan = json.load(open(ops_path))["plan"]
     disp = {}
     for r in csv.DictReader(open(cc_path)):
         if r["Counter_Name"] != counter or not is_engine(r["Kernel_Name"]):
             continue
-        d = disp.setdefault(int(r["Dispatch_Id"]), [r["Kernel_Name"], 0.0])
+        d = disp.setdefault(int(r["Dispatch_Id"]), [r["Kernel_Name"], 0.0, r.get("Queue_Id", "0")])
         d[1] += float(r["Counter_Value"])
     order = sorted(disp)
     names = [disp[i][0] for i in order]
     vals = [disp[i][1] for i in order]
     n = len(plan)
-    _, steps = step_windows(names, n)
     per = collections.defaultdict(list)
-    for w in steps:
-        for j in range(n):
-            per[plan[j]].append(vals[w + j])
-    out = {"counter": counter, "steps": len(steps),
+    try:
+        _, steps = step_windows(names, n)  # sequential engine: one stream, plan order
+        for w in steps:
+            for j in range(n):
+                per[plan[j]].append(vals[w + j])
+        nsteps = len(steps)
+    except SystemExit:  # pipelined engine: front and back parts interleave; match each part alone
+        rows = [{"Kernel_Name": disp[i][0], "v": disp[i][1], "q": disp[i][2]} for i in order]
+        pr, reps = piped_attribution(rows, plan, "q")
+        per = {op: [r["v"] for r in rs] for op, rs in pr.items()}
+        nsteps = min(len(reps["front"]), len(reps["back"]))
+    out = {"counter": counter, "steps": nsteps,
            "ops": {op: sum(v) / len(v) for op, v in per.items()}}
     json.dump(out, open(out_path, "w"), indent=1)
-    print(f"{counter}: {len(steps)} steps attributed")
+    print(f"{counter}: {nsteps} steps attributed")
 
 
 def cmd_traffic(fetch_path, write_path, out_path):
@@ -135,4 +236,5 @@ def cmd_mfma(busy_path, gui_path, op_stats_path, out_path):
 
 if __name__ == "__main__":
     cmd, args = sys.argv[1], sys.argv[2:]
-    {"trace": cmd_trace, "counters": cmd_counters, "traffic": cmd_traffic, "mfma": cmd_mfma}[cmd](*args)
+    {"trace": cmd_trace, "piped": cmd_piped, "counters": cmd_counters, "traffic": cmd_traffic,
+     "mfma": cmd_mfma}[cmd](*args)
