@@ -29,10 +29,10 @@ int pick_splits(int M, int N, int K) {
 }
 }  // namespace
 
-// Tuning override of an op's tile layout / split-K count (tools/back_tune.py):
+// Tuning override of an op's tile layout / split-K count (tools/back_tune.py, probe builds only):
 // PTTS_OVR="name=L[:S],...", read at every plan build.
 static void tile_override(const std::string& name, int& layout, int& ksplit) {
-  const char* e = getenv("PTTS_OVR");
+  const char* e = probe_env("PTTS_OVR");
   if (!e) return;
   const std::string s(e);
   size_t p = 0;
@@ -153,27 +153,19 @@ Engine::Engine(const ptts_engine_config& cfg) {
   admit_slots_ = (int*)dalloc(B);
   admit_st_ = (SlotState*)dalloc((sizeof(SlotState) * B + 3) / 4);
   admit_fpos_ = (int*)dalloc(B);
-  tickets_ = (int*)dalloc(TICKETS);
-  row_tickets_ = (int*)dalloc(ROW_TICKETS);
-  // measured slower than a separate row_reduce launch on every front GEMM (ff2 43 vs 13 us with
-  // the LayerNorm row finisher, ff1 15.6 vs 11.4 us tile-local): opt-in only
-  fuse_splitk_ = getenv("PTTS_FUSED_SPLITK") != nullptr;
   // pipelined stepping: the back part's kernels run at most one workgroup per CU, so the
   // latency-bound front part always finds room on every CU (measured 0.735 -> 0.688 ms per step
   // for the GEMMs alone; tools/sweep_env.sh)
   // three hand-off buffers: the front part may run two frames ahead of the back part. With the
   // back part now the longer of the two alone (498 vs 441 us), the front no longer idles behind
   // it: steady step 0.6370 -> 0.6321 ms (medians of 4; when the front was the longer part, 3
-  // buffers measured 0.5% slower). PTTS_HANDOFF_BUFS=2 restores lockstep.
-  nhb_ = getenv("PTTS_HANDOFF_BUFS") && atoi(getenv("PTTS_HANDOFF_BUFS")) == 2 ? 2 : 3;
-  mimi_attn_fused_ = !getenv("PTTS_MIMI_ATTN_UNFUSED");
-  back_cap_ = getenv("PTTS_BACK_WG_CAP") ? atoi(getenv("PTTS_BACK_WG_CAP")) : 1;
+  // buffers measured 0.5% slower).
+  if (probe_env("PTTS_BACK_WG_CAP")) back_cap_ = atoi(probe_env("PTTS_BACK_WG_CAP"));
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
   mods_ = dalloc((size_t)lsd_ * B * NADA);
   xf_ = dalloc((size_t)B * FD);
   hf_ = dalloc((size_t)B * FD);
   uf_ = dalloc((size_t)B * FD);
-  head_chain_ = !getenv("PTTS_HEAD_CHAIN_OFF");
   PTTS_REQUIRE(hx_floats(B) * 4 < (1ull << 31), "flow-head hand-off regions exceed 2 GB (lsd_decode_steps too large)");
   hx_ = dalloc(hx_floats(B));
   // adaLN shift / scale in the chain's fragment order (written by the adaLN reduce), zeroed:
@@ -275,16 +267,15 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
 }
 
 // The FlowLM step matrices as fragment-packed copies for the register-resident split-K GEMM
-// (PTTS_GEMV: bit mask of the matrices that use it, 1 qkv, 2 out, 4 linear1, 8 linear2, 16 the
-// flow head's adaLN matrix, M = lsd * B rows): out on
-// 32x32 tiles with 8 K slices of 128 (4 waves splitting each), linear2 on 32x32 tiles with 16
-// slices of 256. Alone on the chip every matrix is faster this way (qkv 8.1 -> 4.9 us, out 4.5
-// -> 3.2, linear1 8.1 -> 5.2, linear2 7.9 -> 5.3); in the pipelined step only out + linear2 pay
-// (steady step 0.6595 -> 0.6326 ms, medians of 3), the qkv / linear1 versions on any tile
-// (PTTS_GEMV_WIDE) slow the concurrent back part more than they gain. Default mask: 2 | 8 | 16.
+// (bit mask of the matrices that use it: 1 qkv, 2 out, 4 linear1, 8 linear2, 16 the flow head's
+// adaLN matrix, M = lsd * B rows): out on 32x32 tiles with 8 K slices of 128 (4 waves splitting
+// each), linear2 on 32x32 tiles with 16 slices of 256. Alone on the chip every matrix is faster
+// this way (qkv 8.1 -> 4.9 us, out 4.5 -> 3.2, linear1 8.1 -> 5.2, linear2 7.9 -> 5.3); in the
+// pipelined step only out + linear2 + adaLN pay (steady step 0.6595 -> 0.6326 ms, medians of 3):
+// the qkv / linear1 versions on any tile slow the concurrent back part more than they gain.
 void Engine::derive_gemv() {
   // sequential stepping (the B = 1 first-chunk path, no concurrent back part): every matrix
-  const int mask = getenv("PTTS_GEMV") ? atoi(getenv("PTTS_GEMV")) : pipeline_ ? 26 : 31;
+  const int mask = pipeline_ ? 2 | 8 | 16 : 31;
   gemv_mask_ = mask;
   struct M {
     const float* w;
@@ -292,10 +283,8 @@ void Engine::derive_gemv() {
     GemvShape g;
   };
   std::vector<M> mats;
-  GemvShape wide{4, 128};  // qkv / linear1 tile (PTTS_GEMV_WIDE="wn,kw")
-  GemvShape outg{1, 32};   // out tile (PTTS_GEMV_OUT="wn,kw")
-  if (getenv("PTTS_GEMV_OUT")) sscanf(getenv("PTTS_GEMV_OUT"), "%d,%d", &outg.wn, &outg.kw);
-  if (getenv("PTTS_GEMV_WIDE")) sscanf(getenv("PTTS_GEMV_WIDE"), "%d,%d", &wide.wn, &wide.kw);
+  const GemvShape wide{4, 128};  // qkv / linear1 tile
+  const GemvShape outg{1, 32};   // out tile
   for (int l = 0; l < NL; ++l) {
     const Layout::TL& t = L_.fl[l];
     mats.push_back({W(t.in_proj), 3 * D, D, 1, wide});
@@ -303,8 +292,7 @@ void Engine::derive_gemv() {
     mats.push_back({W(t.l1), FF, D, 4, wide});
     mats.push_back({W(t.l2), D, FF, 8, GemvShape{1, 64}});
   }
-  GemvShape ada{4, 128};  // flow-head adaLN matrix (PTTS_GEMV_ADA="wn,kw"): 0.6365 -> 0.6315 ms
-  if (getenv("PTTS_GEMV_ADA")) sscanf(getenv("PTTS_GEMV_ADA"), "%d,%d", &ada.wn, &ada.kw);
+  const GemvShape ada{4, 128};  // flow-head adaLN matrix: 0.6365 -> 0.6315 ms
   mats.push_back({W(L_.ada_w), NADA, FD, 16, ada});
   size_t total = 0;
   for (const M& m : mats)
@@ -453,7 +441,7 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   // wide skinny GEMMs (FlowLM qkv/ff1, flow-head adaLN): 32x128 LDS-DMA tiles, 8-way split-K
   // (tools/gemm_bench.hip on MI355X: qkv 6.7 -> 6.3 us, ff1 7.9 -> 6.5 us, ada 10.1 -> 8.7 us)
   if (M <= 64 && N >= 3072) {
-    layout = getenv("PTTS_SKINNY_NBUF4") ? 13 : 7;  // 2-buffer LDS (40 KB) co-resides with the back part
+    layout = 7;  // 2-buffer LDS (40 KB) co-resides with the back part
     S = std::max(1, std::min(8, K / 64));
   } else if (M >= 256) {  // prefill passes: MFMA-bound, 64x64 LDS-DMA tiles, no split
     layout = 12;
@@ -484,8 +472,6 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
                        throw Error(PTTS_ERR_HIP, "rocblas_sgemm failed");
                    },
                    2.0 * M * N * K, 4.0 * ((double)N * K + (double)M * K + (double)M * N)});
-    last_split_ = GemmArgs{};
-    last_split_op_ = (size_t)-1;
     *S_out = 1;
     return;
   }
@@ -498,8 +484,6 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
     float* part = partial_;
     ops.push_back({name, [=](hipStream_t s) { gemv_splitk(X, ldx, M, N, K, P, g, part, s); }, 2.0 * M * N * K,
                    4.0 * N * K + 4.0 * ((double)M * K + (double)Sg * M * N)});
-    last_split_ = GemmArgs{};
-    last_split_op_ = (size_t)-1;  // never folded into a reduce (push_rr)
     *S_out = Sg;
     return;
   }
@@ -513,7 +497,7 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
     while ((nch + S - 1) / S > FP8_KSLICE_MAX / 32) ++S;
   }
   auto q8 = q8map_.find(Wt);
-  const bool w8 = q8 != q8map_.end() && M <= 64 && (long)N * K >= (2L << 20) && !getenv("PTTS_W8_OFF");
+  const bool w8 = q8 != q8map_.end() && M <= 64 && (long)N * K >= (2L << 20);
   if (w8) {
     layout = 0;
     const int tiles = ((N + 63) / 64) * ((M + 31) / 32);
@@ -544,39 +528,18 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   a.W = Wt;
   a.S = S;
   a.partial = partial_;
-  {  // FlowLM / flow-head step weights are read once per step: non-temporal loads (PTTS_NT bits)
-    const int nt = getenv("PTTS_NT") ? atoi(getenv("PTTS_NT")) : 3;
-    a.w_nt = M <= 64 && ((layout != 0 && (nt & 1)) || (layout == 0 && (nt & 4)));
-  }
+  // FlowLM / flow-head step weights are read once per step: non-temporal loads on the LDS-DMA
+  // tiles (step -1.1 %; the 32x32 register tile keeps default-policy loads)
+  a.w_nt = M <= 64 && layout != 0;
   ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
                  (w8 || wf8 ? (double)N * K + 4.0 * N : 4.0 * N * K) + 4.0 * ((double)M * K + (double)S * M * N)});
-  last_split_ = a;
-  last_split_op_ = ops.size() - 1;
   *S_out = S;
 }
 
-// The row-reduce epilogue of the split GEMM just emitted: run inside that GEMM's launch (in-launch
-// split-K combine, layouts 0 and 13) when possible, else as its own row_reduce launch.
+// The row-reduce epilogue of the split GEMM just emitted, as its own launch (an in-launch split-K
+// combine by the last-arriving workgroup measured slower on every front GEMM: ff2 43 vs 13 us with
+// the LayerNorm row finisher, ff1 15.6 vs 11.4 us tile-local).
 void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r) {
-  GemmArgs g = last_split_;
-  const bool prev_is_gemm = !ops.empty() && last_split_op_ == ops.size() - 1;
-  const bool tiles_ok = g.layout == 0 || g.layout == 13 || g.layout == 7;
-  const bool ln_ok = !r.ln || (r.N % 256 == 0 && r.N <= 1024);
-  const bool same = prev_is_gemm && r.P == g.partial && r.S == g.S && r.M == g.M && r.N == g.N && !r.fill;
-  if (fuse_splitk_ && same && tiles_ok && ln_ok) {
-    const int gx = (g.layout == 13 || g.layout == 7) ? (g.N + 127) / 128 : (g.N + 31) / 32;
-    const int gy = (g.M + 31) / 32;
-    PTTS_REQUIRE(gx * gy <= TICKETS && gy <= ROW_TICKETS, "split-K ticket arrays too small");
-    g.fuse = r.ln ? 2 : 1;
-    g.tickets = tickets_;
-    g.row_tickets = row_tickets_;
-    g.rr = r;
-    const int S = g.S;
-    Op& op = ops.back();
-    op.fn = [g, S](hipStream_t s) { gemm(g, S, s); };
-    last_split_op_ = (size_t)-1;
-    return;
-  }
   ops.push_back({name, [r](hipStream_t s) { row_reduce(r, s); }});
 }
 
@@ -749,7 +712,7 @@ void Engine::prefill_rows(std::vector<Op>& ops, int slot, int T, int p0) {
 // The persistent flow-head launch needs <= 128 rows and ResBlock tensors at one uniform stride
 // in the packed blob (pack_weights lays the six blocks out identically).
 bool Engine::use_head_chain(int B) const {
-  if (!head_chain_ || !flow_head_fits(B)) return false;
+  if (!flow_head_fits(B)) return false;
   // every workgroup spins on counters the others bump: all of them must be resident at once
   if (flow_head_grid(B) > head_resident_) return false;
   return head_uniform_stride();
@@ -840,7 +803,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     f.x0_ready = 1;
     f.ctr = hctr_;
     f.err = herr_;
-    f.dbg = getenv("PTTS_HEAD_DBG") ? (unsigned long long*)strtoull(getenv("PTTS_HEAD_DBG"), nullptr, 0) : nullptr;
+    f.dbg = probe_env("PTTS_HEAD_DBG") ? (unsigned long long*)strtoull(probe_env("PTTS_HEAD_DBG"), nullptr, 0) : nullptr;
     const double fl = 2.0 * lsd_ * B * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD);
     const double by = 4.0 * ((double)FD * LDIM + 2.0 * FDEPTH * FD * FD + (double)LDIM * FD) +
                       4.0 * lsd_ * B * ((double)FDEPTH * 3 * FD + 2 * FD);
@@ -994,14 +957,9 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
         dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_,
                  fat ? fat_layout : 0);
       const float* qkv = mqkv_;
-      float* Q = mq_;
       float* O = mo_;
-      if (mimi_attn_fused_) {  // RoPE + ring append inside the attention launch
-        ops.push_back({p + ".attention", [=](hipStream_t s) { attention16_qkv(qkv, MR, MNH, mmap, kv, MCTX, O, s); }});
-      } else {
-        ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(nullptr, 0, qkv, MR, MNH, mmap, kv, Q, s); }});
-        ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, MR, MNH, mmap, kv, MCTX, UP, O, s); }});
-      }
+      // RoPE + ring append inside the attention launch
+      ops.push_back({p + ".attention", [=](hipStream_t s) { attention16_qkv(qkv, MR, MNH, mmap, kv, MCTX, O, s); }});
     }
     if (bb & 8) {  // out + LayerScale + residual: one rocBLAS product, the epilogue in a reduce
       blas_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, mpartial_);
@@ -1262,7 +1220,7 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
   // back part of a pipelined step: its launches leave room for the concurrent front part
   set_wg_cap(part == 1 && pipeline_ ? back_cap_ : 0);
   // per-op cap override for back-part launches: PTTS_OP_CAP="name=cap,..." (tuning)
-  const char* opcap = part == 1 && pipeline_ ? getenv("PTTS_OP_CAP") : nullptr;
+  const char* opcap = part == 1 && pipeline_ ? probe_env("PTTS_OP_CAP") : nullptr;
   try {
     for (const Op& op : ops) {
       if (opcap) {
@@ -1299,7 +1257,7 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
 //   sequential: front(k) then back(k) on one stream; the call's frame is frame k.
 //   pipelined:  front(k) on stream_ || back(k-1) on stream_be_ (the back part decodes the frame
 //               the previous call's front part produced); the call's frame is frame k-1. Frame
-//               k's hand-off buffer is k % nhb_ (3, or 2 with PTTS_HANDOFF_BUFS=2): front(k)
+//               k's hand-off buffer is k % nhb_ (3): front(k)
 //               waits only for back(k - nhb_), the last reader of its buffer, and back(k-1) for
 //               front(k-1).
 void Engine::step_async(int B) {
@@ -1392,7 +1350,7 @@ double Engine::time_op(int B, const std::string& name, int reps) {
   }
   PTTS_REQUIRE(sel != nullptr, "no op named " + name + " in the step plan");
   // PTTS_TIME_CAP: time back-part ops with the per-CU cap of pipelined stepping
-  const bool capped = back && pipeline_ && getenv("PTTS_TIME_CAP");
+  const bool capped = back && pipeline_ && probe_env("PTTS_TIME_CAP");
   set_wg_cap(capped ? back_cap_ : 0);
   hipEvent_t e0, e1;
   PTTS_HIP(hipEventCreate(&e0));
@@ -1484,7 +1442,7 @@ void Engine::overlap_probe(int B, int reps, double* us) {
     return 1000.0 * ms / reps;
   };
   // us[7]: front || Mimi transformer || SEANet decoder on three streams (a 3-stage pipeline)
-  if (getenv("PTTS_PROBE_MODES") && strchr(getenv("PTTS_PROBE_MODES"), '7')) {
+  if (probe_env("PTTS_PROBE_MODES") && strchr(probe_env("PTTS_PROBE_MODES"), '7')) {
     size_t cut2 = cut;
     while (cut2 < ops.size() && ops[cut2].name != "seanet.conv0") ++cut2;
     hipGraphExec_t g3[2] = {};
@@ -1534,7 +1492,7 @@ void Engine::overlap_probe(int B, int reps, double* us) {
     }
   }
   // PTTS_PROBE_MODES: digits of the measurements to run (default all: "0123456")
-  const std::string modes = getenv("PTTS_PROBE_MODES") ? getenv("PTTS_PROBE_MODES") : "0123456";
+  const std::string modes = probe_env("PTTS_PROBE_MODES") ? probe_env("PTTS_PROBE_MODES") : "0123456";
   auto want = [&](int m) { return modes.find((char)('0' + m)) != std::string::npos; };
   for (int m = 0; m < 7; ++m) us[m] = -1.0;  // us[7]: see above
   for (int m = 0; m < 4; ++m)

@@ -142,7 +142,6 @@ class Engine {
   int* admit_fpos_ = nullptr;
   float *ysilu_ = nullptr, *mods_ = nullptr, *xf_ = nullptr, *hf_ = nullptr, *uf_ = nullptr;
   // persistent flow-head chain (k_flow_head): hand-off rows, counters, timeout word
-  bool head_chain_ = true;
   bool head_uniform_stride() const;  // ResBlock tensors at one stride (k_flow_head, its packing)
   bool use_head_chain(int B) const;
   float* fhw_ = nullptr;  // the chain's matrices in fragment order (pack_flow_head, at finalize)
@@ -161,8 +160,7 @@ class Engine {
   // Up to three hand-off buffers: front(k) writes buffer k % nhb_ and waits only for back(k - nhb_)
   // (nhb_ = 3 lets front and back drift a step apart instead of running in lockstep).
   static constexpr int NHB = 3;
-  int nhb_ = 3;  // buffers in use (2 or 3)
-  bool mimi_attn_fused_ = true;  // Mimi step: RoPE + ring append inside the attention launch
+  int nhb_ = 3;  // buffers in use
   float* lat_out_[NHB] = {};
   float* eos_out_[NHB] = {};
   FrameFlags* flags_[NHB] = {};
@@ -172,13 +170,7 @@ class Engine {
   float* mpartial_ = nullptr;
   size_t mpcap_ = 0;
   // in-launch split-K combine (front part only; the back part never uses it)
-  static constexpr int TICKETS = 4096, ROW_TICKETS = 256;
-  int* tickets_ = nullptr;
-  int* row_tickets_ = nullptr;
-  bool fuse_splitk_ = false;
-  int back_cap_ = 1;  // PTTS_BACK_WG_CAP: max workgroups per CU of the pipelined back part's kernels
-  GemmArgs last_split_{};
-  size_t last_split_op_ = (size_t)-1;
+  int back_cap_ = 1;  // max workgroups per CU of the pipelined back part's kernels (PTTS_BACK_WG_CAP: probe builds)
   // pipelined stepping (cfg.pipeline): back part on its own stream, parity events
   bool pipeline_ = false;
   hipStream_t stream_be_ = nullptr;

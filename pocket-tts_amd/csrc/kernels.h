@@ -91,9 +91,9 @@ struct GemmArgs {
   int max_wg_per_cu;
   // 1: the weight stream is read with non-temporal loads (once-read FlowLM step weights)
   int w_nt;
-  // measurement probe only (PTTS_BACK_PROBE: back-part launches of a pipelined step;
-  // PTTS_FRONT_PROBE: all other tiled launches; results are wrong): bit 0 skips the MFMAs, bit 1
-  // skips the operand loads of the K loop
+  // measurement probe, -DPTTS_PROBES builds only (tools/; PTTS_BACK_PROBE: back-part launches of a
+  // pipelined step, PTTS_FRONT_PROBE: all other tiled launches; results are wrong): bit 0 skips
+  // the MFMAs, bit 1 the operand loads of the K loop. Ignored by product builds.
   int probe;
   // split-K
   int S;
@@ -111,14 +111,6 @@ struct GemmArgs {
   // elu_out: Y = elu(v) (after the residual); Y2 != null: Y = v and Y2 = elu(v) (same indexing)
   int elu_out;
   float* Y2;
-  // In-launch split-K combine (layouts 0 and 13, mode 0): every workgroup stores its slab into
-  // `partial`, then draws a ticket on its output tile; the last arriver sums the S slabs and runs
-  // the row-reduce epilogue `rr` on the tile (fuse 1). With fuse 2 the tile finishers also draw a
-  // ticket on their 32-row block and the last one applies rr's LayerNorm / modulate to the rows.
-  int fuse;
-  int* tickets;      // one counter per output tile, zero between launches
-  int* row_tickets;  // one counter per 32-row block
-  RowReduceArgs rr;  // rr.P == partial, rr.S == S
 };
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
 

@@ -13,6 +13,14 @@
 
 namespace ptts {
 
+// Measurement probes (PTTS_PROBES builds only, tools/): GemmArgs::probe bit 0 skips the MFMAs,
+// bit 1 the operand loads of the tiled GEMMs (results wrong). A product build compiles them out.
+#ifdef PTTS_PROBES
+#define PTTS_PROBE(a) ((a).probe)
+#else
+#define PTTS_PROBE(a) 0
+#endif
+
 // Workgroups-per-CU cap of the launches issued while it is set (set_wg_cap; the engine sets it
 // while capturing the back part of a pipelined step): dynamic LDS is reserved so that at most
 // `cap` workgroups of a kernel share a CU, leaving room for the concurrently running front part.
@@ -47,8 +55,6 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
-
-__device__ void splitk_combine(const GemmArgs& g, int m0, int n0, int ncols, float* flag);
 
 // Sum over S (<= 16) split-K slabs p[z * stride] in z order, every load issued before the first
 // add (a runtime-bounded loop waited on each load in turn: one L2 round trip per slab).
@@ -175,7 +181,7 @@ __device__ __forceinline__ void gemm_store_tile(const GemmArgs& a, const floatx1
 // (8/pn) * |W| + pn * |A|: weight-heavy Mimi GEMMs and SEANet convs share weight tiles, the
 // activation-heavy late SEANet stages share A row blocks). xcd_pn = 0, or a grid that does not
 // split evenly: contiguous runs of T/8 tiles per XCD (x fastest); identity when T % 8 != 0 or
-// when the in-launch split-K combine keys its tickets on blockIdx.
+// when `on` is false.
 __device__ __forceinline__ void xcd_tile(const GemmArgs& a, bool on, int& bx, int& by) {
   const int gx = gridDim.x, gy = gridDim.y, T = gx * gy;
   const int L = blockIdx.x + blockIdx.y * gx;
@@ -213,7 +219,7 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
   constexpr int WM = Lay<LAYOUT>::WM, WN = Lay<LAYOUT>::WN;
   const int wm = KS ? 0 : wave / WN, wn = KS ? 0 : wave % WN;
   int bx, by;
-  xcd_tile(a, !a.fuse, bx, by);
+  xcd_tile(a, true, bx, by);
   const int n0 = (bx * WN + wn) * 32, m0 = (by * WM + wm) * 32, z = blockIdx.z;
   const int nchunks = a.K >> 5;
   int cb = 0, ce = nchunks, phase = 0;
@@ -369,7 +375,6 @@ __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
 #pragma unroll
       for (int gg = 0; gg < GPW; ++gg) store(wave * GPW + gg, vs[gg]);
     }
-    if (MODE == 0 && a.fuse) splitk_combine(a, m0, n0, 32, red);
   } else if (wave_live) {
     if (ident && !a.partial && m0 + 32 <= a.M && n0 + 32 <= a.N) {
       gemm_store_tile(a, acc, m0, n0, h, r);
@@ -489,7 +494,7 @@ __global__ __launch_bounds__(256) void k_gemm_lds(GemmArgs a) {
       af[4 * i + 0] = x.x; af[4 * i + 1] = x.y; af[4 * i + 2] = x.z; af[4 * i + 3] = x.w;
       bf[4 * i + 0] = y.x; bf[4 * i + 1] = y.y; bf[4 * i + 2] = y.z; bf[4 * i + 3] = y.w;
     }
-    if (!(a.probe & 1)) {
+    if (!(PTTS_PROBE(a) & 1)) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
     }
@@ -581,8 +586,12 @@ __device__ __forceinline__ unsigned lds_addr(const float* p) {
 // TMW x TNW: 32x32 accumulators per wave (register blocking: one A fragment feeds TNW MFMAs,
 // one B fragment TMW), WG tile (32*WM*TMW) x (32*WN*TNW).
 // MODE 1 with S > 1 (single-phase convs): z is a K slice and the tile goes to partial slab z.
-template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1>
-__global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
+// MINB: workgroups per CU the register allocation must allow (__launch_bounds__ min waves per
+// SIMD = MINB). ILV: the DMAs of chunk c + NBUF - 1 are issued between the MFMAs of chunk c (one
+// per 16 / IPW k-steps) instead of as a burst ahead of its fragment reads: an f32 MFMA leaves 56
+// of its 64 issue cycles free, so the DMA issue (60-185 cycles each) hides behind the matrix pipe.
+template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1, int MINB = 1, bool ILV = false>
+__global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
   constexpr int TM = 32 * WM * TMW, TN = 32 * WN * TNW, ROWS = TM + TN;
   constexpr int CPR = BK / 4;        // 16-byte columns per LDS row
   constexpr int RPI = 64 / CPR;      // rows per 1-KiB wave instruction
@@ -597,7 +606,7 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int r = lane & 31, h = lane >> 5;
   int bx, by;
-  xcd_tile(a, !a.fuse, bx, by);
+  xcd_tile(a, true, bx, by);
   const int n0 = bx * TN, m0 = by * TM, z = blockIdx.z;
   const int nchunks = a.K / BK;
   int cb = 0, ce = nchunks, phase = 0;
@@ -638,33 +647,33 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
     }
   }
   const long ldx = a.ldx, hld = a.cin;
-  auto issue = [&](int c, int buf) {
-    if (a.probe & 2) return;
+  // DMA instruction `ins` of this wave for chunk c into LDS buffer buf
+  auto issue_one = [&](int c, int buf, int ins) {
+    if (PTTS_PROBE(a) & 2) return;
+    const int j = wave + 4 * ins;
+    if (j >= NINS) return;  // wave-uniform
     const int k0 = c * BK;
-    int tap = 0, ci = 0;
-    if (MODE != 0) {  // scalar, once per chunk
-      tap = k0 / a.cin;
-      ci = k0 - tap * a.cin;
+    const float* src;
+    if (MODE != 0 && j * RPI < TM) {
+      const int tap = k0 / a.cin;  // scalar
+      const int ci = k0 - tap * a.cin;
+      const int t = src_qs[ins] + tap;
+      const float* px = src_base[ins] + t * ldx + ci;
+      const float* ph = src_hist[ins] + t * hld + ci;
+      src = t >= 0 ? px : ph;
+    } else {
+      src = src_base[ins] + k0;
     }
-#pragma unroll
-    for (int ins = 0; ins < IPW; ++ins) {
-      const int j = wave + 4 * ins;
-      if (j >= NINS) break;  // wave-uniform
-      const float* src;
-      if (MODE != 0 && j * RPI < TM) {
-        const int t = src_qs[ins] + tap;
-        const float* px = src_base[ins] + t * ldx + ci;
-        const float* ph = src_hist[ins] + t * hld + ci;
-        src = t >= 0 ? px : ph;
-      } else {
-        src = src_base[ins] + k0;
-      }
-      // wave-uniform LDS base of this instruction; lane l -> + 16*l bytes
-      const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)((buf * ROWS * BK + j * RPI * BK) * 4));
-      if (a.w_nt && j * RPI >= TM) glds16_nt(src, dst);  // wave-uniform: a W row instruction
-      else glds16(src, dst);
-    }
+    // wave-uniform LDS base of this instruction; lane l -> + 16*l bytes
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)((buf * ROWS * BK + j * RPI * BK) * 4));
+    if (a.w_nt && j * RPI >= TM) glds16_nt(src, dst);  // wave-uniform: a W row instruction
+    else glds16(src, dst);
   };
+  auto issue = [&](int c, int buf) {
+#pragma unroll
+    for (int ins = 0; ins < IPW; ++ins) issue_one(c, buf, ins);
+  };
+  static_assert(!ILV || (BK == 32 && IPW <= 16), "interleaved DMA issue: BK 32, at most one DMA per k-step");
   constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
   floatx16 acc[TMW][TNW];
 #pragma unroll
@@ -686,7 +695,9 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
     // every wave's DMAs of chunk c have landed, and every wave is done with chunk c-1's buffer,
     // which the DMA issued next (chunk c+DIST) overwrites
     __syncthreads();
-    if (c + DIST < ce) issue(c + DIST, (c + DIST - cb) % NBUF);
+    const bool pf = c + DIST < ce;
+    const int pc = c + DIST, pbuf = (c + DIST - cb) % NBUF;
+    if (!ILV && pf) issue(pc, pbuf);
     {
       const int buf = (c - cb) % NBUF;
 #pragma unroll
@@ -718,14 +729,18 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
             bf[jj][4 * i + 0] = y.x; bf[jj][4 * i + 1] = y.y; bf[jj][4 * i + 2] = y.z; bf[jj][4 * i + 3] = y.w;
           }
         }
-        if (!(a.probe & 1)) {
+        if (!(PTTS_PROBE(a) & 1)) {
 #pragma unroll
-          for (int j = 0; j < 16; ++j)
+          for (int j = 0; j < 16; ++j) {
 #pragma unroll
             for (int ii = 0; ii < TMW; ++ii)
 #pragma unroll
               for (int jj = 0; jj < TNW; ++jj)
                 acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[ii][j], bf[jj][j], acc[ii][jj], 0, 0, 0);
+            if (ILV && pf && ((j + 1) * IPW) / 16 != (j * IPW) / 16) issue_one(pc, pbuf, (j * IPW) / 16);
+          }
+        } else if (ILV && pf) {
+          issue(pc, pbuf);
         }
       }
     }
@@ -753,7 +768,6 @@ __global__ __launch_bounds__(256) void k_gemm_glds(GemmArgs a) {
         gemm_store(a, row, col, phase, ident, v);
       }
     }
-  if (MODE == 0 && WM == 1 && TMW == 1 && TNW == 1 && a.fuse) splitk_combine(a, m0, n0, TN, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -819,7 +833,7 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
       for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.f;
   constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
   auto load = [&](int cc, float4 (&A)[TM][4], float4 (&Bv)[TN][4]) {
-    if (a.probe & 2) {
+    if (PTTS_PROBE(a) & 2) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -860,7 +874,7 @@ __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) af[i][k] = elu1(af[i][k]);
     }
-    if (a.probe & 1) return;
+    if (PTTS_PROBE(a) & 1) return;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
 #pragma unroll
@@ -1197,6 +1211,7 @@ static int choose_xcd_pn(const GemmArgs& a, int gx, int gy) {
   }
   return best;
 }
+#ifdef PTTS_PROBES
 static int back_probe() {
   static const int p = getenv("PTTS_BACK_PROBE") ? atoi(getenv("PTTS_BACK_PROBE")) : 0;
   return p;
@@ -1205,11 +1220,14 @@ static int front_probe() {  // the same probe on every uncapped launch (front pa
   static const int p = getenv("PTTS_FRONT_PROBE") ? atoi(getenv("PTTS_FRONT_PROBE")) : 0;
   return p;
 }
+#endif
 template <typename K>
 static void launch_tiled(K kernel, dim3 grid, int threads, hipStream_t s, const GemmArgs& a) {
   GemmArgs b = a;
   b.xcd_pn = choose_xcd_pn(a, (int)grid.x, (int)grid.y);
+#ifdef PTTS_PROBES
   b.probe = g_wg_cap > 0 ? back_probe() : front_probe();  // the cap is set exactly while the back part is captured
+#endif
   hipLaunchKernelGGL(kernel, grid, dim3(threads), cap_lds(kernel, std::max(a.max_wg_per_cu, g_wg_cap)), s, b);
 }
 
@@ -1246,6 +1264,24 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     PTTS_GLRB(26, 2, 2, 4, 2, 2)  // 128 x 128, 4 buffers
     PTTS_GLRB(27, 1, 4, 3, 2, 1)  //  64 x 128 (waves side by side in N)
 #undef PTTS_GLRB
+#define PTTS_GLX(L, WM_, WN_, NB_, TMW_, TNW_, MINB_)                                                 \
+  case L:                                                                                             \
+    launch_tiled((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_, MINB_, true>),                      \
+                 dim3((a.N + 32 * WN_ * TNW_ - 1) / (32 * WN_ * TNW_),                                \
+                      (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z), 256, s, a);            \
+    return;
+    // interleaved DMA issue (ILV), experiments
+    PTTS_GLX(30, 2, 2, 3, 2, 2, 1)  // 128 x 128
+    PTTS_GLX(31, 2, 2, 2, 2, 2, 2)  // 128 x 128, 2 per CU
+    PTTS_GLX(32, 2, 2, 3, 1, 1, 2)  //  64 x  64, 2 per CU
+    PTTS_GLX(33, 2, 2, 2, 1, 1, 2)  //  64 x  64, 2 buffers, 2 per CU
+    PTTS_GLX(34, 2, 2, 3, 2, 1, 1)  // 128 x  64
+    PTTS_GLX(35, 2, 2, 2, 2, 1, 2)  // 128 x  64, 2 per CU
+    PTTS_GLX(36, 2, 2, 3, 1, 2, 1)  //  64 x 128
+    PTTS_GLX(37, 2, 2, 4, 1, 1, 1)  //  64 x  64, 4 buffers
+    PTTS_GLX(38, 2, 2, 4, 2, 2, 1)  // 128 x 128, 4 buffers
+    PTTS_GLX(39, 2, 2, 3, 1, 2, 2)  //  64 x 128, 2 per CU
+#undef PTTS_GLX
     default:
       break;
   }
@@ -1456,8 +1492,7 @@ __device__ __forceinline__ float act1(float x, int act) {
 
 // Every load of a thread (its S slab float4s and the bias / gate / residual operands) is issued
 // before the first add: one memory round trip. Absent operands are read from a valid stand-in
-// address and dropped by a select (no branches around loads). Shared by the row-reduce kernel
-// and the in-launch split-K combine of the GEMM kernels (identical summation order).
+// address and dropped by a select (no branches around loads).
 template <int SMAX>
 __device__ __forceinline__ float4 rr_value(const RowReduceArgs& a, int m, int n) {
   const float* p = a.P + (long)m * a.N + n;
@@ -1579,97 +1614,6 @@ __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   const float den = sqrtf(block_sum(q, sh) / (float)a.N + a.eps);
   if (!ok) return;
   *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = rr_ln(a, m, n, d, den);
-}
-
-// ---------------------------------------------------------------------------------------------
-// In-launch split-K combine (cdna_hip_programming.md, "In-launch split-K reduction"): slab
-// stores -> vmcnt(0) on every wave -> barrier -> one lane: agent-scope release fence, vmcnt(0),
-// relaxed agent-scope ticket add; the workgroup drawing target-1 is the reducer: one lane's
-// agent-scope acquire fence + vmcnt(0) before the barrier, then plain loads of the slabs.
-// The reducer re-arms the counter for the next launch. `flag` is a word of the kernel's one LDS
-// array (a second __shared__ object would de-pipeline the LDS-DMA loop).
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool splitk_arrive(int* cnt, int target, float* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old == target - 1;
-    if (last) {
-      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last ? 1.f : 0.f;
-  }
-  __syncthreads();
-  const bool last = *flag != 0.f;
-  __syncthreads();  // the flag word is reused by the caller's LDS afterwards
-  return last;
-}
-
-// rows [m0, m0+32) x cols [n0, n0+ncols) of the row-reduce epilogue (256 threads)
-template <int SMAX>
-__device__ void splitk_tile_finish(const RowReduceArgs& a, int m0, int n0, int ncols) {
-  const int per_row = ncols / 4;
-  for (int e = threadIdx.x; e < 32 * per_row; e += 256) {
-    const int m = m0 + e / per_row, n = n0 + 4 * (e % per_row);
-    if (m >= a.M || n >= a.N) continue;
-    rr_store(a, m, n, rr_value<SMAX>(a, m, n));
-  }
-}
-__device__ void splitk_finish(const RowReduceArgs& a, int m0, int n0, int ncols) {
-  if (a.S <= 1) splitk_tile_finish<1>(a, m0, n0, ncols);
-  else if (a.S <= 2) splitk_tile_finish<2>(a, m0, n0, ncols);
-  else if (a.S <= 4) splitk_tile_finish<4>(a, m0, n0, ncols);
-  else if (a.S <= 8) splitk_tile_finish<8>(a, m0, n0, ncols);
-  else splitk_tile_finish<16>(a, m0, n0, ncols);
-}
-// LayerNorm (+modulate) of rows [m0, m0+32) from Y (N <= 1024, N % 256 == 0): one wave per row
-__device__ void splitk_rows_ln(const RowReduceArgs& a, int m0) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nq = a.N / 256;  // float4 per lane
-  for (int r = wave; r < 32; r += 4) {
-    const int m = m0 + r;
-    if (m >= a.M) break;
-    float4 v[4];
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i < nq) {
-        v[i] = *reinterpret_cast<const float4*>(a.Y + (long)m * a.ldy + 4 * lane + 256 * i);
-        sum += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-      }
-    }
-    const float mean = wave_sum(sum) / (float)a.N;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i < nq) {
-        v[i] = make_float4(v[i].x - mean, v[i].y - mean, v[i].z - mean, v[i].w - mean);
-        q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
-      }
-    }
-    const float den = sqrtf(wave_sum(q) / (float)a.N + a.eps);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i < nq) {
-        const int n = 4 * lane + 256 * i;
-        *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = rr_ln(a, m, n, v[i], den);
-      }
-    }
-  }
-}
-// whole in-launch combine for the workgroup that stored tile (bx, by) of a 32 x ncols tiling
-__device__ void splitk_combine(const GemmArgs& g, int m0, int n0, int ncols, float* flag) {
-  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-  if (!splitk_arrive(g.tickets + tile, g.S, flag)) return;
-  splitk_finish(g.rr, m0, n0, ncols);
-  if (g.fuse != 2) return;
-  if (!splitk_arrive(g.row_tickets + blockIdx.y, gridDim.x, flag)) return;
-  splitk_rows_ln(g.rr, m0);
 }
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s) {
@@ -2289,15 +2233,8 @@ void attention_step_qkv(const float* P, int S, int M, int nh, RowMap map, KvStor
   // attention shares each CU with a back-part workgroup, and this register budget keeps two of
   // its workgroups resident beside it. Steady step 0.690 -> 0.673 ms against 4 x 64 keys
   // (238 VGPRs, faster alone); 8 x 32, 4 x 48, 4 x 16, 2 x 64, 8 x 48 measured in between
-  // (tools/sweep_env.sh). PTTS_ATTN_WIDE=1 selects the 4 x 64 form.
-  static const bool wide = getenv("PTTS_ATTN_WIDE") != nullptr;
-  static const bool nt = !getenv("PTTS_NT") || (atoi(getenv("PTTS_NT")) & 2);
-  if (nt)
-    hipLaunchKernelGGL((k_attn_decode_qkv<4, 8, true>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
-  else if (wide)
-    hipLaunchKernelGGL((k_attn_decode_qkv<4, 16>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
-  else
-    hipLaunchKernelGGL((k_attn_decode_qkv<4, 8>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
+  // (tools/sweep_env.sh). KV blocks are read once per step: non-temporal loads (-1.1 % step).
+  hipLaunchKernelGGL((k_attn_decode_qkv<4, 8, true>), dim3(M, nh), dim3(256), 0, s, P, S, M, nh, map, kv, rope, O);
 }
 
 __global__ __launch_bounds__(256) void k_rope_table(float* tab, int npos) {
@@ -3008,8 +2945,12 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
   bool dead = false;
   float4 xo = make_float4(0.f, 0.f, 0.f, 0.f);  // wave 0: residual tile x[orow][ocol..+3]
   int sk = 0;
+#ifdef PTTS_PROBES  // s_memrealtime stamps of workgroups 0-3 (tools/head_stamps.py)
 #define FH_STAMP()                                                                     \
   if (a.dbg && tid == 0 && blockIdx.x < 4 && sk < 120) a.dbg[blockIdx.x * 128 + sk++] = __builtin_amdgcn_s_memrealtime()
+#else
+#define FH_STAMP() (void)sk
+#endif
   // probe layout: [entry, x0 published, 6 x 8 ResBlock stamps, final: swept, done]
   FH_STAMP();
 
