@@ -9,9 +9,16 @@ on the configs[2] job exactly as the GPU bench runs it, per utterance:
   KV is copied in), then TIMED: 40-token text prefill + 125 generated frames (forced, no EOS),
   temp 0.7 noise replaced by the deterministic temp-0 path (the per-frame cost is the same).
 
+Two builds of the same C source (oracle/Makefile):
+  blocked   libptts_cpu_fast.so (-DORC_FAST): cache-blocked AVX2/FMA GEMMs for every linear and
+            conv (the form candle's gemm crate gives the reference on a CPU). The headline value.
+  plain     libptts_oracle.so, the checker: unblocked dot loops, no FMA contraction. Reported
+            beside it (a bounded 40-frame sample).
 Two layouts:
-  per-core  P single-thread worker processes (OMP_NUM_THREADS=1), each pinned to its own core,
-            one utterance each, started together; value = P x 10 s / (last end - first start).
+  per-core  P single-thread worker processes (OMP_NUM_THREADS=1), each pinned to its own core, U
+            utterances each in sequence, started together; value = P x U x 10 s / (last end -
+            first start). P is the box's CPU share (16 on a 1-GPU box: the harness sizes worker
+            pools to it), U = 2, so the 32 utterances of the GPU's B = 32 job run on 16 cores.
   all-core  one process whose OpenMP intra-op threads use every core of the share, utterances one
             after another (Candle's B = 1 intra-op mode); value = n x 10 s / wall.
 
@@ -41,6 +48,13 @@ def _job_inputs(u):
     return prompt, ids
 
 
+def _oracle(lib_name):
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _oracle import Oracle
+
+    return Oracle(0x5EED, lib_name=lib_name)
+
+
 def _run_utterance(o, u, frames):
     """Untimed voice prefill, then the timed text prefill + frames; returns (start, end)."""
     prompt, ids = _job_inputs(u)
@@ -54,32 +68,35 @@ def _run_utterance(o, u, frames):
     return t0, time.monotonic()
 
 
-def worker(core, u, frames):
-    """One pinned single-thread process: setup, report ready, wait for go, run, report times."""
+def worker(core, u0, n_utt, frames, lib_name):
+    """One pinned single-thread process: setup (untimed voice prefill of its utterances), report
+    ready, wait for go, run its utterances one after another, report times."""
     if core >= 0:
         os.sched_setaffinity(0, {core})
-    sys.path.insert(0, str(ROOT / "tests"))
-    from _oracle import Oracle
-
-    o = Oracle(0x5EED)
-    prompt, ids = _job_inputs(u)
-    s = o.new_state(PROMPT_FRAMES + TEXT_TOKENS + frames + 8)
-    s.prefill(prompt)
+    o = _oracle(lib_name)
+    states = []
+    for u in range(u0, u0 + n_utt):
+        prompt, ids = _job_inputs(u)
+        s = o.new_state(PROMPT_FRAMES + TEXT_TOKENS + frames + 8)
+        s.prefill(prompt)
+        states.append((s, ids))
     print("ready", flush=True)
     sys.stdin.readline()
     t0 = time.monotonic()
-    s.prefill_tokens(ids)
-    lat = None
-    for _ in range(frames):
-        lat = s.step(lat)["latent"]
+    for s, ids in states:
+        s.prefill_tokens(ids)
+        lat = None
+        for _ in range(frames):
+            lat = s.step(lat)["latent"]
     print(json.dumps({"t0": t0, "t1": time.monotonic()}), flush=True)
 
 
-def per_core(procs, frames):
+def per_core(procs, frames, utts_per_proc=1, lib_name="libptts_oracle.so"):
     cores = sorted(os.sched_getaffinity(0))[:procs]
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    ps = [subprocess.Popen([sys.executable, __file__, "--worker", str(c), str(i), str(frames)], env=env,
-                           stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True) for i, c in enumerate(cores)]
+    ps = [subprocess.Popen([sys.executable, __file__, "--worker", str(c), str(i * utts_per_proc), str(utts_per_proc),
+                            str(frames), lib_name], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+          for i, c in enumerate(cores)]
     try:
         for p in ps:
             assert p.stdout.readline().strip() == "ready"
@@ -94,12 +111,9 @@ def per_core(procs, frames):
     return len(cores), wall
 
 
-def all_core(n_utt, threads, frames):
+def all_core(n_utt, threads, frames, lib_name):
     os.environ["OMP_NUM_THREADS"] = str(threads)
-    sys.path.insert(0, str(ROOT / "tests"))
-    from _oracle import Oracle
-
-    o = Oracle(0x5EED)
+    o = _oracle(lib_name)
     wall = 0.0
     for u in range(n_utt):
         t0, t1 = _run_utterance(o, u, frames)
@@ -125,28 +139,42 @@ def physical_cores():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=16, help="per-core layout: worker processes (<= CPU share)")
+    ap.add_argument("--utts-per-proc", type=int, default=2, help="per-core layout: utterances per process")
     ap.add_argument("--allcore-utts", type=int, default=2, help="all-core layout: utterances in sequence")
     ap.add_argument("--frames", type=int, default=125)
-    ap.add_argument("--worker", nargs=3, type=int, help=argparse.SUPPRESS)
+    ap.add_argument("--plain-frames", type=int, default=40, help="bounded sample of the unblocked checker build")
+    ap.add_argument("--worker", nargs=5, help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.worker:
-        worker(*a.worker)
+        c, u0, n, f, lib_name = a.worker
+        worker(int(c), int(u0), int(n), int(f), lib_name)
         return
     share = len(os.sched_getaffinity(0))
     procs = max(1, min(a.procs, share))
-    audio = a.frames * 0.08
-    n, wall = per_core(procs, a.frames)
-    out = {"value": round(n * audio / wall, 3), "unit": "audio-sec/wall-sec", "cores": n, "kind": "port",
-           "layout": f"{n} single-thread processes pinned one per core, one utterance each",
-           "sample": f"{n} utterances x ({TEXT_TOKENS}-token text prefill + {a.frames} frames), voice "
+    fast, plain = "libptts_cpu_fast.so", "libptts_oracle.so"
+    n, wall = per_core(procs, a.frames, a.utts_per_proc, fast)
+    utts = n * a.utts_per_proc
+    out = {"value": round(utts * a.frames * 0.08 / wall, 3), "unit": "audio-sec/wall-sec", "cores": n, "kind": "port",
+           "build": "blocked (libptts_cpu_fast.so: cache-blocked AVX2/FMA GEMMs, the stand-in for candle's gemm crate)",
+           "layout": f"{n} single-thread processes pinned one per core, {a.utts_per_proc} utterances each in sequence "
+                     f"({utts} utterances = the GPU job's batch)",
+           "sample": f"{utts} utterances x ({TEXT_TOKENS}-token text prefill + {a.frames} frames), voice "
                      f"({PROMPT_FRAMES}-frame prompt) precomputed; fp32 C restatement of the reference "
                      f"(Candle unbuildable offline)",
-           "wall_s": round(wall, 3), "nproc": os.cpu_count(), "affinity_cpus": share, **(physical_cores() or {})}
+           "wall_s": round(wall, 3), "per_core_realtime": round(a.frames * 0.08 * a.utts_per_proc / wall, 3),
+           "nproc": os.cpu_count(), "affinity_cpus": share, **(physical_cores() or {})}
+    if a.plain_frames > 0:
+        n2, w2 = per_core(procs, a.plain_frames, 1, plain)
+        out["plain_build"] = {"value": round(n2 * a.plain_frames * 0.08 / w2, 3), "unit": "audio-sec/wall-sec",
+                              "cores": n2, "wall_s": round(w2, 3),
+                              "build": "libptts_oracle.so (the checker: unblocked dot loops, no FMA contraction)",
+                              "sample": f"{n2} utterances x ({TEXT_TOKENS}-token prefill + {a.plain_frames} frames), "
+                                        f"one per pinned single-thread process"}
     if a.allcore_utts > 0:
         threads = procs
-        w = all_core(a.allcore_utts, threads, a.frames)
-        out["all_core"] = {"value": round(a.allcore_utts * audio / w, 3), "unit": "audio-sec/wall-sec",
-                           "threads": threads, "wall_s": round(w, 3),
+        w = all_core(a.allcore_utts, threads, a.frames, fast)
+        out["all_core"] = {"value": round(a.allcore_utts * a.frames * 0.08 / w, 3), "unit": "audio-sec/wall-sec",
+                           "threads": threads, "wall_s": round(w, 3), "build": "blocked",
                            "sample": f"{a.allcore_utts} utterances in sequence, OpenMP intra-op threads"}
     print(json.dumps(out))
 

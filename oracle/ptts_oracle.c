@@ -86,7 +86,8 @@ int orc_synth_head(uint64_t seed, const char* name, const int64_t* shape, int nd
 /* ---------------- model ---------------- */
 typedef struct { float *in_proj, *out_proj, *n1w, *n1b, *n2w, *n2b, *l1, *l2, *ls1, *ls2; } Layer;
 typedef struct { float *w, *b; int cin, cout, k, stride; } Conv; /* w repacked [cout][k][cin] */
-typedef struct { float *w, *b; int cin, cout, r; } ConvTr;     /* w as torch [cin][cout][2r] */
+typedef struct { float *w, *b; int cin, cout, r; float* wp; } ConvTr; /* w as torch [cin][cout][2r];
+                                                                     ORC_FAST: wp = [cout][2r][cin] */
 
 struct orc_model {
   uint64_t seed;
@@ -168,6 +169,12 @@ static ConvTr mkconvtr(const orc_model* m, const char* pfx, int cin, int cout, i
   c.w = orc_getw(m, nm, cin, cout, 2 * r);
   snprintf(nm, sizeof nm, "%s.bias", pfx);
   c.b = orc_getw(m, nm, cout, 0, 0);
+#ifdef ORC_FAST
+  c.wp = (float*)malloc(sizeof(float) * (size_t)cin * cout * 2 * r);
+  for (int i = 0; i < cin; ++i)
+    for (int o = 0; o < cout; ++o)
+      for (int j = 0; j < 2 * r; ++j) c.wp[((size_t)o * 2 * r + j) * cin + i] = c.w[((size_t)i * cout + o) * 2 * r + j];
+#endif
   return c;
 }
 static void mklayer(const orc_model* m, Layer* L, const char* pfx, int d, int ff, int ls) {
@@ -318,15 +325,89 @@ void orc_model_destroy(orc_model* m) {
   for (int l = 0; l < MNL; ++l) { free_layer(&m->mdec[l]); free_layer(&m->menc[l]); }
   free_conv(&m->dconv0); free_conv(&m->dfinal); free_conv(&m->econv0); free_conv(&m->efinal);
   for (int i = 0; i < 3; ++i) {
-    free_conv(&m->dres_a[i]); free_conv(&m->dres_b[i]); free(m->dtr[i].w); free(m->dtr[i].b);
+    free_conv(&m->dres_a[i]); free_conv(&m->dres_b[i]); free(m->dtr[i].w); free(m->dtr[i].b); free(m->dtr[i].wp);
     free_conv(&m->eres_a[i]); free_conv(&m->eres_b[i]); free_conv(&m->edown[i]);
   }
   free(m);
 }
 
 /* ---------------- primitive ops ---------------- */
+#ifdef ORC_FAST
+/* CPU-BASELINE BUILD ONLY (libptts_cpu_fast.so, oracle/Makefile): never the checker. A cache-
+ * blocked AVX2/FMA GEMM, y[i][n] = x[i].W[n] over K-contiguous rows (x row stride ldx), the form
+ * candle's gemm-crate matmuls and im2col convs take on a CPU: a 3-row x 4-column register tile of
+ * 8-wide FMA accumulators (12 ymm), columns in blocks of 64 so a block of W stays in L2 while the
+ * rows stream. M = 1 (the B = 1 GEMV) uses an 8-column tile sharing each x load. K % 8 tails
+ * are handled scalar. Differs from the oracle's rounding (FMA, 8-way partial sums). */
+#include <immintrin.h>
+static inline float hsum8(__m256 v) {
+  __m128 a = _mm_add_ps(_mm256_castps256_ps128(v), _mm256_extractf128_ps(v, 1));
+  a = _mm_add_ps(a, _mm_movehl_ps(a, a));
+  a = _mm_add_ss(a, _mm_movehdup_ps(a));
+  return _mm_cvtss_f32(a);
+}
+static void gemm_nt(float* y, int ldy, const float* x, long ldx, const float* W, int M, int N, int K,
+                    const float* b) {
+  const int K8 = K & ~7;
+  if (M == 1) {
+#pragma omp parallel for schedule(static) if ((long)N * K > 200000)
+    for (int n0 = 0; n0 < N; n0 += 8) {
+      const int nn = N - n0 < 8 ? N - n0 : 8;
+      __m256 acc[8];
+      for (int c = 0; c < 8; ++c) acc[c] = _mm256_setzero_ps();
+      for (int k = 0; k < K8; k += 8) {
+        const __m256 xv = _mm256_loadu_ps(x + k);
+        for (int c = 0; c < nn; ++c) acc[c] = _mm256_fmadd_ps(xv, _mm256_loadu_ps(W + (size_t)(n0 + c) * K + k), acc[c]);
+      }
+      for (int c = 0; c < nn; ++c) {
+        float v = hsum8(acc[c]);
+        for (int k = K8; k < K; ++k) v += x[k] * W[(size_t)(n0 + c) * K + k];
+        y[n0 + c] = b ? v + b[n0 + c] : v;
+      }
+    }
+    return;
+  }
+  const int nblk = (N + 63) / 64, mblk = (M + 2) / 3;
+#pragma omp parallel for collapse(2) schedule(static) if ((long)M * N * K > 200000)
+  for (int nb = 0; nb < nblk; ++nb)
+    for (int mb = 0; mb < mblk; ++mb) {
+      const int i0 = 3 * mb, ni = M - i0 < 3 ? M - i0 : 3;
+      const int ne = (nb + 1) * 64 < N ? (nb + 1) * 64 : N;
+      const float* xr[3];
+      for (int r = 0; r < 3; ++r) xr[r] = x + (size_t)(i0 + (r < ni ? r : 0)) * ldx;
+      for (int n0 = nb * 64; n0 < ne; n0 += 4) {
+        const int nn = ne - n0 < 4 ? ne - n0 : 4;
+        const float* wr[4];
+        for (int c = 0; c < 4; ++c) wr[c] = W + (size_t)(n0 + (c < nn ? c : 0)) * K;
+        __m256 acc[3][4];
+        for (int r = 0; r < 3; ++r)
+          for (int c = 0; c < 4; ++c) acc[r][c] = _mm256_setzero_ps();
+        for (int k = 0; k < K8; k += 8) {
+          const __m256 x0 = _mm256_loadu_ps(xr[0] + k), x1 = _mm256_loadu_ps(xr[1] + k), x2 = _mm256_loadu_ps(xr[2] + k);
+          for (int c = 0; c < 4; ++c) {
+            const __m256 wv = _mm256_loadu_ps(wr[c] + k);
+            acc[0][c] = _mm256_fmadd_ps(x0, wv, acc[0][c]);
+            acc[1][c] = _mm256_fmadd_ps(x1, wv, acc[1][c]);
+            acc[2][c] = _mm256_fmadd_ps(x2, wv, acc[2][c]);
+          }
+        }
+        for (int r = 0; r < ni; ++r)
+          for (int c = 0; c < nn; ++c) {
+            float v = hsum8(acc[r][c]);
+            for (int k = K8; k < K; ++k) v += xr[r][k] * wr[c][k];
+            y[(size_t)(i0 + r) * ldy + n0 + c] = b ? v + b[n0 + c] : v;
+          }
+      }
+    }
+}
+#endif
+
 /* y[M][N] = x[M][K] . W[N][K]^T (+ b)   (candle Linear: y = x W^T + b) */
 static void linear(float* y, const float* x, const float* W, const float* b, int M, int N, int K) {
+#ifdef ORC_FAST
+  gemm_nt(y, N, x, K, W, M, N, K, b);
+  return;
+#endif
 #pragma omp parallel for collapse(2) schedule(static) if ((long)M * N * K > 200000)
   for (int i = 0; i < M; ++i)
     for (int n = 0; n < N; ++n) {
@@ -551,6 +632,12 @@ static void sconv(const Conv* c, const float* x, int T, float* hist, float* y, i
   if (P) memcpy(xp, hist, sizeof(float) * (size_t)P * c->cin);
   for (int i = 0; i < T * c->cin; ++i) xp[(size_t)P * c->cin + i] = apply_elu ? elu(x[i]) : x[i];
   int To = T / c->stride;
+#ifdef ORC_FAST /* output row t's taps are the contiguous k*cin floats at row t*stride of xp */
+  gemm_nt(y, c->cout, xp, (long)c->stride * c->cin, c->w, To, c->cout, c->k * c->cin, c->b);
+  if (P) memcpy(hist, xp + (size_t)T * c->cin, sizeof(float) * (size_t)P * c->cin);
+  free(xp);
+  return;
+#endif
 #pragma omp parallel for collapse(2) schedule(static) if ((long)To * c->cout * c->k * c->cin > 200000)
   for (int t = 0; t < To; ++t)
     for (int o = 0; o < c->cout; ++o) {
@@ -573,7 +660,17 @@ static void sconvtr(const ConvTr* c, const float* x, int T, float* partial, floa
   float* full = (float*)calloc((size_t)To * c->cout, sizeof(float));
   float* e = (float*)malloc(sizeof(float) * (size_t)T * c->cin);
   for (int i = 0; i < T * c->cin; ++i) e[i] = elu(x[i]);
+#ifdef ORC_FAST /* one GEMM [T][cin] x [cout*2r][cin]^T, then the overlap-add of the 2r taps */
+  float* g = (float*)malloc(sizeof(float) * (size_t)T * c->cout * K);
+  gemm_nt(g, c->cout * K, e, c->cin, c->wp, T, c->cout * K, c->cin, NULL);
+  for (int t = 0; t < T; ++t)
+    for (int o = 0; o < c->cout; ++o)
+      for (int j = 0; j < K; ++j) full[(size_t)(t * r + j) * c->cout + o] += g[((size_t)t * c->cout + o) * K + j];
+  free(g);
+  if (0)
+#else
 #pragma omp parallel for schedule(static) if ((long)T * c->cout * c->cin * K > 200000)
+#endif
   for (int o = 0; o < c->cout; ++o)
     for (int t = 0; t < T; ++t)
       for (int j = 0; j < K; ++j) {

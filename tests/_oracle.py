@@ -8,14 +8,15 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
-_LIB = None
+ORACLE = "libptts_oracle.so"  # the checker
+CPU_FAST = "libptts_cpu_fast.so"  # same source, -DORC_FAST: the CPU-baseline build (bench only)
+_LIBS: dict = {}
 F32P = C.POINTER(C.c_float)
 
 
-def lib() -> C.CDLL:
-    global _LIB
-    if _LIB is None:
-        path = ROOT / "oracle" / "libptts_oracle.so"
+def lib(name: str = ORACLE) -> C.CDLL:
+    if name not in _LIBS:
+        path = ROOT / "oracle" / name
         if not path.exists():
             raise FileNotFoundError(f"{path} missing: run `make -C oracle` (or __graft_entry__.build())")
         L = C.CDLL(str(path))
@@ -44,8 +45,8 @@ def lib() -> C.CDLL:
         L.orc_time_embeddings.argtypes = [C.c_void_p, C.c_int, F32P]
         L.orc_bench.restype = C.c_double
         L.orc_bench.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
-        _LIB = L
-    return _LIB
+        _LIBS[name] = L
+    return _LIBS[name]
 
 
 def fp(a: np.ndarray | None):
@@ -59,8 +60,8 @@ class Oracle:
     """One synthetic-weight model (seed) on the CPU; quant = weight quantization scope
     (0 none, 1 flow_lm.*, 2 all: the oracle's quantize.rs restatement)."""
 
-    def __init__(self, seed: int = 0x5EED, quant: int = 0):
-        self.L = lib()
+    def __init__(self, seed: int = 0x5EED, quant: int = 0, lib_name: str = ORACLE):
+        self.L = lib(lib_name)
         self.m = self.L.orc_model_create_ex(seed, quant)
 
     def __del__(self):
