@@ -152,9 +152,11 @@ int ptts_voice_from_prompt(ptts_engine* e, const float* prompt, int n_frames, pt
 int ptts_voice_from_pcm(ptts_engine* e, const float* pcm, int n_samples, ptts_voice** out);
 /* The voice-cloning front end of TTSModel::get_voice_state / get_voice_state_from_bytes
  * (tts_model.rs:428-463) after the WAV decode, then get_voice_state_from_tensor (:504-577):
- * `n_samples` mono samples at `sample_rate` Hz are resampled to 24 kHz on the GPU (the
- * resample_poly rule of the Python reference's convert_audio, audio_utils.py:8-28, which the Rust
- * resample() of audio.rs:197-255 states it matches), zero-padded to whole frames and encoded.
+ * `n_samples` mono samples at `sample_rate` Hz are resampled to 24 kHz on the GPU by the
+ * resample_poly rule of the Python reference's convert_audio (audio_utils.py:8-28: the rule the
+ * reference's own ref.wav -> ref_mimi_input pair was made with), zero-padded to whole frames and
+ * encoded. The Rust driver resamples with rubato's FastFixedIn instead (audio.rs:210-231), a
+ * deliberate divergence: its parity with this path is unpinned.
  * chunk_frames = TTSModel.voice_prompt_chunk_frames: the encoder chunk length in frames; 0 = the
  * reference's adaptive rule (adaptive_voice_prompt_chunk_frames, tts_model.rs:562-577: whole
  * prompt up to 120 frames, then 120/180/240), < 0 = one pass (the Python reference,

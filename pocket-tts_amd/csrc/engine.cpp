@@ -536,11 +536,28 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   *S_out = S;
 }
 
+// Algorithmic cost of a row-reduce launch (HBM-bound): the S slabs, the operands it reads per row
+// (bias, gate, residual, LayerNorm affine, modulation) and every row it stores, plus the side jobs.
+static Op rr_op(const std::string& name, const RowReduceArgs& a) {
+  const double mn = (double)a.M * a.N;
+  double f = mn * (a.S + 1 + (a.act ? 8 : 0) + (a.ln ? 8 : 0));
+  double b = mn * a.S + (a.bias ? a.N : 0) + (a.gate ? (a.ldg ? mn : a.N) : 0) + (a.R ? mn : 0) + (a.Y ? mn : 0) +
+             (a.Y2 ? mn : 0) + (a.euler ? 2.0 * a.M * 32 : 0);
+  if (a.ln) b += mn + (a.ln_w ? 2.0 * a.N : 0) + (a.mshift ? 2.0 * mn : 0);
+  if (a.fhm) b += mn * 2.0 / 3.0;  // the fragment-order copy of the shift / scale columns
+  if (a.fill) b += 4.0 * a.fill_n4;
+  if (a.x0_hx) {  // x0 = cur W_in^T + b_in for x0_B rows
+    b += (double)a.x0_B * (32 + 512) + 32.0 * 512;
+    f += 2.0 * a.x0_B * 32 * 512;
+  }
+  return Op{name, [a](hipStream_t s) { row_reduce(a, s); }, f, 4.0 * b};
+}
+
 // The row-reduce epilogue of the split GEMM just emitted, as its own launch (an in-launch split-K
 // combine by the last-arriving workgroup measured slower on every front GEMM: ff2 43 vs 13 us with
 // the LayerNorm row finisher, ff1 15.6 vs 11.4 us tile-local).
 void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r) {
-  ops.push_back({name, [r](hipStream_t s) { row_reduce(r, s); }});
+  ops.push_back(rr_op(name, r));
 }
 
 // Y[M][N] = X[M][K] W[N][K]^T through rocBLAS (row-major as column-major Y^T = W^T X^T)
@@ -651,7 +668,12 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       const float* P = partial_;
       float* O = o_;
       const float* rope = rope_;
-      ops.push_back({p + ".attention", [=](hipStream_t s) { attention_step_qkv(P, S, M, NH, map, kv, rope, O, s); }});
+      // per row: K and V of every head over its L cached positions (8,192 B per position), the QKV
+      // slabs, the appended K/V and the output row; QK^T + PV = 4,096 flops per position
+      const double L = plan_ctx_ > 0 ? plan_ctx_ : max_ctx_ / 2.0;
+      ops.push_back({p + ".attention", [=](hipStream_t s) { attention_step_qkv(P, S, M, NH, map, kv, rope, O, s); },
+                     (double)M * 4096.0 * L,
+                     (double)M * (8192.0 * L + 4.0 * (S * 3.0 * D + 2.0 * D + D) + 64.0 * 4 * 2)});
     } else {
       {
         const float* P = partial_;
@@ -749,7 +771,9 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     const int lsd = lsd_;
     SlotState* st = st_;
     float *ys = ysilu_, *cur = cur_, *eos = eos_;
-    ops.push_back({"head.flow_cond", [=](hipStream_t s) { flow_cond(P, S, B, bias, temb, lsd, st, ys, cur, eos, s); }});
+    ops.push_back({"head.flow_cond", [=](hipStream_t s) { flow_cond(P, S, B, bias, temb, lsd, st, ys, cur, eos, s); },
+                   (double)B * NCOND * (S + 1) + 4.0 * lsd * B * FD,
+                   4.0 * ((double)S * B * NCOND + NCOND + lsd * FD + lsd * (double)B * FD + B * (LDIM + 1.0))});
   }
   // all adaLN modulations of all lsd steps in one GEMM (mlp.rs:322-368)
   linear_split(ops, "head.ada_gemm", ysilu_, FD, lsd_ * B, W(L_.ada_w), NADA, FD, &S);
@@ -913,7 +937,8 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     c.eos_out = eos_out_[hb];
     c.flags = flags_[hb];
     c.fpos = fpos_;
-    ops.push_back({"front_commit", [c](hipStream_t s) { front_commit(c, s); }});
+    ops.push_back({"front_commit", [c](hipStream_t s) { front_commit(c, s); }, 0.0,
+                   (double)B * (sizeof(SlotState) * 2 + 4.0 * (1 + 3 * LDIM + 1 + 2 + 2))});
   }
 }
 
@@ -930,7 +955,9 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     float *x = mx_, *h = mh_;
     const FrameFlags* fl = flags_[hb];
     ops.push_back({"mimi.quant_upsample",
-                   [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qin, qout, fl, x, h, lw, lb, s); }});
+                   [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qin, qout, fl, x, h, lw, lb, s); },
+                   (double)B * (2.0 * MD * LDIM + 2.0 * MD * 2 * UP + 8.0 * UP * MD),
+                   4.0 * ((double)B * (LDIM + 2 * MD + 2.0 * UP * MD) + 2.0 * MD * LDIM + MD * 2.0 * UP + 2.0 * MD)});
   }
   const int MR = B * UP;
   RowMap mmap{0, UP, 0, mpos_};
@@ -958,8 +985,13 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
                  fat ? fat_layout : 0);
       const float* qkv = mqkv_;
       float* O = mo_;
-      // RoPE + ring append inside the attention launch
-      ops.push_back({p + ".attention", [=](hipStream_t s) { attention16_qkv(qkv, MR, MNH, mmap, kv, MCTX, O, s); }});
+      // RoPE + ring append inside the attention launch. Per utterance: the K and V of its window
+      // (W keys x 8 heads x 64 x 2, read once for its 16 queries), its 16 QKV rows in, the 16
+      // output rows, the appended K/V; 16 queries x W keys x 8 heads x 64 x 4 flops = 65,536 W
+      const double Wn = plan_win_ > 0 ? plan_win_ : (double)(MCTX + UP - 1);
+      ops.push_back({p + ".attention", [=](hipStream_t s) { attention16_qkv(qkv, MR, MNH, mmap, kv, MCTX, O, s); },
+                     (double)B * 65536.0 * Wn,
+                     (double)B * (4.0 * 2 * MNH * 64 * Wn + 4.0 * UP * (3.0 * MD + MD + 2.0 * MD))});
     }
     if (bb & 8) {  // out + LayerScale + residual: one rocBLAS product, the epilogue in a reduce
       blas_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, mpartial_);
@@ -974,14 +1006,15 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       g.ldr = MD;
       g.Y = mx_;
       g.ldy = MD;
-      ops.push_back({p + ".out_reduce", [g](hipStream_t s) { row_reduce(g, s); }});
+      ops.push_back(rr_op(p + ".out_reduce", g));
     } else {
       dense_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, nullptr, ACT_NONE, W(t.ls1), mx_, mx_);
     }
     {
       const float *x = mx_, *w = W(t.n2w), *b = W(t.n2b);
       float* h = mh_;
-      ops.push_back({p + ".ln2", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); }});
+      ops.push_back({p + ".ln2", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); },
+                     8.0 * MR * MD, 4.0 * (2.0 * MR * MD + 2.0 * MD)});
     }
     if (bb & 2) {
       PTTS_REQUIRE((size_t)MR * MFF <= mpcap_, "back split-K slab buffer too small");
@@ -994,7 +1027,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       g.act = ACT_GELU;
       g.Y = mu_;
       g.ldy = MFF;
-      ops.push_back({p + ".ff1_gelu", [g](hipStream_t s) { row_reduce(g, s); }});
+      ops.push_back(rr_op(p + ".ff1_gelu", g));
     } else {
       dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
                fat ? fat_layout : 0);
@@ -1044,7 +1077,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
         r.Hout = mh_;
         r.ldh = MD;
       }
-      ops.push_back({p + ".ff2_reduce", [r](hipStream_t s) { row_reduce(r, s); }});
+      ops.push_back(rr_op(p + ".ff2_reduce", r));
     }
   }
   // SEANetDecoder (seanet.rs:396-402): conv0 -> [ELU, convtr(r), resblock] x3 -> ELU, conv(64->1).
@@ -1090,7 +1123,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     r.act = ACT_ELU;
     r.Y = a0_;
     r.ldy = 512;
-    ops.push_back({"seanet.conv0_reduce", [r](hipStream_t s) { row_reduce(r, s); }});
+    ops.push_back(rr_op("seanet.conv0_reduce", r));
   } else {
     conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, W(L_.dc0_b), nullptr,
             a0_, 16, 1, big ? l_c0 : 0, 1);
@@ -1124,7 +1157,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       rr.Y = cb_[0];
       rr.Y2 = ce_[0];
       rr.ldy = r * (ch / 2);
-      ops.push_back({p + ".convtr_reduce", [rr](hipStream_t s) { row_reduce(rr, s); }});
+      ops.push_back(rr_op(p + ".convtr_reduce", rr));
     } else if (big && blas_ && (bbs & 64)) {  // explicit [x(q-1) | x(q)] rows + one rocBLAS product
       const float *X = cin_buf, *H = hist_[1 + 2 * i];
       float* A = mcol_;
@@ -1141,7 +1174,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       rr.Y = cb_[i];
       rr.Y2 = ce_[i];
       rr.ldy = r * (ch / 2);
-      ops.push_back({p + ".convtr_reduce", [rr](hipStream_t s) { row_reduce(rr, s); }});
+      ops.push_back(rr_op(p + ".convtr_reduce", rr));
     } else {
       conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 0, W(L_.dtr_w[i]), r * (ch / 2), 2, 1,
               trb_[i], nullptr, cb_[i], T, 1, l_tr, 0, ce_[i]);
@@ -1163,7 +1196,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       g.ldr = ch;
       g.Y2 = ca_[i];
       g.ldy = ch;
-      ops.push_back({p + ".res_conv1_reduce", [g](hipStream_t s) { row_reduce(g, s); }});
+      ops.push_back(rr_op(p + ".res_conv1_reduce", g));
     } else {
       conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 0, W(L_.drb_w[i]), ch, 1, 1,
               W(L_.drb_b[i]), cb_[i], ca_[i], T, 1, l_r1, 1);
@@ -1173,7 +1206,8 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   {
     const float *X = ca_[2], *H = hist_[7], *w = W(L_.dfin_w), *b = W(L_.dfin_b);
     float* Y = pcm_[hb];
-    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, FRAME, 64, 3, w, b, Y, 0, s); }});
+    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, FRAME, 64, 3, w, b, Y, 0, s); },
+                   2.0 * B * FRAME * 3 * 64, 4.0 * ((double)B * FRAME * 64 + B * 2.0 * 64 + B * FRAME + 3 * 64 + 1)});
   }
   // ---- commit of the back part: conv histories and Mimi positions of rows with a frame
   {
@@ -1184,7 +1218,9 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     c.B = B;
     c.flags = flags_[hb];
     c.mpos = mpos_;
-    ops.push_back({"commit", [c](hipStream_t s) { step_commit(c, s); }});
+    double hb_bytes = 0;  // every history row is read from its activation and stored
+    for (int i = 0; i < 8; ++i) hb_bytes += 8.0 * B * hist_P_[i] * hist_C_[i];
+    ops.push_back({"commit", [c](hipStream_t s) { step_commit(c, s); }, 0.0, hb_bytes + 16.0 * B});
   }
 }
 
@@ -1198,6 +1234,19 @@ std::vector<Op> Engine::build_step(int B) {
 
 std::vector<std::string> Engine::plan_names(int B) {
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
+  // the attention costs are for the rows' current positions (what time_op replays): the mean
+  // FlowLM context over rows [0, B) and the mean Mimi window (positions + 16 queries, <= 265)
+  sync();
+  std::vector<int> fp(B), mp(B);
+  PTTS_HIP(hipMemcpy(fp.data(), fpos_, sizeof(int) * B, hipMemcpyDeviceToHost));
+  PTTS_HIP(hipMemcpy(mp.data(), mpos_, sizeof(int) * B, hipMemcpyDeviceToHost));
+  double L = 0, Wn = 0;
+  for (int b = 0; b < B; ++b) {
+    L += fp[b] + 1;
+    Wn += std::min(mp[b] + UP, MCTX + UP - 1);
+  }
+  plan_ctx_ = L / B;
+  plan_win_ = Wn / B;
   std::vector<std::string> v;
   char buf[64];
   for (auto& op : build_step(B)) {

@@ -161,6 +161,8 @@ class Engine {
   // (nhb_ = 3 lets front and back drift a step apart instead of running in lockstep).
   static constexpr int NHB = 3;
   int nhb_ = 3;  // buffers in use
+  // positions the attention ops' algorithmic costs are stated for (plan_names; 0 = a default)
+  double plan_ctx_ = 0, plan_win_ = 0;
   float* lat_out_[NHB] = {};
   float* eos_out_[NHB] = {};
   FrameFlags* flags_[NHB] = {};

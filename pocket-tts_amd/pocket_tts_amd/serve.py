@@ -23,7 +23,7 @@ HTTP (`create_app`, FastAPI; routes of pocket-tts-cli/src/server/routes.rs:20-30
                            noise_clamp?, lsd_steps?} -> audio/wav (handlers.rs:128-213)
   POST /stream             same body -> chunked 16-bit PCM LE (handlers.rs:215-310): the first
                            frame as soon as it exists, later frames coalesced to at most one
-                           chunk per 5 ms per stream
+                           chunk per 20 ms per stream
   POST /v1/audio/speech    OpenAI body {model, input, voice?, response_format?} -> wav / pcm
                            (handlers.rs:380-398)
 Wire formats follow crates/pocket-tts/src/audio.rs:110-185 (clamp to [-1, 1], x 32767,
@@ -54,13 +54,59 @@ VERSION = "0.1.0"
 # wire formats (audio.rs:110-185) live in .audio: pcm_i16_le_bytes, wav_bytes
 
 
+class FrameChannel:
+    """One producer (the scheduler thread), one consumer: the queue.Queue calls a Request's
+    consumers use (put / get / get_nowait / empty), without a lock and condition round trip per
+    frame. A deque append is atomic under the GIL, so put() is one append and, only while a
+    consumer is blocked in get(), one notify (the scheduler delivers 32 frames per ~0.6-ms step:
+    a locked Queue.put per frame cost it a large share of the step)."""
+
+    def __init__(self):
+        self._d: deque = deque()
+        self._cv = threading.Condition(threading.Lock())
+        self._waiting = False
+
+    def put(self, item):
+        self._d.append(item)
+        if self._waiting:  # the consumer set this before it checked the deque: it sees either
+            with self._cv:  # the appended item or this notify
+                self._cv.notify()
+
+    def get_nowait(self):
+        try:
+            return self._d.popleft()
+        except IndexError:
+            raise queue.Empty from None
+
+    def empty(self) -> bool:
+        return not self._d
+
+    def get(self, timeout: float | None = None):
+        try:
+            return self._d.popleft()
+        except IndexError:
+            pass
+        deadline = None if timeout is None else time.monotonic() + timeout
+        with self._cv:
+            self._waiting = True
+            try:
+                while not self._d:
+                    rem = None if deadline is None else deadline - time.monotonic()
+                    if rem is not None and rem <= 0:
+                        raise queue.Empty
+                    self._cv.wait(rem)
+                return self._d.popleft()
+            finally:
+                self._waiting = False
+
+
 # ---------------------------------------------------------------------------------------------
 @dataclass
 class Request:
     ids: np.ndarray
     voice: Voice
     params: GenerationParams
-    out: "queue.Queue" = field(default_factory=queue.Queue)  # np.ndarray frames, then None
+    out: FrameChannel = field(default_factory=FrameChannel)  # np.ndarray frames, then None
     slot: int = -1
     frames: int = 0
     waker: Callable[[], None] | None = None  # set by an async consumer (HTTP /stream)
@@ -172,7 +218,7 @@ class BatchScheduler:
                 req.frames += 1
                 if req.frames == 1:
                     req.times["first"] = time.time()
-                req.put(res.pcm[slot].copy())
+                req.put(res.pcm[slot])  # a view: fetch() returns fresh arrays every step
                 if res.last[slot]:
                     req.times["last"] = time.time()
                     if self.trace:
@@ -324,7 +370,9 @@ class OpenAIRequest(BaseModel):
     words: int | None = None
 
 
-CHUNK_INTERVAL_S = 0.005  # /stream: at most one chunk per stream per 5 ms after the first
+# /stream: at most one chunk per stream per 20 ms after the first (32 streams x 50 wakes/s keep the
+# event loop, which shares the GIL with the scheduler thread, well below one core)
+CHUNK_INTERVAL_S = 0.02
 
 
 async def pcm_chunks(r: Request):
@@ -332,7 +380,7 @@ async def pcm_chunks(r: Request):
     on the event loop (call_soon_threadsafe, at most one pending wake per stream); each wake
     sends every frame available at that moment as ONE chunk of 16-bit PCM, then the stream
     waits CHUNK_INTERVAL_S before the next. The first frame goes out as soon as it exists; later
-    frames coalesce, so 32 streams of a GPU producing ~1000x real time cost at most 200 chunks/s
+    frames coalesce, so 32 streams of a GPU producing ~4000x real time cost at most 50 chunks/s
     each instead of one event-loop round trip per 80-ms frame (which throttled the whole server).
     """
     import asyncio
@@ -491,7 +539,7 @@ def _worker_engine(args, Engine):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     kw = dict(max_slots=args.slots, max_ctx=args.max_ctx, weights_path=args.weights, pipeline=True)
-    if world == 1:
+    if "WORLD_SIZE" not in os.environ:  # a plain single-GPU server
         return Engine(device=local, **kw), 0, 1, None
     import torch
     import torch.distributed as dist
@@ -532,6 +580,8 @@ def main(argv=None):
     ap.add_argument("--tokenizer", default=None)
     ap.add_argument("--weights", default=None)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--torchrun", action="store_true",
+                    help="launch the worker(s) as torch.distributed ranks even for --gpus 1 (the N-GPU path)")
     ap.add_argument("--slots", type=int, default=32)
     ap.add_argument("--max-ctx", type=int, default=1024)
     ap.add_argument("--host", default="127.0.0.1")
@@ -541,7 +591,7 @@ def main(argv=None):
     args = ap.parse_args(argv)
     import sys
 
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.torchrun) and "WORLD_SIZE" not in os.environ:
         import socket
         import subprocess
 
@@ -569,10 +619,13 @@ def main(argv=None):
         name, path = spec.split("=", 1)
         if path.endswith(".npy"):
             voices[name] = engine.voice_from_prompt(np.load(path, allow_pickle=False).astype(np.float32))
-        else:
-            from .tts_model import read_wav_mono
+        else:  # a WAV voice prompt: resampled to 24 kHz on the GPU, Mimi-encoded (tts_model.rs:446-463)
+            from .audio import read_wav
 
-            voices[name] = engine.voice_from_pcm(read_wav_mono(path))
+            audio, sr = read_wav(path)
+            if audio.shape[0] != 1:
+                raise SystemExit(f"voice prompt {path} must be mono")
+            voices[name] = engine.voice_from_audio(audio[0], sr)
     if not voices:
         raise SystemExit("at least one --voice NAME=path is required")
     service = TTSService(BatchScheduler(engine), voices, default_voice=next(iter(voices)),
