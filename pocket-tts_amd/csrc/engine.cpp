@@ -1265,7 +1265,9 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
   if (part == 0) build_front(ops, B, hb);
   else build_back(ops, B, hb, qp);
   hipGraph_t g = nullptr;
-  PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+  // captured on the stream it is launched on (the back part of a pipelined step: stream_be_)
+  hipStream_t cs = part == 1 && pipeline_ ? stream_be_ : stream_;
+  PTTS_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
   // back part of a pipelined step: its launches leave room for the concurrent front part
   set_wg_cap(part == 1 && pipeline_ ? back_cap_ : 0);
   // per-op cap override for back-part launches: PTTS_OP_CAP="name=cap,..." (tuning)
@@ -1279,22 +1281,22 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
         if (at != std::string::npos && (at == 0 || e[at - 1] == ',')) cap = atoi(e.c_str() + at + key.size());
         set_wg_cap(cap);
       }
-      op.fn(stream_);
+      op.fn(cs);
     }
     if (part == 0) {  // the hand-off timeout word, read by fetch() without a device round trip
-      PTTS_HIP(hipMemcpyAsync(h_err_, herr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
+      PTTS_HIP(hipMemcpyAsync(h_err_, herr_, sizeof(int), hipMemcpyDeviceToHost, cs));
     } else {  // the frame of this buffer leaves HBM inside the step (fetch() reads host memory)
-      PTTS_HIP(hipMemcpyAsync(h_pcm_[hb], pcm_[hb], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, stream_));
+      PTTS_HIP(hipMemcpyAsync(h_pcm_[hb], pcm_[hb], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, cs));
       PTTS_HIP(hipMemcpyAsync(h_meta_[hb], meta_[hb], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
-                              stream_));
+                              cs));
     }
   } catch (...) {
     set_wg_cap(0);
-    (void)hipStreamEndCapture(stream_, &g);
+    (void)hipStreamEndCapture(cs, &g);
     throw;
   }
   set_wg_cap(0);
-  PTTS_HIP(hipStreamEndCapture(stream_, &g));
+  PTTS_HIP(hipStreamEndCapture(cs, &g));
   hipGraphExec_t ge = nullptr;
   PTTS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   graph_defs_[key] = g;
