@@ -8,8 +8,6 @@
 //   activations                row-major [rows][features]; Mimi/SEANet channels-last [slot][time][ch]
 #include "engine.h"
 
-#include <rocblas/rocblas.h>
-
 #include <hip/hip_ext.h>
 
 #include <algorithm>
@@ -50,6 +48,12 @@ static void tile_override(const std::string& name, int& layout, int& ksplit) {
   }
 }
 
+// layouts served by k_gemm_glds (kernels.hip gemm_launch): the only ones that split a conv's K
+static bool lds_dma_layout(int layout) {
+  return (layout >= 6 && layout <= 8) || (layout >= 11 && layout <= 16) || (layout >= 21 && layout <= 27) ||
+         (layout >= 30 && layout <= 39);
+}
+
 float* Engine::dalloc(size_t n) {
   void* p = nullptr;
   PTTS_HIP(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(float)));
@@ -81,13 +85,6 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_REQUIRE(dev_ >= 0 && dev_ < ndev, "HIP device ordinal out of range");
   PTTS_HIP(hipSetDevice(dev_));
   PTTS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  if (!getenv("PTTS_BLAS") || atoi(getenv("PTTS_BLAS")) != 0) {
-    rocblas_handle h = nullptr;
-    if (rocblas_create_handle(&h) == rocblas_status_success) {
-      (void)rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
-      blas_ = h;
-    }
-  }
 
   L_ = pack_weights(nullptr, nullptr);
   if (cfg.weight_blob) {
@@ -120,13 +117,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
     eos_out_[q] = meta_[q] + (size_t)B * (LDIM + 2);
     pcm_[q] = dalloc((size_t)B * FRAME);
   }
-  // back part's own split-K slabs: Mimi QKV (2 slabs), Mimi ff2 (4), SEANet conv0 (8), convtr0 (4)
-  mpcap_ = std::max({(size_t)2 * B * UP * 3 * MD, (size_t)8 * B * UP * MD, (size_t)4 * B * UP * RATIOS[0] * (MD / 2),
-                     (size_t)B * FRAME * 64});  // the last: stage-2 k1 conv as one rocBLAS product
+  // back part's own split-K slabs: up to 8 slices of the Mimi / conv0 rows (B * 16 x 512), 4 of the
+  // stage-0 transposed conv (B * 16 x 6 * 256)
+  mpcap_ = std::max({(size_t)8 * B * UP * MD, (size_t)4 * B * UP * RATIOS[0] * (MD / 2)});
   mpartial_ = dalloc(mpcap_);
-  // explicit conv operands for the rocBLAS convs (PTTS_BACK_BLAS 64 / 128): the largest is the
-  // stage-2 transposed conv's [B * 480][2 * 128]
-  mcol_ = dalloc((size_t)B * 480 * 2 * 128);
 
   // streaming conv histories (SEANetDecoder, seanet.rs:307-402): source T, channels, rows kept
   const int hT[8] = {16, 16, 96, 96, 480, 480, 1920, 1920};
@@ -235,7 +229,6 @@ Engine::~Engine() {
   if (stream_be_) (void)hipStreamSynchronize(stream_be_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
-  if (blas_) (void)rocblas_destroy_handle((rocblas_handle)blas_);  // after every graph that recorded it
   for (int q = 0; q < NHB; ++q) {
     if (ev_front_[q]) (void)hipEventDestroy(ev_front_[q]);
     if (ev_back_[q]) (void)hipEventDestroy(ev_back_[q]);
@@ -443,8 +436,10 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   if (M <= 64 && N >= 3072) {
     layout = 7;  // 2-buffer LDS (40 KB) co-resides with the back part
     S = std::max(1, std::min(8, K / 64));
-  } else if (M >= 256) {  // prefill passes: MFMA-bound, 64x64 LDS-DMA tiles, no split
-    layout = 12;
+  } else if (M >= 256) {  // prefill passes (text admission, M = 48 rows per slot): MFMA-bound,
+    // 128x64 / 64x128 LDS-DMA tiles with the DMAs interleaved between the MFMAs, two workgroups
+    // per CU, no split (tools/mm_bench.hip at M = 1536: qkv 89, out 73, ff1 108, ff2 79 TF/s)
+    layout = N >= 3072 ? 35 : 39;
     S = 1;
   } else if (M <= 64 && K >= 4096) {  // FlowLM ff2: 8 slabs (tools/gemm_bench.hip flow.ff2: 8.5 -> 7.3 us)
     S = 8;
@@ -457,24 +452,6 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   // large matrices (qkv, ff1, ff2, adaLN; >= 2M weights): below that the launch is latency-bound
   // and the f32 copy of the same values is as fast (tools/w8_probe.py). Prefill passes
   // (M >= 256) keep the f32 copy too: they are MFMA-bound.
-  if (blas_ && M >= 256 && name.rfind("prefill", 0) == 0 && q8map_.find(Wt) == q8map_.end() &&
-      f8map_.find(Wt) == f8map_.end()) {
-    // row-major Y[M][N] = X[M][K] W[N][K]^T as column-major Y^T (N x M) = W^T(N x K) X^T(K x M)
-    PTTS_REQUIRE((size_t)M * N <= pcap_, "split-K partial buffer too small");
-    rocblas_handle h = (rocblas_handle)blas_;
-    float* part = partial_;
-    ops.push_back({name,
-                   [=](hipStream_t s) {
-                     const float one = 1.f, zero = 0.f;
-                     if (rocblas_set_stream(h, s) != rocblas_status_success ||
-                         rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &one, Wt, K,
-                                       X, (rocblas_int)ldx, &zero, part, N) != rocblas_status_success)
-                       throw Error(PTTS_ERR_HIP, "rocblas_sgemm failed");
-                   },
-                   2.0 * M * N * K, 4.0 * ((double)N * K + (double)M * K + (double)M * N)});
-    *S_out = 1;
-    return;
-  }
   auto gv = gvmap_.find(Wt);
   if (gv != gvmap_.end() && M <= 64 && (gemv_mask_ & gv->second.bit)) {  // register-resident weights (derive_gemv)
     const GemvShape g = gv->second.g;
@@ -560,22 +537,6 @@ void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowRed
   ops.push_back(rr_op(name, r));
 }
 
-// Y[M][N] = X[M][K] W[N][K]^T through rocBLAS (row-major as column-major Y^T = W^T X^T)
-void Engine::blas_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,
-                     int K, float* Y) {
-  PTTS_REQUIRE(blas_ != nullptr, "rocBLAS handle unavailable");
-  rocblas_handle h = (rocblas_handle)blas_;
-  ops.push_back({name,
-                 [=](hipStream_t s) {
-                   const float one = 1.f, zero = 0.f;
-                   if (rocblas_set_stream(h, s) != rocblas_status_success ||
-                       rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &one, Wt, K, X, K,
-                                     &zero, Y, N) != rocblas_status_success)
-                     throw Error(PTTS_ERR_HIP, "rocblas_sgemm failed");
-                 },
-                 2.0 * M * N * K, 4.0 * ((double)N * K + (double)M * K + (double)M * N)});
-}
-
 void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,
                       int K, const float* bias, int act, const float* rscale, const float* R, float* Y, int layout) {
   PTTS_REQUIRE(K % 32 == 0, "GEMM K must be a multiple of 32");
@@ -613,8 +574,7 @@ void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float*
   PTTS_REQUIRE(!(layout == 8 || layout == 15 || layout == 16) || cin % 64 == 0, "BK 64 tiles need cin % 64 == 0");
   // ksplit > 1: single-phase conv on an LDS-DMA tile, K split into ksplit partial slabs in the
   // back part's slab buffer; the caller adds the row-reduce epilogue
-  PTTS_REQUIRE(ksplit == 1 || (phases == 1 && layout >= 6 && layout != 9 && layout != 10 && layout < 17),
-               "K-split convs need a single-phase LDS-DMA tile");
+  PTTS_REQUIRE(ksplit == 1 || (phases == 1 && lds_dma_layout(layout)), "K-split convs need a single-phase LDS-DMA tile");
   GemmArgs a{};
   a.mode = 1;
   a.layout = layout;
@@ -942,9 +902,42 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
   }
 }
 
+// Tiles of the back part's GEMMs and convs at B >= 16 (the MFMA-bound shapes), one row per launch:
+// LDS-DMA tile layout (kernels.hip gemm_launch) and split-K slices. Chosen from tools/mm_bench.hip
+// (each launch alone on the chip, B = 32) and A/B runs of the pipelined step, where the back part
+// shares every CU with the latency-bound front part. Below B = 16 every GEMM runs on
+// the 32x32 register tile (layout 0) with the split-K noted at the launch.
+struct BackTile {
+  int layout, splits;
+};
+static BackTile back_tile(const std::string& op, bool pipeline) {
+  static const struct {
+    const char* op;
+    BackTile seq, pipe;
+  } table[] = {
+      {"mimi.qkv", {33, 1}, {33, 1}},
+      {"mimi.out", {33, 4}, {33, 4}},
+      {"mimi.ff1", {33, 1}, {33, 1}},
+      {"mimi.ff2", {33, 4}, {33, 4}},
+      {"seanet.conv0", {33, 4}, {33, 4}},
+      {"seanet.up0.convtr", {33, 4}, {33, 4}},
+      {"seanet.up1.convtr", {33, 1}, {33, 1}},
+      {"seanet.up2.convtr", {33, 1}, {33, 1}},
+  };
+  for (const auto& t : table)
+    if (op == t.op) return pipeline ? t.pipe : t.seq;
+  throw Error(PTTS_ERR_INVALID, "no tile for " + op);
+}
+
 // BACK part of a step: Mimi decode of the frames the front part left in buffer `hb`; `qp` is the
 // frame's parity for the quantizer history (the previous frame's quantizer output is in qp ^ 1).
 void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
+  const bool big = B >= 16;  // B * 16 >= 256 Mimi rows: the LDS-DMA tiles fill the chip
+  auto tile = [&](const std::string& op, int small_splits) {
+    BackTile t = big ? back_tile(op, pipeline_) : BackTile{0, small_splits};
+    tile_override(op, t.layout, t.splits);  // probe builds only (tools/back_tune.py)
+    return t;
+  };
   // ---- Mimi decode (mimi.rs:143-157): quantize + upsample, decoder transformer, SEANet decoder
   {
     const float *lat = lat_out_[hb], *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w),
@@ -961,109 +954,80 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   }
   const int MR = B * UP;
   RowMap mmap{0, UP, 0, mpos_};
+  // a split-K GEMM into the back part's own slab buffer, its epilogue in a row reduce
+  auto split_gemm = [&](const std::string& name, const float* X, int M, const float* Wt, int N, int K, BackTile t) {
+    PTTS_REQUIRE(t.splits >= 1 && t.splits <= 16, name + ": split-K 1..16");
+    PTTS_REQUIRE((size_t)t.splits * M * N <= mpcap_, "back split-K slab buffer too small");
+    GemmArgs a{};
+    a.mode = 0;
+    a.layout = t.layout;
+    a.M = M;
+    a.N = N;
+    a.K = K;
+    a.Nw = (N + 31) / 32 * 32;
+    a.X = X;
+    a.ldx = K;
+    a.W = Wt;
+    a.S = t.splits;
+    a.partial = mpartial_;
+    const int S = t.splits;
+    ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
+                   4.0 * ((double)N * K + (double)M * K + (double)S * M * N)});
+  };
   for (int l = 0; l < MNL; ++l) {
     const Layout::TL& t = L_.mdec[l];
     const std::string p = "mimi.l" + std::to_string(l);
     KvStore kv{ring_ + (long)l * ring_layer_, ring_slot_, RING};
-    // fat GEMMs (B*16 rows): LDS-DMA tiles once there are enough rows to fill the chip. BK 64,
-    // 3 buffers alone on the chip (tools/gemm_bench.hip); BK 32, 2 buffers in pipelined stepping,
-    // whose lighter workgroups leave more room to the concurrent front part (qkv + ff1 at 6:
-    // steady step 0.6661 -> 0.6587 ms, tools/sweep_env.sh over PTTS_OVR)
-    const bool fat = MR >= 256;
-    const int fat_layout = pipeline_ ? 6 : 15;
-    // Mimi GEMMs through rocBLAS (fat shapes only), PTTS_BACK_BLAS bits: 1 qkv, 2 ff1 (+ a GELU
-    // pass), 4 ff2 (one unsplit product into the existing reduce). Pipelined default 4: once the
-    // back part bounded the step, ff2 on rocBLAS measured 0.6205 -> 0.6028 and 0.6124 -> 0.6070
-    // ms (medians of 3-4, two boxes); qkv +0.7 % / -0.4 %, ff1 slower, all three 0.6103; bit 8
-    // (out + LayerScale/residual reduce) 0.6146 against 0.6121. Bits 16 / 32 (SEANet k1 convs,
-    // below) measured 0.842 / 0.683 ms: those skinny products stay on the hand-written tiles
-    const int bb = !(fat && blas_) ? 0 : getenv("PTTS_BACK_BLAS") ? atoi(getenv("PTTS_BACK_BLAS")) : pipeline_ ? 4 : 0;
-    {  // QKV: one pass, 64x64 LDS-DMA tiles once there are enough rows (tools/gemm_bench.hip c2.mimi.qkv)
-      if (bb & 1) blas_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, mqkv_);
-      else
-        dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_,
-                 fat ? fat_layout : 0);
+    {  // QKV in one pass; RoPE + ring append inside the attention launch
+      const BackTile tq = tile("mimi.qkv", 1);
+      dense_op(ops, p + ".qkv_gemm", mh_, MR, W(t.in_proj), 3 * MD, MD, nullptr, ACT_NONE, nullptr, nullptr, mqkv_,
+               tq.layout);
       const float* qkv = mqkv_;
       float* O = mo_;
-      // RoPE + ring append inside the attention launch. Per utterance: the K and V of its window
-      // (W keys x 8 heads x 64 x 2, read once for its 16 queries), its 16 QKV rows in, the 16
-      // output rows, the appended K/V; 16 queries x W keys x 8 heads x 64 x 4 flops = 65,536 W
+      // per utterance: the K and V of its window (W keys x 8 heads x 64 x 2, read once for its 16
+      // queries), its 16 QKV rows in, the 16 output rows, the appended K/V; 16 queries x W keys x
+      // 8 heads x 64 x 4 flops = 65,536 W
       const double Wn = plan_win_ > 0 ? plan_win_ : (double)(MCTX + UP - 1);
       ops.push_back({p + ".attention", [=](hipStream_t s) { attention16_qkv(qkv, MR, MNH, mmap, kv, MCTX, O, s); },
                      (double)B * 65536.0 * Wn,
                      (double)B * (4.0 * 2 * MNH * 64 * Wn + 4.0 * UP * (3.0 * MD + MD + 2.0 * MD))});
     }
-    if (bb & 8) {  // out + LayerScale + residual: one rocBLAS product, the epilogue in a reduce
-      blas_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, mpartial_);
-      RowReduceArgs g{};
-      g.P = mpartial_;
-      g.S = 1;
-      g.M = MR;
-      g.N = MD;
-      g.gate = W(t.ls1);
-      g.ldg = 0;
-      g.R = mx_;
-      g.ldr = MD;
-      g.Y = mx_;
-      g.ldy = MD;
-      ops.push_back(rr_op(p + ".out_reduce", g));
-    } else {
-      dense_op(ops, p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, nullptr, ACT_NONE, W(t.ls1), mx_, mx_);
-    }
-    {
-      const float *x = mx_, *w = W(t.n2w), *b = W(t.n2b);
-      float* h = mh_;
-      ops.push_back({p + ".ln2", [=](hipStream_t s) { layernorm(x, MD, h, MD, MR, MD, w, b, 1e-5f, s); },
-                     8.0 * MR * MD, 4.0 * (2.0 * MR * MD + 2.0 * MD)});
-    }
-    if (bb & 2) {
-      PTTS_REQUIRE((size_t)MR * MFF <= mpcap_, "back split-K slab buffer too small");
-      blas_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, mpartial_);
-      RowReduceArgs g{};
-      g.P = mpartial_;
-      g.S = 1;
-      g.M = MR;
-      g.N = MFF;
-      g.act = ACT_GELU;
-      g.Y = mu_;
-      g.ldy = MFF;
-      ops.push_back(rr_op(p + ".ff1_gelu", g));
-    } else {
-      dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_,
-               fat ? fat_layout : 0);
-    }
-    {  // K = 2048, split-K; LayerScale + residual (+ the next layer's norm1) in the reduce. Fat:
-       // 64x64 LDS-DMA tiles, 4 slices; few rows (B < 16, the first-chunk path): 32x32 tiles, 8
-       // slices (16 -> 128 workgroups: 18.2 -> ~7 us at B = 1, and no separate norm1 launch)
-      int S = fat ? 4 : 8, lay = fat ? 6 : 0;
-      tile_override(p + ".ff2_gemm", lay, S);
-      PTTS_REQUIRE(S >= 1 && S <= 16 &&
-                       (lay == 0 || lay == 6 || lay == 7 || lay == 11 || lay == 12 || lay == 13 || lay == 14),
-                   "mimi ff2: split-K 1..16 on a single-phase tile");
-      GemmArgs a{};
-      a.mode = 0;
-      a.layout = lay;
-      a.M = MR;
-      a.N = MD;
-      a.K = MFF;
-      a.Nw = MD;
-      a.X = mu_;
-      a.ldx = MFF;
-      a.W = W(t.l2);
-      a.S = S;
-      a.partial = mpartial_;
-      if (bb & 4) S = 1;
-      PTTS_REQUIRE((size_t)S * MR * MD <= mpcap_, "back split-K slab buffer too small");
-      if (bb & 4) blas_op(ops, p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, mpartial_);
-      else
-        ops.push_back({p + ".ff2_gemm", [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * MR * MD * MFF,
-                       4.0 * ((double)MD * MFF + (double)MR * MFF + 2.0 * MR * MD)});
+    {  // out projection, split-K; LayerScale + residual and this layer's norm2 in the reduce
+      const BackTile to = tile("mimi.out", 4);
+      split_gemm(p + ".out_gemm", mo_, MR, W(t.out_proj), MD, MD, to);
       RowReduceArgs r{};
       r.P = mpartial_;
-      r.S = S;
+      r.S = to.splits;
       r.M = MR;
       r.N = MD;
-      r.gate = W(t.ls2);  // per-column LayerScale: gate row stride 0
+      r.gate = W(t.ls1);  // per-column LayerScale: gate row stride 0
+      r.ldg = 0;
+      r.R = mx_;
+      r.ldr = MD;
+      r.Y = mx_;
+      r.ldy = MD;
+      r.ln = 1;
+      r.ln_w = W(t.n2w);
+      r.ln_b = W(t.n2b);
+      r.eps = 1e-5f;
+      r.Hout = mh_;
+      r.ldh = MD;
+      ops.push_back(rr_op(p + ".out_reduce_ln2", r));
+    }
+    {  // linear1 + GELU in the tile epilogue
+      const BackTile tf = tile("mimi.ff1", 1);
+      dense_op(ops, p + ".ff1_gemm", mh_, MR, W(t.l1), MFF, MD, nullptr, ACT_GELU, nullptr, nullptr, mu_, tf.layout);
+    }
+    {  // linear2 (K = 2048), split-K; LayerScale + residual (+ the next layer's norm1) in the reduce.
+       // Few rows (B < 16, the first-chunk path): 32x32 tiles, 8 slices (16 -> 128 workgroups)
+      const BackTile tf = tile("mimi.ff2", 8);
+      split_gemm(p + ".ff2_gemm", mu_, MR, W(t.l2), MD, MFF, tf);
+      RowReduceArgs r{};
+      r.P = mpartial_;
+      r.S = tf.splits;
+      r.M = MR;
+      r.N = MD;
+      r.gate = W(t.ls2);
       r.ldg = 0;
       r.R = mx_;
       r.ldr = MD;
@@ -1082,38 +1046,17 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   }
   // SEANetDecoder (seanet.rs:396-402): conv0 -> [ELU, convtr(r), resblock] x3 -> ELU, conv(64->1).
   // Every ELU is applied once, by the producer of the activation (elu_out / the dual store Y2),
-  // so the consumers' operand loads are plain: a0, ce, cv and ca hold ELU'd activations (and so
-  // do the histories of the convs that read them; elu(0) = 0 keeps the zero reset valid), cb
-  // stays raw for the resblock skip. Transposed convs run with their r phases merged into N: one
-  // 2-tap conv over rows (x[q-1], x[q]) whose output row q is the r time rows q*r .. q*r+r-1 of
-  // the channels-last output, N = r * Cout (packed [r][Cout][2][Cin] = [r*Cout][2*Cin]).
-  const bool big = B >= 16;
-  // PTTS_BACK_BLAS bits for SEANet convs as rocBLAS products (+ reduce): 16 stage-2 k1 conv, 32
-  // stage-0/1 k1 convs, 64 transposed convs and 128 conv0 (both on an explicit im2col operand).
-  // All measured slower in the pipelined step (0.842 / 0.683 / 0.667 / 0.622 against 0.603-0.612
-  // ms): the hand-written implicit-GEMM tiles stay.
-  const int bbs = getenv("PTTS_BACK_BLAS") ? atoi(getenv("PTTS_BACK_BLAS")) : 0;
-  // Tiles: the tools/gemm_bench.hip choices (each launch alone on the chip, B = 32), except where
-  // the pipelined step (tools/sweep_env.sh over PTTS_OVR, steady step time) prefers lighter
-  // workgroups beside the concurrent front part (the choices move with the front/back balance:
-  // see the res_conv3 note below). Tiles that were faster alone under the per-CU cap (tools/
-  // back_tune.py: 32 us less back time in all) each made the pipelined step slower while the
-  // front part was the longer one.
-  int l_c0 = 6, s_c0 = 8;  // conv0 tile / split-K (PTTS_OVR may change them)
-  tile_override("seanet.conv0", l_c0, s_c0);
-  const bool conv_blas = big && blas_ && (bbs & 128);
-  if (s_c0 > 1 || conv_blas) {  // K = 7 x 512: 64x64 LDS-DMA tiles, 8-way split-K, bias + ELU in the
-                                // reduce (every B: at B = 1 the unsplit launch had 16 workgroups, 27.4 us)
-    if (conv_blas) {  // explicit operand + one rocBLAS product
-      s_c0 = 1;
-      const float *X = mx_, *H = hist_[0];
-      float* A = mcol_;
-      ops.push_back({"seanet.conv0_im2col", [=](hipStream_t s) { im2col(X, H, B, 16, 1, 6, 512, 7, A, s); }});
-      blas_op(ops, "seanet.conv0", mcol_, B * 16, W(L_.dc0_w), 512, 7 * 512, mpartial_);
-    } else {
-      conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
-              nullptr, 16, 1, l_c0, 0, nullptr, s_c0);
-    }
+  // so the consumers' operand loads are plain: a0, ce and ca hold ELU'd activations (and so do the
+  // histories of the convs that read them; elu(0) = 0 keeps the zero reset valid), cb stays raw for
+  // the resblock skip. Transposed convs run with their r phases merged into N: one 2-tap conv over
+  // rows (x[q-1], x[q]) whose output row q is the r time rows q*r .. q*r+r-1 of the channels-last
+  // output, N = r * Cout (packed [r][Cout][2][Cin] = [r*Cout][2*Cin]).
+  {  // conv0 (K = 7 x 512, M = 16 B rows): split-K fills the chip; bias + ELU in the reduce (every B:
+     // at B = 1 the unsplit launch had 16 workgroups, 27.4 us)
+    const BackTile tc = tile("seanet.conv0", 8);
+    const int s_c0 = std::max(tc.splits, 2);
+    conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
+            nullptr, 16, 1, big ? tc.layout : 6, 0, nullptr, s_c0);
     RowReduceArgs r{};
     r.P = mpartial_;
     r.S = s_c0;
@@ -1124,33 +1067,20 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     r.Y = a0_;
     r.ldy = 512;
     ops.push_back(rr_op("seanet.conv0_reduce", r));
-  } else {
-    conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, W(L_.dc0_b), nullptr,
-            a0_, 16, 1, big ? l_c0 : 0, 1);
   }
   const float* cin_buf = a0_;
   int T = 16, ch = 512;
   for (int i = 0; i < 3; ++i) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
-    // per-stage tiles (tools/gemm_bench.hip, rb.* cases, B = 32; see above for pipelined)
-    const int l_tr = big ? (i == 0 ? 20 : (i == 1 ? 13 : 22)) : 0;
-    // stages 0-1 k3 convs: the register-blocked tiles in pipelined stepping too since the front
-    // part got shorter (flow-head chain 74 -> 47 us): steady step 0.626 -> 0.608 ms (medians of 3);
-    // while the front was the longer part, the 64x64 LDS-DMA tile (6) was 1.6 % faster
-    const int l_r3 = !big ? 0 : i == 2 ? 14 : (i == 0 ? 18 : 20);
-    // stage 2's k1 conv (M = 32 * 3840 rows, N = 64): 128x64 register-blocked LDS-DMA tile in
-    // pipelined stepping, steady step 0.6310 -> 0.6188 ms (medians of 4; its 64x64 / 128x128
-    // neighbours 22 / 21 measured 0.644 / 0.652)
-    const int l_r1 = !big ? 0 : (i == 2 && pipeline_) ? 23 : 6;
-    int l_t0 = 6, s_t0 = i == 0 ? 4 : 1;  // split-K of the first transposed conv (PTTS_OVR may change it)
-    if (i == 0) tile_override(p + ".convtr", l_t0, s_t0);
-    if (big && i == 0 && s_t0 > 1 && !(blas_ && (bbs & 64))) {  // M = 16 B rows only: 4-way split-K fills the chip; bias + dual store in the reduce
+    const BackTile tt = tile(p + ".convtr", 1);
+    if (big && tt.splits > 1) {  // stage 0 (M = 16 B rows): split-K; bias + dual raw / ELU store in the reduce
+      PTTS_REQUIRE(i == 0, "split-K transposed conv: stage 0 only");
       conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1], 1, 1, 0, W(L_.dtr_w[0]), r * (ch / 2), 2, 1, nullptr,
-              nullptr, nullptr, T, 1, l_t0, 0, nullptr, s_t0);
+              nullptr, nullptr, T, 1, tt.layout, 0, nullptr, tt.splits);
       RowReduceArgs rr{};
       rr.P = mpartial_;
-      rr.S = s_t0;
+      rr.S = tt.splits;
       rr.M = B * T;
       rr.N = r * (ch / 2);
       rr.bias = trb_[0];
@@ -1158,48 +1088,24 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       rr.Y2 = ce_[0];
       rr.ldy = r * (ch / 2);
       ops.push_back(rr_op(p + ".convtr_reduce", rr));
-    } else if (big && blas_ && (bbs & 64)) {  // explicit [x(q-1) | x(q)] rows + one rocBLAS product
-      const float *X = cin_buf, *H = hist_[1 + 2 * i];
-      float* A = mcol_;
-      const int Tc = T, cc = ch;
-      PTTS_REQUIRE((size_t)B * T * r * (ch / 2) <= mpcap_, "back split-K slab buffer too small");
-      ops.push_back({p + ".convtr_im2col", [=](hipStream_t s) { im2col(X, H, B, Tc, 1, 1, cc, 2, A, s); }});
-      blas_op(ops, p + ".convtr", mcol_, B * T, W(L_.dtr_w[i]), r * (ch / 2), 2 * ch, mpartial_);
-      RowReduceArgs rr{};
-      rr.P = mpartial_;
-      rr.S = 1;
-      rr.M = B * T;
-      rr.N = r * (ch / 2);
-      rr.bias = trb_[i];
-      rr.Y = cb_[i];
-      rr.Y2 = ce_[i];
-      rr.ldy = r * (ch / 2);
-      ops.push_back(rr_op(p + ".convtr_reduce", rr));
     } else {
       conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 0, W(L_.dtr_w[i]), r * (ch / 2), 2, 1,
-              trb_[i], nullptr, cb_[i], T, 1, l_tr, 0, ce_[i]);
+              trb_[i], nullptr, cb_[i], T, 1, tt.layout, 0, ce_[i]);
     }
     T *= r;
     ch /= 2;
-    conv_op(ops, p + ".res_conv3", ce_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 0, W(L_.dra_w[i]), ch / 2, 3, 1,
-            W(L_.dra_b[i]), nullptr, cv_[i], T, 1, l_r3, 1);
-    if (big && blas_ && (bbs & (i == 2 ? 16 : 32))) {  // k1 conv = plain GEMM: rocBLAS, then bias + skip + ELU
-      PTTS_REQUIRE((size_t)B * T * ch <= mpcap_, "back split-K slab buffer too small");
-      blas_op(ops, p + ".res_conv1", cv_[i], B * T, W(L_.drb_w[i]), ch, ch / 2, mpartial_);
-      RowReduceArgs g{};
-      g.P = mpartial_;
-      g.S = 1;
-      g.M = B * T;
-      g.N = ch;
-      g.bias = W(L_.drb_b[i]);
-      g.R = cb_[i];
-      g.ldr = ch;
-      g.Y2 = ca_[i];
-      g.ldy = ch;
-      ops.push_back(rr_op(p + ".res_conv1_reduce", g));
-    } else {
+    if (big) {  // fused residual block: k3 conv + ELU + k1 conv + skip + ELU, the hidden rows in LDS
+      const ResBlockArgs rb{ce_[i], hist_[2 + 2 * i], cb_[i], W(L_.dra_w[i]), W(L_.dra_b[i]), W(L_.drb_w[i]),
+                            W(L_.drb_b[i]), ca_[i], B, T, ch};
+      const double hd = ch / 2;
+      ops.push_back({p + ".resblock", [rb](hipStream_t s) { resblock(rb, s); },
+                     2.0 * B * T * (hd * 3 * ch + ch * hd),
+                     4.0 * ((double)B * T * ch * 3 + B * 2.0 * ch + hd * 3 * ch + ch * hd + hd + ch)});
+    } else {  // few rows: the two convs on 32x32 tiles (more workgroups than the fused tiles)
+      conv_op(ops, p + ".res_conv3", ce_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 0, W(L_.dra_w[i]), ch / 2, 3, 1,
+              W(L_.dra_b[i]), nullptr, cv_[i], T, 1, 0, 1);
       conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 0, W(L_.drb_w[i]), ch, 1, 1,
-              W(L_.drb_b[i]), cb_[i], ca_[i], T, 1, l_r1, 1);
+              W(L_.drb_b[i]), cb_[i], ca_[i], T, 1, 0, 1);
     }
     cin_buf = ca_[i];
   }

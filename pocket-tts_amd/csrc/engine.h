@@ -84,8 +84,6 @@ class Engine {
                int P, int stride, int elu, const float* Wt, int cout, int ktaps, int phases, const float* bias,
                const float* R, float* Y, int T_out, int tstride, int layout = 0, int elu_out = 0,
                float* Y2 = nullptr, int ksplit = 1);
-  void blas_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N, int K,
-               float* Y);
   void dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N, int K,
                 const float* bias, int act, const float* rscale, const float* R, float* Y,
                 int layout = 0);
@@ -112,7 +110,6 @@ class Engine {
   // rocBLAS handle for the plain fp32 GEMMs of the text / voice prefill passes (M >= 256 rows,
   // eager, never captured): the library's tiles run at 117-149 TF/s on those shapes, twice the
   // hand-written 64x64 tile; the step's GEMMs stay hand-written (PTTS_BLAS=0 disables it)
-  void* blas_ = nullptr;
   bool own_blob_ = true, ready_ = false;
   hipStream_t stream_ = nullptr;
   Layout L_{};
@@ -145,10 +142,9 @@ class Engine {
   bool head_uniform_stride() const;  // ResBlock tensors at one stride (k_flow_head, its packing)
   bool use_head_chain(int B) const;
   float* fhw_ = nullptr;  // the chain's matrices in fragment order (pack_flow_head, at finalize)
-  float* hx_ = nullptr;
-  float* fhm_ = nullptr;
+  float* hx_ = nullptr;   // flow-head hand-off regions [lsd * 13][roundup(B, 16)][512] (k_flow_head)
+  float* fhm_ = nullptr;  // adaLN shift / scale in k_flow_head's fragment order (FlowHeadArgs::fhm)
   float* fh_inw_t_ = nullptr;  // flow-head input projection transposed [32][512] (x0 side job)
-  float* mcol_ = nullptr;  // explicit conv operands for rocBLAS convs (PTTS_BACK_BLAS 64 / 128)  // adaLN shift / scale in k_flow_head's fragment order (FlowHeadArgs::fhm)  // flow-head hand-off regions [lsd * 13][roundup(B, 16)][512] (k_flow_head)
   size_t hx_floats(int B) const { return (size_t)lsd_ * 13 * ((B + 15) / 16 * 16) * FD; }
   float* inw_t_ = nullptr;  // input_linear weight transposed, [32][1024] (k_input_ln)
   int *hctr_ = nullptr, *herr_ = nullptr;

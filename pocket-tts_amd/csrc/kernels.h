@@ -343,6 +343,17 @@ void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols
 void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, const float* w, const float* bias,
                 float* Y, int elu_in, hipStream_t s);
 
+// Fused SEANet residual block of one decoder stage (seanet.rs:43-89, kernels [3, 1], true skip):
+// Y = elu(R + b1 + conv_k1(elu(b3 + conv_k3(E)))) over [B][T][C] channels-last rows, E's two rows
+// before the frame from HE [B][2][C]. W3 [H][3][C] ([Cout][k][Cin]), W1 [C][H]. The intermediate
+// stays in LDS. Stages: (C, H, T) = (256, 128, 96), (128, 64, 480), (64, 32, 1920).
+struct ResBlockArgs {
+  const float *E, *HE, *R, *W3, *b3, *W1, *b1;
+  float* Y;
+  int B, T, C;
+};
+void resblock(const ResBlockArgs& a, hipStream_t s);
+
 // Encoder first conv (Cin == 1): Y[b][t][co] = bias[co] + sum_j w[co][j] * xpad[t + j], with
 // the 6-sample zero history (constant padding, conv.py:90-108).
 void conv_cin1(const float* X, int T, int cout, int k, const float* w, const float* bias, float* Y,

@@ -10,6 +10,7 @@
 #include "kernels.h"
 
 #include <cmath>
+#include <stdexcept>
 
 namespace ptts {
 
@@ -647,23 +648,25 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
     }
   }
   const long ldx = a.ldx, hld = a.cin;
-  // DMA instruction `ins` of this wave for chunk c into LDS buffer buf
-  auto issue_one = [&](int c, int buf, int ins) {
-    if (PTTS_PROBE(a) & 2) return;
+  // source of this lane's 16 bytes for DMA instruction `ins` of this wave and chunk c
+  auto dma_src = [&](int c, int ins) -> const float* {
     const int j = wave + 4 * ins;
-    if (j >= NINS) return;  // wave-uniform
     const int k0 = c * BK;
-    const float* src;
     if (MODE != 0 && j * RPI < TM) {
       const int tap = k0 / a.cin;  // scalar
       const int ci = k0 - tap * a.cin;
       const int t = src_qs[ins] + tap;
       const float* px = src_base[ins] + t * ldx + ci;
       const float* ph = src_hist[ins] + t * hld + ci;
-      src = t >= 0 ? px : ph;
-    } else {
-      src = src_base[ins] + k0;
+      return t >= 0 ? px : ph;
     }
+    return src_base[ins] + k0;
+  };
+  // DMA instruction `ins` of this wave from src into LDS buffer buf
+  auto dma = [&](const float* src, int buf, int ins) {
+    if (PTTS_PROBE(a) & 2) return;
+    const int j = wave + 4 * ins;
+    if (j >= NINS) return;  // wave-uniform
     // wave-uniform LDS base of this instruction; lane l -> + 16*l bytes
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)((buf * ROWS * BK + j * RPI * BK) * 4));
     if (a.w_nt && j * RPI >= TM) glds16_nt(src, dst);  // wave-uniform: a W row instruction
@@ -671,7 +674,7 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
   };
   auto issue = [&](int c, int buf) {
 #pragma unroll
-    for (int ins = 0; ins < IPW; ++ins) issue_one(c, buf, ins);
+    for (int ins = 0; ins < IPW; ++ins) dma(dma_src(c, ins), buf, ins);
   };
   static_assert(!ILV || (BK == 32 && IPW <= 16), "interleaved DMA issue: BK 32, at most one DMA per k-step");
   constexpr bool elu = MODE == 2;  // compile-time: an if-converted ELU costs ~250 VALU per chunk
@@ -698,6 +701,18 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
     const bool pf = c + DIST < ce;
     const int pc = c + DIST, pbuf = (c + DIST - cb) % NBUF;
     if (!ILV && pf) issue(pc, pbuf);
+    // ILV: the next chunk's DMA sources are formed here, ahead of this chunk's fragment reads, and
+    // pinned (an empty asm that rewrites them), so no address arithmetic lands between the MFMAs:
+    // with it there, the compiler reused the registers of queued MFMAs' operands for the address
+    // (v_lshl_add_u64 right behind the MFMA that reads it) and tiles came out wrong
+    const float* nsrc[IPW];
+    if (ILV) {
+#pragma unroll
+      for (int ins = 0; ins < IPW; ++ins) {
+        nsrc[ins] = dma_src(pf ? pc : c, ins);
+        asm volatile("" : "+v"(nsrc[ins]));
+      }
+    }
     {
       const int buf = (c - cb) % NBUF;
 #pragma unroll
@@ -737,7 +752,7 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
 #pragma unroll
               for (int jj = 0; jj < TNW; ++jj)
                 acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[ii][j], bf[jj][j], acc[ii][jj], 0, 0, 0);
-            if (ILV && pf && ((j + 1) * IPW) / 16 != (j * IPW) / 16) issue_one(pc, pbuf, (j * IPW) / 16);
+            if (ILV && pf && ((j + 1) * IPW) / 16 != (j * IPW) / 16) dma(nsrc[(j * IPW) / 16], pbuf, (j * IPW) / 16);
           }
         } else if (ILV && pf) {
           issue(pc, pbuf);
@@ -2581,6 +2596,125 @@ void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols
 // rows for t < 0) are read with coalesced 256-B row loads, ELU'd once per element and transposed
 // through a padded LDS tile (row stride 65: conflict-free column reads); lane t then forms output
 // t as a plain k x cin dot product (weights broadcast from LDS).
+// =============================================================================================
+// Fused SEANet residual block of one decoder stage (seanet.rs:43-89; SEANetResnetBlock with one
+// residual layer, kernel sizes [3, 1], true skip): per (utterance, time tile of TT rows)
+//   v = elu(b3 + conv_k3(E))          E = elu(convtr output), the stage's k3 conv input; its two
+//                                       rows before the frame come from the conv history HE
+//   Y = elu(R + b1 + conv_k1(v))       R = the raw convtr output (skip); Y = the next stage's
+//                                       (or the final conv's) ELU'd input
+// The intermediate v never leaves the CU: it goes from the first GEMM's accumulators to LDS and
+// is the second GEMM's A operand. Both GEMMs run on v_mfma_f32_32x32x2_f32 with A fragments read
+// from LDS (rows padded by 16 B: conflict-free ds_read_b128) and W fragments straight from global
+// memory (L2-resident; each lane one 64-B piece of a weight row), one K chunk ahead.
+// Shapes (B = 32): stage 0 C 256 / H 128 / T 96, stage 1 128 / 64 / 480, stage 2 64 / 32 / 1920.
+// =============================================================================================
+template <int C, int H, int TT>
+__global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
+  constexpr int LDE = C + 4, LDV = H + 4;
+  __shared__ __attribute__((aligned(16))) float sm[(TT + 2) * LDE + TT * LDV];
+  float* sE = sm;
+  float* sV = sm + (TT + 2) * LDE;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.y, t0 = blockIdx.x * TT;
+  // ---- E rows t0-2 .. t0+TT-1 (history rows for t < 0) into LDS
+  constexpr int C4 = C / 4;
+  for (int e = tid; e < (TT + 2) * C4; e += 256) {
+    const int row = e / C4, c4 = e - row * C4;
+    const int t = t0 - 2 + row;
+    const float* src = t >= 0 ? a.E + ((long)b * a.T + t) * C : a.HE + ((long)b * 2 + (t + 2)) * C;
+    *reinterpret_cast<float4*>(sE + row * LDE + 4 * c4) = *reinterpret_cast<const float4*>(src + 4 * c4);
+  }
+  __syncthreads();
+  // ---- GEMM 1: v[TT][H] = E3[TT][3C] . W3[H][3C]^T, k = tap * C + c reads sE[i + tap][c]
+  constexpr int MB = TT / 32, NB1 = H / 32, K1 = 3 * C / 32;
+  for (int blk = wave; blk < MB * NB1; blk += 4) {
+    const int mi = blk / NB1, ni = blk - mi * NB1;
+    const float* wrow = a.W3 + (long)(32 * ni + r) * (3 * C) + 16 * h;
+    floatx16 acc;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+    float4 wb[4], wn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wb[q] = *reinterpret_cast<const float4*>(wrow + 4 * q);
+    for (int kc = 0; kc < K1; ++kc) {
+      const int kn = kc + 1 < K1 ? kc + 1 : kc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wn[q] = *reinterpret_cast<const float4*>(wrow + 32 * kn + 4 * q);
+      const int k0 = 32 * kc + 16 * h, tap = k0 / C, c = k0 - tap * C;
+      const float* ap = sE + (32 * mi + r + tap) * LDE + c;
+      float af[16], bf[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(ap + 4 * q);
+        af[4 * q] = x.x; af[4 * q + 1] = x.y; af[4 * q + 2] = x.z; af[4 * q + 3] = x.w;
+        bf[4 * q] = wb[q].x; bf[4 * q + 1] = wb[q].y; bf[4 * q + 2] = wb[q].z; bf[4 * q + 3] = wb[q].w;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wb[q] = wn[q];
+    }
+    const int col = 32 * ni + r;
+    const float bias = a.b3[col];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int row = 32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h;
+      sV[row * LDV + col] = elu1(acc[g] + bias);
+    }
+  }
+  __syncthreads();
+  // ---- GEMM 2: Y[TT][C] = elu(R + b1 + v . W1[C][H]^T)
+  constexpr int NB2 = C / 32, K2 = H / 32;
+  for (int blk = wave; blk < MB * NB2; blk += 4) {
+    const int mi = blk / NB2, ni = blk - mi * NB2;
+    const float* wrow = a.W1 + (long)(32 * ni + r) * H + 16 * h;
+    floatx16 acc;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < K2; ++kc) {
+      const float* ap = sV + (32 * mi + r) * LDV + 32 * kc + 16 * h;
+      float af[16], bf[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(ap + 4 * q);
+        const float4 y = *reinterpret_cast<const float4*>(wrow + 32 * kc + 4 * q);
+        af[4 * q] = x.x; af[4 * q + 1] = x.y; af[4 * q + 2] = x.z; af[4 * q + 3] = x.w;
+        bf[4 * q] = y.x; bf[4 * q + 1] = y.y; bf[4 * q + 2] = y.z; bf[4 * q + 3] = y.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
+    }
+    const int col = 32 * ni + r;
+    const float bias = a.b1[col];
+    const long base = ((long)b * a.T + t0) * C + col;
+    float rv[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) rv[g] = a.R[base + (long)(32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h) * C];
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+      a.Y[base + (long)(32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h) * C] = elu1(acc[g] + bias + rv[g]);
+  }
+}
+
+void resblock(const ResBlockArgs& a, hipStream_t s) {
+  // time tiles: stage 0 32 rows (96 workgroups), stage 1 96 (160), stage 2 128 (480) at B = 32
+  if (a.C == 256 && a.T % 32 == 0)
+    hipLaunchKernelGGL((k_resblock<256, 128, 32>), dim3(a.T / 32, a.B), dim3(256),
+                       cap_lds(k_resblock<256, 128, 32>, g_wg_cap), s, a);
+  else if (a.C == 128 && a.T % 96 == 0)
+    hipLaunchKernelGGL((k_resblock<128, 64, 96>), dim3(a.T / 96, a.B), dim3(256),
+                       cap_lds(k_resblock<128, 64, 96>, g_wg_cap), s, a);
+  else if (a.C == 64 && a.T % 128 == 0)
+    hipLaunchKernelGGL((k_resblock<64, 32, 128>), dim3(a.T / 128, a.B), dim3(256),
+                       cap_lds(k_resblock<64, 32, 128>, g_wg_cap), s, a);
+  else
+    throw std::runtime_error("resblock: unsupported stage shape");
+}
+
 template <int KT>
 __global__ __launch_bounds__(256) void k_conv_cout1(const float* X, const float* H, int B, int T, int cin,
                                                     const float* w, const float* bias, float* Y, int elu_in) {

@@ -7,9 +7,15 @@ The launcher never touches the GPU. It starts (1) the server, `python -m pocket_
 client processes, so the load generator does not share the server's interpreter. Each client
 thread POSTs /stream (chunked 16-bit PCM) with 40 token ids and eos_threshold = +1e9 (no EOS:
 each request runs its max_gen_len = 22 * 13 = 286 frames, the tts_model.rs:968-969 rule for the 20
-words stated with the ids). Reports whole-job audio-sec/wall-sec through HTTP and the p50 / p90 time to first chunk.
+words stated with the ids), CLOSED LOOP: each of the 32 streams issues its next request as soon as
+the previous one ends, for --seconds per round, so a round is a steady state of continuous
+batching (slots recycled as requests finish and new ones are admitted in small groups) rather than
+one synchronized burst. Reports per round the audio-sec/wall-sec through HTTP (audio of the
+requests that completed inside the round / round wall time) and the p50 / p90 time to first chunk
+(burst: the first request of each stream, all released together; steady: every later request),
+and the median over rounds.
 
-  python tools/serve_load.py [--clients 32] [--procs 4] [--rounds 2] [--port 8765] [--out f.json]"""
+  python tools/serve_load.py [--clients 32] [--procs 4] [--rounds 3] [--seconds 6] [--port 8765] [--out f.json]"""
 
 import argparse
 import json
@@ -29,9 +35,10 @@ def ids(i):
     return [(k * 97 + 13 + 7 * i) % 4000 for k in range(40)]
 
 
-def client(port, first, n, t_go):
+def client(port, first, n, t_go, seconds):
     """n streams (ids first..first+n-1) in threads, all released at wall time t_go (shared by
-    every client process); prints one JSON line per stream."""
+    every client process), each issuing requests back to back until t_go + seconds; prints one
+    JSON line: per stream, the list of its requests."""
     import httpx
 
     base = f"http://127.0.0.1:{port}"
@@ -46,15 +53,19 @@ def client(port, first, n, t_go):
     def one(j):
         go.wait()
         time.sleep(max(0.0, t_go - time.time()))
-        t0 = time.time()
-        t_first, nbytes = None, 0
-        with clients[j].stream("POST", base + "/stream", json={"token_ids": ids(first + j), "words": 20, "eos_threshold": 1e9}) as r:
-            r.raise_for_status()
-            for chunk in r.iter_bytes():
-                if t_first is None and chunk:
-                    t_first = time.time()
-                nbytes += len(chunk)
-        out[j] = {"start": t0, "first": t_first, "end": time.time(), "samples": nbytes // 2}
+        reqs = []
+        while time.time() < t_go + seconds:
+            t0 = time.time()
+            t_first, nbytes = None, 0
+            body = {"token_ids": ids(first + j + 97 * len(reqs)), "words": 20, "eos_threshold": 1e9}
+            with clients[j].stream("POST", base + "/stream", json=body) as r:
+                r.raise_for_status()
+                for chunk in r.iter_bytes():
+                    if t_first is None and chunk:
+                        t_first = time.time()
+                    nbytes += len(chunk)
+            reqs.append({"start": t0, "first": t_first, "end": time.time(), "samples": nbytes // 2})
+        out[j] = reqs
 
     ts = [threading.Thread(target=one, args=(j,)) for j in range(n)]
     for t in ts:
@@ -68,7 +79,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clients", type=int, default=32)
     ap.add_argument("--procs", type=int, default=4)
-    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--seconds", type=float, default=6.0, help="closed-loop duration of one round")
     ap.add_argument("--port", type=int, default=8765)
     ap.add_argument("--out", default="")
     ap.add_argument("--workdir", default=os.path.join(HERE, "..", "gpurun_out"))
@@ -94,14 +106,15 @@ def main():
                     break
             except httpx.HTTPError:
                 time.sleep(0.1)
-        result = {"clients": args.clients, "procs": args.procs, "route": "/stream", "rounds": []}
+        result = {"clients": args.clients, "procs": args.procs, "route": "/stream", "seconds_per_round": args.seconds,
+                  "rounds": []}
         per = [args.clients // args.procs + (1 if p < args.clients % args.procs else 0) for p in range(args.procs)]
         for rnd in range(args.rounds):
             procs, first = [], 0
             t_go = time.time() + 3.0  # client processes start, import httpx and connect first
             for n in per:
                 procs.append(subprocess.Popen([sys.executable, __file__, "client", str(args.port), str(first), str(n),
-                                               repr(t_go)], stdout=subprocess.PIPE, text=True))
+                                               repr(t_go), repr(args.seconds)], stdout=subprocess.PIPE, text=True))
                 first += n
             streams = []
             for p in procs:
@@ -109,17 +122,24 @@ def main():
                 if p.returncode != 0:
                     raise SystemExit(f"client failed ({p.returncode})")
                 streams += json.loads(o.strip().splitlines()[-1])
-            t0 = min(s["start"] for s in streams)
-            wall = max(s["end"] for s in streams) - t0
-            samples = sum(s["samples"] for s in streams)
-            ttfc = sorted(s["first"] - s["start"] for s in streams)
-            rec = {"round": rnd, "wall_s": round(wall, 3), "audio_s": round(samples / 24000.0, 2),
+            reqs = [q for st in streams for q in st]
+            t0 = min(q["start"] for q in reqs)
+            wall = max(q["end"] for q in reqs) - t0
+            samples = sum(q["samples"] for q in reqs)
+            burst = sorted(st[0]["first"] - st[0]["start"] for st in streams)
+            steady = sorted(q["first"] - q["start"] for st in streams for q in st[1:])
+            pct = lambda v, f: round(1e3 * v[min(len(v) - 1, int(f * (len(v) - 1)))], 2) if v else None
+            rec = {"round": rnd, "wall_s": round(wall, 3), "requests": len(reqs), "audio_s": round(samples / 24000.0, 2),
                    "audio_sec_per_wall_sec": round(samples / 24000.0 / wall, 2),
-                   "frames_per_request": streams[0]["samples"] // 1920,
-                   "ttfc_p50_ms": round(1e3 * ttfc[len(ttfc) // 2], 2),
-                   "ttfc_p90_ms": round(1e3 * ttfc[int(0.9 * (len(ttfc) - 1))], 2)}
+                   "frames_per_request": reqs[0]["samples"] // 1920,
+                   "ttfc_burst_p50_ms": pct(burst, 0.5), "ttfc_burst_p90_ms": pct(burst, 0.9),
+                   "ttfc_steady_p50_ms": pct(steady, 0.5), "ttfc_steady_p90_ms": pct(steady, 0.9)}
             result["rounds"].append(rec)
             print(json.dumps(rec), flush=True)
+        med = lambda k: float(np.median([r[k] for r in result["rounds"] if r[k] is not None]))
+        result["median"] = {k: round(med(k), 2) for k in ("audio_sec_per_wall_sec", "ttfc_burst_p50_ms",
+                                                          "ttfc_steady_p50_ms", "ttfc_steady_p90_ms")}
+        print(json.dumps({"median": result["median"]}), flush=True)
         r = httpx.post(base + "/v1/audio/speech", json={"token_ids": ids(0), "words": 20, "response_format": "wav"}, timeout=120)
         r.raise_for_status()
         result["openai_wav_bytes"] = len(r.content)
@@ -135,6 +155,6 @@ def main():
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "client":
-        client(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5]))
+        client(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5]), float(sys.argv[6]))
     else:
         main()
