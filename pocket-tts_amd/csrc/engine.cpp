@@ -915,14 +915,19 @@ static BackTile back_tile(const std::string& op, bool pipeline) {
     const char* op;
     BackTile seq, pipe;
   } table[] = {
-      {"mimi.qkv", {33, 1}, {33, 1}},
-      {"mimi.out", {33, 4}, {33, 4}},
-      {"mimi.ff1", {33, 1}, {33, 1}},
-      {"mimi.ff2", {33, 4}, {33, 4}},
-      {"seanet.conv0", {33, 4}, {33, 4}},
-      {"seanet.up0.convtr", {33, 4}, {33, 4}},
-      {"seanet.up1.convtr", {33, 1}, {33, 1}},
-      {"seanet.up2.convtr", {33, 1}, {33, 1}},
+      {"mimi.qkv", {32, 1}, {32, 1}},
+      {"mimi.out", {32, 4}, {32, 4}},
+      {"mimi.ff1", {32, 1}, {32, 1}},
+      {"mimi.ff2", {32, 4}, {32, 4}},
+      {"seanet.conv0", {32, 4}, {32, 4}},
+      {"seanet.up0.convtr", {32, 4}, {32, 4}},
+      {"seanet.up1.convtr", {32, 1}, {32, 1}},
+      {"seanet.up2.convtr", {32, 1}, {32, 1}},
+      // the stage-0/1 residual convs when not fused (see resblock_fused)
+      {"seanet.up0.res_conv3", {18, 1}, {18, 1}},
+      {"seanet.up1.res_conv3", {20, 1}, {20, 1}},
+      {"seanet.up0.res_conv1", {6, 1}, {6, 1}},
+      {"seanet.up1.res_conv1", {6, 1}, {6, 1}},
   };
   for (const auto& t : table)
     if (op == t.op) return pipeline ? t.pipe : t.seq;
@@ -1094,18 +1099,25 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     }
     T *= r;
     ch /= 2;
-    if (big) {  // fused residual block: k3 conv + ELU + k1 conv + skip + ELU, the hidden rows in LDS
+    // fused residual block (k3 conv + ELU + k1 conv + skip + ELU, the hidden rows in LDS) where it
+    // beats the two conv launches: stage 2 (480 workgroups; 22.5 us against 16.8 + 11.0). Stages
+    // 0 and 1 have 96 / 160 workgroups of it and measured slower than their two tuned launches.
+    // PTTS_RESBLOCK_STAGES (probe builds): bit mask of the stages that fuse.
+    int fused_stages = 4;
+    if (probe_env("PTTS_RESBLOCK_STAGES")) fused_stages = atoi(probe_env("PTTS_RESBLOCK_STAGES"));
+    if (big && (fused_stages >> i & 1)) {
       const ResBlockArgs rb{ce_[i], hist_[2 + 2 * i], cb_[i], W(L_.dra_w[i]), W(L_.dra_b[i]), W(L_.drb_w[i]),
                             W(L_.drb_b[i]), ca_[i], B, T, ch};
       const double hd = ch / 2;
       ops.push_back({p + ".resblock", [rb](hipStream_t s) { resblock(rb, s); },
                      2.0 * B * T * (hd * 3 * ch + ch * hd),
                      4.0 * ((double)B * T * ch * 3 + B * 2.0 * ch + hd * 3 * ch + ch * hd + hd + ch)});
-    } else {  // few rows: the two convs on 32x32 tiles (more workgroups than the fused tiles)
+    } else {  // the two convs (few rows: 32x32 tiles, more workgroups than the fused tiles)
+      const int lr3 = big ? tile(p + ".res_conv3", 1).layout : 0, lr1 = big ? tile(p + ".res_conv1", 1).layout : 0;
       conv_op(ops, p + ".res_conv3", ce_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 0, W(L_.dra_w[i]), ch / 2, 3, 1,
-              W(L_.dra_b[i]), nullptr, cv_[i], T, 1, 0, 1);
+              W(L_.dra_b[i]), nullptr, cv_[i], T, 1, lr3, 1);
       conv_op(ops, p + ".res_conv1", cv_[i], B, T, ch / 2, nullptr, 0, 1, 0, W(L_.drb_w[i]), ch, 1, 1,
-              W(L_.drb_b[i]), cb_[i], ca_[i], T, 1, 0, 1);
+              W(L_.drb_b[i]), cb_[i], ca_[i], T, 1, lr1, 1);
     }
     cin_buf = ca_[i];
   }

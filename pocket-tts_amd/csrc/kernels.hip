@@ -1952,6 +1952,22 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
   const float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
   const int cmask = kv.cap - 1;
   auto kidx = [&](int kp) { return RING ? (kp & cmask) : kp; };
+  const int ntiles = (kmax - kmin + 16) / 16;
+  float4 kf[4], vf[4];
+  auto load = [&](int t) {
+    const int kt = kmin + 16 * t;
+    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)kidx(min(kt + c, kmax)) * 64 + 16 * G);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kf[i] = kr[i];
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx)
+      vf[sidx] = *reinterpret_cast<const float4*>(vbase + (long)kidx(min(kt + 4 * G + sidx, kmax)) * 64 + 4 * c);
+  };
+  // a wave whose first key tile holds only keys older than this step's appended rows issues its
+  // loads now, so their latency overlaps the append below (the append never evicts a key of the
+  // window: the ring holds window + 16 positions)
+  const bool early = FUSE && wave < ntiles && kmin + 16 * wave + 15 < qpos0;
+  if (early) load(wave);
   // Q^T fragment: query c (rows past nrows reuse the last row; never stored), dims 16G..16G+15
   float qf[16];
   if (FUSE) {
@@ -1996,18 +2012,7 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
   floatx4 o[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int ntiles = (kmax - kmin + 16) / 16;
-  float4 kf[4], vf[4];
-  auto load = [&](int t) {
-    const int kt = kmin + 16 * t;
-    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)kidx(min(kt + c, kmax)) * 64 + 16 * G);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) kf[i] = kr[i];
-#pragma unroll
-    for (int sidx = 0; sidx < 4; ++sidx)
-      vf[sidx] = *reinterpret_cast<const float4*>(vbase + (long)kidx(min(kt + 4 * G + sidx, kmax)) * 64 + 4 * c);
-  };
-  if (wave < ntiles) load(wave);
+  if (wave < ntiles && !early) load(wave);
   for (int t = wave; t < ntiles; t += A16_WAVES) {
     const int kt = kmin + 16 * t;
     float ka[16];
@@ -2636,13 +2641,15 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
     floatx16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
-    float4 wb[4], wn[4];
+    // W fragments three chunks ahead (an L2 / MALL round trip is several chunks of MFMAs): a ring
+    // of three register sets with fixed roles per unrolled step
+    float4 w0[4], w1[4], w2[4];
+    auto wload = [&](int kc, float4 (&w)[4]) {
+      const int k = kc < K1 ? kc : K1 - 1;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) wb[q] = *reinterpret_cast<const float4*>(wrow + 4 * q);
-    for (int kc = 0; kc < K1; ++kc) {
-      const int kn = kc + 1 < K1 ? kc + 1 : kc;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) wn[q] = *reinterpret_cast<const float4*>(wrow + 32 * kn + 4 * q);
+      for (int q = 0; q < 4; ++q) w[q] = *reinterpret_cast<const float4*>(wrow + 32 * k + 4 * q);
+    };
+    auto step = [&](int kc, const float4 (&w)[4]) {
       const int k0 = 32 * kc + 16 * h, tap = k0 / C, c = k0 - tap * C;
       const float* ap = sE + (32 * mi + r + tap) * LDE + c;
       float af[16], bf[16];
@@ -2650,12 +2657,21 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
       for (int q = 0; q < 4; ++q) {
         const float4 x = *reinterpret_cast<const float4*>(ap + 4 * q);
         af[4 * q] = x.x; af[4 * q + 1] = x.y; af[4 * q + 2] = x.z; af[4 * q + 3] = x.w;
-        bf[4 * q] = wb[q].x; bf[4 * q + 1] = wb[q].y; bf[4 * q + 2] = wb[q].z; bf[4 * q + 3] = wb[q].w;
+        bf[4 * q] = w[q].x; bf[4 * q + 1] = w[q].y; bf[4 * q + 2] = w[q].z; bf[4 * q + 3] = w[q].w;
       }
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) wb[q] = wn[q];
+    };
+    static_assert(K1 % 3 == 0, "K1 = 3C/32 chunks: a multiple of 3 (the ring)");
+    wload(0, w0);
+    wload(1, w1);
+    for (int kc = 0; kc < K1; kc += 3) {
+      wload(kc + 2, w2);
+      step(kc, w0);
+      wload(kc + 3, w0);
+      step(kc + 1, w1);
+      wload(kc + 4, w1);
+      step(kc + 2, w2);
     }
     const int col = 32 * ni + r;
     const float bias = a.b3[col];
