@@ -142,6 +142,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
   // split-K slabs: skinny FlowLM/head GEMMs, and the 2-way split Mimi QKV (B*16 rows x 1536)
   pcap_ = std::max({(size_t)4 << 20, (size_t)2 * B * UP * 3 * MD, (size_t)PREFILL * FF});
   partial_ = dalloc(pcap_);
+  tslab_ = dalloc(TAIL_CAP);
+  tickets_ = (int*)dalloc(TICKETS);  // zero; every split-tail launch leaves them zero
   ids_dev_ = (int*)dalloc(PREFILL);
   rowtab_dev_ = (int*)dalloc(PREFILL);
   admit_slots_ = (int*)dalloc(B);
@@ -430,16 +432,19 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
                           const float* Wt, int N, int K, int* S_out) {
   PTTS_REQUIRE(K % 32 == 0, "GEMM K must be a multiple of 32");
   int S = pick_splits(M, N, K);
-  int layout = 0;
+  int layout = 0, tail = 0;
   // wide skinny GEMMs (FlowLM qkv/ff1, flow-head adaLN): 32x128 LDS-DMA tiles, 8-way split-K
   // (tools/gemm_bench.hip on MI355X: qkv 6.7 -> 6.3 us, ff1 7.9 -> 6.5 us, ada 10.1 -> 8.7 us)
   if (M <= 64 && N >= 3072) {
     layout = 7;  // 2-buffer LDS (40 KB) co-resides with the back part
     S = std::max(1, std::min(8, K / 64));
   } else if (M >= 256) {  // prefill passes (text admission, M = 48 rows per slot): MFMA-bound,
-    // 128x64 / 64x128 LDS-DMA tiles with the DMAs interleaved between the MFMAs, two workgroups
-    // per CU, no split (tools/mm_bench.hip at M = 1536: qkv 89, out 73, ff1 108, ff2 79 TF/s)
-    layout = N >= 3072 ? 35 : 39;
+    // LDS-DMA tiles with the DMAs interleaved between the MFMAs and a split tail (the tiles past
+    // whole rounds of the CUs' workgroup slots run as K slices; tools/mm_bench.hip at M = 1536,
+    // against rocBLAS fp32 on the same box: qkv 108 / 111, out 88 / 98, ff1 112 / 125, ff2 117 /
+    // 122 TF/s): 128x64, two per CU, 4 slices; linear1 128x64 one per CU, 2 slices
+    layout = N >= 4096 && K <= 1024 ? 34 : 35;
+    tail = N >= 4096 && K <= 1024 ? 2 : 4;
     S = 1;
   } else if (M <= 64 && K >= 4096) {  // FlowLM ff2: 8 slabs (tools/gemm_bench.hip flow.ff2: 8.5 -> 7.3 us)
     S = 8;
@@ -505,6 +510,13 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   a.W = Wt;
   a.S = S;
   a.partial = partial_;
+  if (tail > 0 && S == 1 && !w8 && !wf8) {
+    a.tail_S = tail;
+    a.tail_slab = tslab_;
+    a.tail_cap = (long)TAIL_CAP;
+    a.tickets = tickets_;
+    a.tickets_cap = TICKETS;
+  }
   // FlowLM / flow-head step weights are read once per step: non-temporal loads on the LDS-DMA
   // tiles (step -1.1 %; the 32x32 register tile keeps default-policy loads)
   a.w_nt = M <= 64 && layout != 0;
@@ -928,6 +940,8 @@ static BackTile back_tile(const std::string& op, bool pipeline) {
       {"seanet.up1.res_conv3", {20, 1}, {20, 1}},
       {"seanet.up0.res_conv1", {6, 1}, {6, 1}},
       {"seanet.up1.res_conv1", {6, 1}, {6, 1}},
+      {"seanet.up2.res_conv3", {14, 1}, {14, 1}},
+      {"seanet.up2.res_conv1", {6, 1}, {23, 1}},
   };
   for (const auto& t : table)
     if (op == t.op) return pipeline ? t.pipe : t.seq;

@@ -132,6 +132,11 @@ class Engine {
   static constexpr int PREFILL = 2048;  // rows per prefill pass (batched admission: all slots' text)
   size_t pcap_ = 0;
   float *x_ = nullptr, *h_ = nullptr, *q_ = nullptr, *o_ = nullptr, *u_ = nullptr, *partial_ = nullptr;
+  // split-tail scratch of the prefill GEMMs (GemmArgs::tail_S; one stream at a time uses it)
+  static constexpr size_t TAIL_CAP = (size_t)16 << 20;
+  static constexpr int TICKETS = 1024;
+  float* tslab_ = nullptr;
+  int* tickets_ = nullptr;
   int* ids_dev_ = nullptr;
   int* rowtab_dev_ = nullptr;   // [PREFILL] slot << 16 | pos, -1 = padding row
   int* admit_slots_ = nullptr;  // [max_slots] staged admission list

@@ -98,6 +98,17 @@ struct GemmArgs {
   // split-K
   int S;
   float* partial;  // [S][M][N] when S > 1
+  // split tail (dense, LDS-DMA ILV tiles, S == 1): the tiles that fill whole rounds of the CUs'
+  // workgroup slots run over all of K; the remainder (fewer tiles than slots) is cut into tail_S
+  // K slices, one workgroup each, whose partial tiles go to tail_slab [rem][tail_S][TM*TN]; the
+  // last slice to finish (tickets[rem], zero between launches) sums them in slice order and
+  // applies the epilogue. gemm() derives the split of the grid; capacities are checked.
+  int tail_S;
+  float* tail_slab;
+  long tail_cap;  // floats in tail_slab
+  int* tickets;
+  int tickets_cap;
+  int tail_full, tiles_n;  // set by gemm()
   // epilogue (S == 1)
   const float* bias;
   int act;

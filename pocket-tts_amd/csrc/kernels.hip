@@ -577,6 +577,20 @@ __device__ __forceinline__ void glds16_nt(const float* gsrc, unsigned lds_byte) 
       : "v"(gsrc), "s"(lds_byte)
       : "memory");
 }
+// write-through (sc1) 16-byte store and L2-bypassing load: partial tiles handed between
+// workgroups on different XCDs (each XCD has its own L2)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+typedef unsigned int sc1_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void sc1_st(__amdgpu_buffer_rsrc_t r, int byte_off, float4 f) {
+  const sc1_u32x4 v = {__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
+}
+__device__ __forceinline__ float4 sc1_ld(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  const sc1_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
 __device__ __forceinline__ unsigned lds_addr(const float* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) float*)(p);
 }
@@ -607,7 +621,23 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int r = lane & 31, h = lane >> 5;
   int bx, by;
-  xcd_tile(a, true, bx, by);
+  int tail_u = -1;  // split tail: this workgroup's (tile, slice) unit among the remainder tiles
+  if (ILV && MODE == 0 && a.tail_S > 0) {
+    // 1-D grid: whole tiles first (contiguous runs of them per XCD), then tail_S units per
+    // remainder tile
+    const int L = blockIdx.x, F = a.tail_full;
+    int t;
+    if (L < F) {
+      t = (F & 7) == 0 ? (L & 7) * (F >> 3) + (L >> 3) : L;
+    } else {
+      tail_u = L - F;
+      t = F + tail_u / a.tail_S;
+    }
+    bx = t % a.tiles_n;
+    by = t / a.tiles_n;
+  } else {
+    xcd_tile(a, true, bx, by);
+  }
   const int n0 = bx * TN, m0 = by * TM, z = blockIdx.z;
   const int nchunks = a.K / BK;
   int cb = 0, ce = nchunks, phase = 0;
@@ -616,6 +646,11 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
     ce = (int)((long)nchunks * (z + 1) / a.S);
   } else {
     phase = z;
+  }
+  if (tail_u >= 0) {
+    const int zt = tail_u % a.tail_S;
+    cb = (int)((long)nchunks * zt / a.tail_S);
+    ce = (int)((long)nchunks * (zt + 1) / a.tail_S);
   }
   const float* Wp = a.W + (long)phase * a.w_phase_stride;
   const unsigned lds_base = lds_addr(lds);
@@ -760,6 +795,78 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
       }
     }
   }
+  if (ILV && MODE == 0 && tail_u >= 0) {
+    // split tail: publish this slice's partial tile (register order, 1 KB per float4 row of the
+    // wave), count in; the last of the tile's tail_S slices sums them in slice order
+    const int ti = tail_u / a.tail_S, zt = tail_u % a.tail_S;
+    const auto rs = sc1_rsrc(a.tail_slab + (long)ti * a.tail_S * TM * TN);
+    auto off = [&](int zz, int ii, int jj, int q) {
+      return (((zz * 4 + wave) * TMW * TNW + ii * TNW + jj) * 4 + q) * 1024 + 16 * lane;
+    };
+#pragma unroll
+    for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < TNW; ++jj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          sc1_st(rs, off(zt, ii, jj, q),
+                 make_float4(acc[ii][jj][4 * q], acc[ii][jj][4 * q + 1], acc[ii][jj][4 * q + 2], acc[ii][jj][4 * q + 3]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int last;
+    if (tid == 0)
+      last = __hip_atomic_fetch_add(a.tickets + ti, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tail_S - 1;
+    __syncthreads();
+    if (!last) return;
+    if (tid == 0) __hip_atomic_store(a.tickets + ti, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the slab loads below the ticket
+    // slice order: t = P0 + P1 + ... ; one slice's 4 * TMW * TNW loads in flight at a time
+    float4 t[TMW][TNW][4];
+#pragma unroll
+    for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < TNW; ++jj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          t[ii][jj][q] = zt == 0 ? make_float4(acc[ii][jj][4 * q], acc[ii][jj][4 * q + 1], acc[ii][jj][4 * q + 2],
+                                               acc[ii][jj][4 * q + 3])
+                                 : sc1_ld(rs, off(0, ii, jj, q));
+#pragma unroll 1
+    for (int zz = 1; zz < a.tail_S; ++zz) {
+      float4 v[TMW][TNW][4];
+#pragma unroll
+      for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < TNW; ++jj)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[ii][jj][q] = zz == zt ? make_float4(acc[ii][jj][4 * q], acc[ii][jj][4 * q + 1], acc[ii][jj][4 * q + 2],
+                                                  acc[ii][jj][4 * q + 3])
+                                    : sc1_ld(rs, off(zz, ii, jj, q));
+#pragma unroll
+      for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < TNW; ++jj)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            t[ii][jj][q].x += v[ii][jj][q].x;
+            t[ii][jj][q].y += v[ii][jj][q].y;
+            t[ii][jj][q].z += v[ii][jj][q].z;
+            t[ii][jj][q].w += v[ii][jj][q].w;
+          }
+    }
+#pragma unroll
+    for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < TNW; ++jj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[ii][jj][4 * q] = t[ii][jj][q].x;
+          acc[ii][jj][4 * q + 1] = t[ii][jj][q].y;
+          acc[ii][jj][4 * q + 2] = t[ii][jj][q].z;
+          acc[ii][jj][4 * q + 3] = t[ii][jj][q].w;
+        }
+  }
   const bool ident = gemm_ident(a, MODE, phase);
 #pragma unroll
   for (int ii = 0; ii < TMW; ++ii)
@@ -768,19 +875,17 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
       const int tm0 = m0 + 32 * TMW * wm + 32 * ii, tn0 = n0 + 32 * TNW * wn + 32 * jj;
       if (ident && !a.partial && tm0 + 32 <= a.M && tn0 + 32 <= a.N) {
         gemm_store_tile(a, acc[ii][jj], tm0, tn0, h, r);
-        continue;
-      }
+      } else {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int row = tm0 + (g & 3) + 8 * (g >> 2) + 4 * h;
-        const int col = tn0 + r;
-        if (row >= a.M || col >= a.N) continue;
-        float v = acc[ii][jj][g];
-        if (a.partial) {
-          a.partial[((long)z * a.M + row) * a.N + col] = v;
-          continue;
+        for (int g = 0; g < 16; ++g) {
+          const int row = tm0 + (g & 3) + 8 * (g >> 2) + 4 * h;
+          const int col = tn0 + r;
+          if (row < a.M && col < a.N) {
+            const float v = acc[ii][jj][g];
+            if (a.partial) a.partial[((long)z * a.M + row) * a.N + col] = v;
+            else gemm_store(a, row, col, phase, ident, v);
+          }
         }
-        gemm_store(a, row, col, phase, ident, v);
       }
     }
 }
@@ -1246,6 +1351,35 @@ static void launch_tiled(K kernel, dim3 grid, int threads, hipStream_t s, const 
   hipLaunchKernelGGL(kernel, grid, dim3(threads), cap_lds(kernel, std::max(a.max_wg_per_cu, g_wg_cap)), s, b);
 }
 
+// Split tail (GemmArgs::tail_S): whole rounds of the CUs' workgroup slots (256 CUs x MINB) run
+// whole tiles; the remaining tiles are cut into tail_S K slices that run as the last round.
+static constexpr int NUM_CUS = 256;
+template <typename K>
+static void launch_split_tail(K kernel, int TM, int TN, int minb, hipStream_t s, const GemmArgs& a) {
+  GemmArgs b = a;
+  b.tiles_n = (a.N + TN - 1) / TN;
+  const int tiles_m = (a.M + TM - 1) / TM, tiles = b.tiles_n * tiles_m, slots = NUM_CUS * minb;
+  b.tail_full = tiles / slots * slots;
+  const int rem = tiles - b.tail_full;
+  if (rem == 0) {  // whole rounds: every workgroup takes a whole tile, the ordinary 2-D grid
+    b.tail_S = 0;
+    launch_tiled(kernel, dim3((unsigned)b.tiles_n, (unsigned)tiles_m, 1), 256, s, b);
+    return;
+  }
+  b.tail_S = std::min(b.tail_S, a.K / 32);
+  while (b.tail_S > 1 && (long)rem * b.tail_S * TM * TN > a.tail_cap) --b.tail_S;  // scratch-bound
+  if (b.tail_S <= 1) {
+    b.tail_S = 0;
+    launch_tiled(kernel, dim3((unsigned)b.tiles_n, (unsigned)tiles_m, 1), 256, s, b);
+    return;
+  }
+  if (rem > a.tickets_cap || !a.tail_slab || !a.tickets || a.S != 1)
+    throw std::runtime_error("gemm: split tail needs its slab and tickets and S == 1");
+  b.xcd_pn = 0;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)(b.tail_full + rem * b.tail_S)), dim3(256),
+                     cap_lds(kernel, a.max_wg_per_cu), s, b);
+}
+
 template <int MODE>
 static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
   switch (a.layout) {
@@ -1254,15 +1388,19 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     launch_tiled((k_gemm_glds<MODE, WM_, WN_, BK_, NB_>),                                              \
                  dim3((a.N + 32 * WN_ - 1) / (32 * WN_), (a.M + 32 * WM_ - 1) / (32 * WM_), grid_z), 256, s, a); \
     return;
+    // the product's layouts (engine.cpp: linear_split, back_tile); the rest are compiled only into
+    // -DPTTS_PROBES builds (tools/, PTTS_OVR sweeps)
     PTTS_GLDS(6, 2, 2, 32, 2)
     PTTS_GLDS(7, 1, 4, 32, 2)
+    PTTS_GLDS(14, 4, 1, 32, 4)
+#ifdef PTTS_PROBES
     PTTS_GLDS(8, 2, 2, 64, 2)
     PTTS_GLDS(11, 2, 2, 32, 3)
     PTTS_GLDS(12, 2, 2, 32, 4)
     PTTS_GLDS(13, 1, 4, 32, 4)
-    PTTS_GLDS(14, 4, 1, 32, 4)
     PTTS_GLDS(15, 2, 2, 64, 3)
     PTTS_GLDS(16, 1, 4, 64, 3)
+#endif
 #undef PTTS_GLDS
 #define PTTS_GLRB(L, WM_, WN_, NB_, TMW_, TNW_)                                                       \
   case L:                                                                                             \
@@ -1271,73 +1409,87 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
                       (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z), 256, s, a);            \
     return;
     // register-blocked LDS-DMA tiles (per-wave TMW x TNW accumulators)
+    PTTS_GLRB(23, 2, 2, 3, 2, 1)  // 128 x  64
+#ifdef PTTS_PROBES
     PTTS_GLRB(21, 2, 2, 3, 2, 2)  // 128 x 128
     PTTS_GLRB(22, 2, 2, 3, 1, 2)  //  64 x 128
-    PTTS_GLRB(23, 2, 2, 3, 2, 1)  // 128 x  64
     PTTS_GLRB(24, 4, 1, 3, 2, 1)  // 256 x  32
     PTTS_GLRB(25, 4, 1, 3, 1, 2)  // 128 x  64 (waves stacked in M)
     PTTS_GLRB(26, 2, 2, 4, 2, 2)  // 128 x 128, 4 buffers
     PTTS_GLRB(27, 1, 4, 3, 2, 1)  //  64 x 128 (waves side by side in N)
+#endif
 #undef PTTS_GLRB
 #define PTTS_GLX(L, WM_, WN_, NB_, TMW_, TNW_, MINB_)                                                 \
   case L:                                                                                             \
+    if (MODE == 0 && a.tail_S > 0) {                                                                  \
+      launch_split_tail((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_, MINB_, true>),               \
+                        32 * WM_ * TMW_, 32 * WN_ * TNW_, MINB_, s, a);                                \
+      return;                                                                                         \
+    }                                                                                                 \
     launch_tiled((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_, MINB_, true>),                      \
                  dim3((a.N + 32 * WN_ * TNW_ - 1) / (32 * WN_ * TNW_),                                \
                       (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z), 256, s, a);            \
     return;
-    // interleaved DMA issue (ILV), experiments
+    // interleaved DMA issue (ILV)
+    PTTS_GLX(32, 2, 2, 3, 1, 1, 2)  //  64 x  64, 2 per CU (back part)
+    PTTS_GLX(34, 2, 2, 3, 2, 1, 1)  // 128 x  64 (prefill linear1)
+    PTTS_GLX(35, 2, 2, 2, 2, 1, 2)  // 128 x  64, 2 per CU (prefill)
+#ifdef PTTS_PROBES
     PTTS_GLX(30, 2, 2, 3, 2, 2, 1)  // 128 x 128
     PTTS_GLX(31, 2, 2, 2, 2, 2, 2)  // 128 x 128, 2 per CU
-    PTTS_GLX(32, 2, 2, 3, 1, 1, 2)  //  64 x  64, 2 per CU
     PTTS_GLX(33, 2, 2, 2, 1, 1, 2)  //  64 x  64, 2 buffers, 2 per CU
-    PTTS_GLX(34, 2, 2, 3, 2, 1, 1)  // 128 x  64
-    PTTS_GLX(35, 2, 2, 2, 2, 1, 2)  // 128 x  64, 2 per CU
     PTTS_GLX(36, 2, 2, 3, 1, 2, 1)  //  64 x 128
     PTTS_GLX(37, 2, 2, 4, 1, 1, 1)  //  64 x  64, 4 buffers
     PTTS_GLX(38, 2, 2, 4, 2, 2, 1)  // 128 x 128, 4 buffers
     PTTS_GLX(39, 2, 2, 3, 1, 2, 2)  //  64 x 128, 2 per CU
+#endif
 #undef PTTS_GLX
     default:
       break;
   }
   switch (a.layout) {
+    case 0:
+      launch_tiled((k_gemm<MODE, 0>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 256, s, a);
+      return;
+    case 9:
+      launch_tiled((k_gemm<MODE, 9>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 512, s, a);
+      return;
+    case 18:
+      launch_tiled((k_gemm_rb<MODE, 1, 2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), 256, s, a);
+      return;
+    case 20:
+      launch_tiled((k_gemm_rb<MODE, 2, 2>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), 256, s, a);
+      return;
+#ifdef PTTS_PROBES
     case 4:
       hipLaunchKernelGGL((k_gemm_lds<MODE, 0>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), dim3(256), 0, s,
                          a);
-      break;
+      return;
     case 5:
       hipLaunchKernelGGL((k_gemm_lds<MODE, 1>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), dim3(256), 0, s,
                          a);
-      break;
+      return;
     case 1:
       launch_tiled((k_gemm<MODE, 1>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), 256, s, a);
-      break;
+      return;
     case 2:
       launch_tiled((k_gemm<MODE, 2>), dim3((a.N + 127) / 128, (a.M + 31) / 32, grid_z), 256, s, a);
-      break;
+      return;
     case 3:
       launch_tiled((k_gemm<MODE, 3>), dim3((a.N + 31) / 32, (a.M + 127) / 128, grid_z), 256, s, a);
-      break;
-    case 9:
-      launch_tiled((k_gemm<MODE, 9>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 512, s, a);
-      break;
-    case 18:
-      launch_tiled((k_gemm_rb<MODE, 1, 2>), dim3((a.N + 63) / 64, (a.M + 31) / 32, grid_z), 256, s, a);
-      break;
+      return;
     case 19:
       launch_tiled((k_gemm_rb<MODE, 2, 1>), dim3((a.N + 31) / 32, (a.M + 63) / 64, grid_z), 256, s, a);
-      break;
-    case 20:
-      launch_tiled((k_gemm_rb<MODE, 2, 2>), dim3((a.N + 63) / 64, (a.M + 63) / 64, grid_z), 256, s, a);
-      break;
+      return;
     case 10:
       launch_tiled((k_gemm<MODE, 10>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 256, s, a);
-      break;
+      return;
     case 17:
       launch_tiled((k_gemm<MODE, 17>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 512, s, a);
-      break;
+      return;
+#endif
     default:
-      launch_tiled((k_gemm<MODE, 0>), dim3((a.N + 31) / 32, (a.M + 31) / 32, grid_z), 256, s, a);
+      throw std::runtime_error("gemm: tile layout " + std::to_string(a.layout) + " is not in this build");
   }
 }
 

@@ -3,9 +3,9 @@
 // the SEANet implicit-GEMM convs at B = 32). Each variant is checked against a naive fp64-accumulated
 // kernel, then timed with HIP events (20 warm launches, 100 timed, median of 5 blocks of 20), on
 // uniform random operands. rocBLAS is the calibration only (tools, never the product).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ipocket-tts_amd/csrc tools/mm_bench.hip \
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPTTS_PROBES -Iinclude -Ipocket-tts_amd/csrc tools/mm_bench.hip \
 //        -lrocblas -o tools/bin/mm_bench
-// Usage: mm_bench [case-substring] [layout] [S]
+// Usage: mm_bench [case-substring] [layout] [S]   (S < 0: split tail of -S slices, ILV layouts)
 #include "../pocket-tts_amd/csrc/kernels.hip"
 
 #include <rocblas/rocblas.h>
@@ -71,13 +71,18 @@ int main(int argc, char** argv) {
   const char* only_case = argc > 1 ? argv[1] : nullptr;
   const int only_layout = argc > 2 ? atoi(argv[2]) : -100;
   const int only_s = argc > 3 ? atoi(argv[3]) : -1;
+  setvbuf(stdout, nullptr, _IOLBF, 0);
   hipStream_t st;
   CK(hipStreamCreate(&st));
   rocblas_handle bh;
   rocblas_create_handle(&bh);
   rocblas_set_stream(bh, st);
   const int B = 32;
-  float *P, *Y, *ref, *got;
+  float *P, *Y, *ref, *got, *slab;
+  int* tickets;
+  CK(hipMalloc(&slab, sizeof(float) * (32 << 20)));
+  CK(hipMalloc(&tickets, sizeof(int) * 4096));
+  CK(hipMemset(tickets, 0, sizeof(int) * 4096));
   CK(hipMalloc(&P, sizeof(float) * (96 << 20)));
   CK(hipMalloc(&Y, sizeof(float) * (64 << 20)));
   CK(hipMalloc(&ref, sizeof(float) * (64 << 20)));
@@ -111,8 +116,10 @@ int main(int argc, char** argv) {
     a.T_out = T_in; a.out_tstride = 1;
     cases.push_back({nm, a, v});
   };
-  const std::vector<std::pair<int, int>> big = {{-1, 1}, {12, 1}, {21, 1}, {26, 1}, {30, 1}, {31, 1}, {38, 1},
-                                                {34, 1}, {35, 1}, {36, 1}, {39, 1}, {30, 2}, {31, 2}};
+  const std::vector<std::pair<int, int>> big = {{-1, 1}, {30, 1}, {31, 1}, {34, 1}, {35, 1}, {36, 1}, {39, 1},
+                                                {30, -2}, {30, -4}, {30, -8}, {31, -2}, {31, -4}, {31, -8},
+                                                {34, -2}, {34, -4}, {34, -8}, {36, -2}, {36, -4}, {36, -8},
+                                                {32, -2}, {32, -4}, {35, -2}, {35, -4}, {39, -2}, {39, -4}};
   const std::vector<std::pair<int, int>> mid = {{-1, 1}, {6, 1}, {12, 1}, {15, 1}, {32, 1}, {33, 1}, {37, 1},
                                                 {34, 1}, {35, 1}, {36, 1}, {39, 1}, {21, 1}, {30, 1}, {31, 1},
                                                 {6, 2}, {32, 2}, {33, 2}, {34, 2}, {35, 2}, {30, 2}, {31, 2},
@@ -154,7 +161,16 @@ int main(int argc, char** argv) {
       if (layout == -1 && a.mode != 0) continue;
       const int bk = (layout == 8 || layout == 15 || layout == 16) ? 64 : 32;
       if (layout >= 0 && (a.K % bk != 0 || (a.mode == 1 && a.cin % bk != 0))) continue;
-      if (S > 1) {
+      if (S < 0) {
+        if (layout < 30 || a.mode != 0) continue;
+        v.S = 1;
+        v.partial = nullptr;
+        v.tail_S = -S;
+        v.tail_slab = slab;
+        v.tail_cap = 32l << 20;
+        v.tickets = tickets;
+        v.tickets_cap = 4096;
+      } else if (S > 1) {
         if (a.K / bk < S) continue;
         v.S = S;
         v.partial = P;
@@ -168,10 +184,15 @@ int main(int argc, char** argv) {
           rocblas_sgemm(bh, rocblas_operation_transpose, rocblas_operation_none, a.N, a.M, a.K, &one, a.W, a.K, a.X,
                         (rocblas_int)a.ldx, &zero, Y, a.N);
         } else {
-          gemm(v, S, st);
+          gemm(v, S > 0 ? S : 1, st);
         }
       };
-      run();
+      try {
+        run();
+      } catch (const std::exception& e) {
+        printf("   L%d S %d : %s\n", layout, S, e.what());
+        continue;
+      }
       CK(hipGetLastError());
       if (S > 1) hipLaunchKernelGGL(k_sum, dim3((out_n + 255) / 256), dim3(256), 0, st, P, S, out_n, got);
       else CK(hipMemcpyAsync(got, Y, out_n * 4, hipMemcpyDeviceToDevice, st));
