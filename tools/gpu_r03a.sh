@@ -22,4 +22,12 @@ if [ -n "${SWEEP:-}" ]; then
       bash tools/sweep_env.sh > $OUT/sweep.log 2>&1 || { echo "sweep failed"; tail -n 20 $OUT/sweep.log; exit 1; }
   grep median $OUT/sweep.log
 fi
+if [ -f gpubin/devlib/libprobes.so ] && [ "${DEVX:-1}" = "1" ]; then  # experiments on a working-copy probe build
+  MMB_CAP=1 timeout -k 10 300 ./gpubin/mm_bench mimi > $OUT/mm_bench_cap1_mimi.log 2>&1 || { echo "mm_bench cap failed"; exit 1; }
+  MMB_CAP=1 timeout -k 10 300 ./gpubin/mm_bench conv > $OUT/mm_bench_cap1_conv.log 2>&1 || { echo "mm_bench cap failed"; exit 1; }
+  L40="mimi.qkv=40,mimi.out=40:4,mimi.ff1=40,mimi.ff2=40:4,seanet.conv0=40:4,seanet.up0.convtr=40:4,seanet.up1.convtr=40,seanet.up2.convtr=40"
+  PTTS_LIB=gpubin/devlib/libprobes.so VAR=PTTS_OVR VALUES="- $L40" REPS=2 bash tools/sweep_env.sh > $OUT/sweep40.log 2>&1 \
+      || { echo "sweep40 failed"; tail -n 5 $OUT/sweep40.log; exit 1; }
+  grep median $OUT/sweep40.log
+fi
 exit 0
