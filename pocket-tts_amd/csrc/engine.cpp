@@ -214,6 +214,12 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_HIP(hipEventCreateWithFlags(&ev_admit_, hipEventDisableTiming));
   pipeline_ = cfg.pipeline != 0;
   head_resident_ = flow_head_max_resident(dev_);
+  flm_resident_ = flow_lm_max_resident(dev_);
+  // k_flow_lm hand-off regions: one set per front hand-off buffer, all empty (0xFFFFFFFF); the
+  // launch of step k reads set k % 3 and empties set (k + 1) % 3
+  flm_ws_ = dalloc((size_t)NHB * flow_lm_set_floats());
+  PTTS_HIP(hipMemset(flm_ws_, 0xFF, sizeof(float) * NHB * flow_lm_set_floats()));
+  PTTS_HIP(hipDeviceSynchronize());  // null-stream memset: see dalloc
 
   if (!cfg.defer_weights) {
     std::unique_ptr<TensorSource> src = cfg.weights_path && cfg.weights_path[0]
@@ -307,11 +313,54 @@ void Engine::derive_gemv() {
   PTTS_HIP(hipStreamSynchronize(stream_));
 }
 
+// The FlowLM step matrices in the fragment order of the persistent transformer launch (k_flow_lm):
+// in_proj and out_proj {1, 32} (8 K slices of 128), linear1 and linear2 {1, 64} (slices of 256).
+void Engine::derive_flow_lm() {
+  const size_t per_layer = (size_t)4 * D * D + (size_t)2 * D * FF;
+  void* p = nullptr;
+  PTTS_HIP(hipMalloc(&p, sizeof(float) * per_layer * NL));  // every element is written by the packing
+  allocs_.push_back(p);
+  flm_pack_ = (float*)p;
+  for (int l = 0; l < NL; ++l) {
+    const Layout::TL& t = L_.fl[l];
+    float* dst = flm_pack_ + per_layer * l;
+    pack_gemv(W(t.in_proj), 3 * D, D, GemvShape{1, 32}, dst, stream_);
+    pack_gemv(W(t.out_proj), D, D, GemvShape{1, 32}, dst + (size_t)3 * D * D, stream_);
+    pack_gemv(W(t.l1), FF, D, GemvShape{1, 64}, dst + (size_t)4 * D * D, stream_);
+    pack_gemv(W(t.l2), D, FF, GemvShape{1, 64}, dst + (size_t)4 * D * D + (size_t)D * FF, stream_);
+  }
+  // the launch's per-layer operand table (FlowLmArgs::lw)
+  std::vector<const float*> tab((size_t)NL * FL_LW);
+  for (int l = 0; l < NL; ++l) {
+    const Layout::TL& t = L_.fl[l];
+    const float* pl = flm_pack_ + per_layer * l;
+    const float* e[FL_LW] = {pl, pl + (size_t)3 * D * D, pl + (size_t)4 * D * D, pl + (size_t)4 * D * D + (size_t)D * FF,
+                             W(t.n1w), W(t.n1b), W(t.n2w), W(t.n2b)};
+    for (int i = 0; i < FL_LW; ++i) tab[(size_t)FL_LW * l + i] = e[i];
+  }
+  if (!flm_tab_) flm_tab_ = (const float**)dalloc(tab.size() * sizeof(void*) / sizeof(float));
+  PTTS_HIP(hipMemcpy(flm_tab_, tab.data(), tab.size() * sizeof(void*), hipMemcpyHostToDevice));
+  PTTS_HIP(hipGetLastError());
+  PTTS_HIP(hipStreamSynchronize(stream_));
+}
+
+// The six FlowLM layers of a step as one persistent launch: B <= 32 rows, f32 weights, the
+// launch's 256 workgroups co-resident (each waits for data the others store), and sequential
+// stepping only: in a pipelined step the concurrent back part's workgroups share every CU, and a
+// phase of the persistent launch waits for its slowest workgroup (steady step 0.584 -> 0.640 ms at
+// B = 32, while alone the launch matched the 48 launches it replaces, 312 vs 304 us).
+bool Engine::use_flow_lm(int B) const {
+  if (pipeline_ || !flm_pack_ || !flm_ws_ || nhb_ != NHB || !flow_lm_fits(B) || flow_lm_grid() > flm_resident_)
+    return false;
+  return !probe_env("PTTS_FLM_OFF");  // probe builds: the 48-launch form for A/B runs
+}
+
 void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   if (fp8_ && f8map_.empty()) derive_fp8();
   if (wq_ == QUANT_NONE && !fp8_ && gvmap_.empty()) derive_gemv();
+  if (wq_ == QUANT_NONE && !fp8_ && !flm_pack_) derive_flow_lm();
   if (!inw_t_) {  // every element is written by the transpose below: no (null-stream) memset
     void* p = nullptr;
     PTTS_HIP(hipMalloc(&p, sizeof(float) * LDIM * D));
@@ -732,7 +781,39 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     ops.push_back({"flow.input_ln1", [=](hipStream_t s) { input_ln(lat, w, lw, lb, x, h, B, s); },
                    2.0 * B * D * LDIM, 4.0 * ((double)D * LDIM + (double)B * (LDIM + 2 * D))});
   }
-  flow_layers(ops, B, RowMap{0, 1, 0, fpos_}, 1, true, "flow");
+  if (use_flow_lm(B)) {
+    FlowLmArgs f{};
+    f.B = B;
+    f.x = x_;
+    f.h = h_;
+    const size_t per_layer = (size_t)4 * D * D + (size_t)2 * D * FF;
+    f.lw = flm_tab_;
+    f.onw = W(L_.out_norm_w);
+    f.onb = W(L_.out_norm_b);
+    f.kv = kv_;
+    f.kv_layer = kv_layer_;
+    f.kv_slot = kv_slot_;
+    f.cap = max_ctx_;
+    f.map = RowMap{0, 1, 0, fpos_, nullptr};
+    f.rope = rope_;
+    const size_t set = flow_lm_set_floats();
+    f.ws = flm_ws_ + set * hb;
+    f.ws_next = flm_ws_ + set * ((hb + 1) % NHB);
+    f.err = herr_;
+    f.dbg = probe_env("PTTS_FLM_DBG") ? (unsigned long long*)strtoull(probe_env("PTTS_FLM_DBG"), nullptr, 0) : nullptr;
+    // per row and layer: 2 (4 D^2 + 2 D FF) GEMM flops + 4,096 L attention flops; bytes: the
+    // step's f32 matrices once, K and V of L cached positions (8,192 B each) per row and layer
+    const double L = plan_ctx_ > 0 ? plan_ctx_ : max_ctx_ / 2.0;
+    const double fl = (double)B * NL * (2.0 * per_layer + 4096.0 * L);
+    const double by = 4.0 * per_layer * NL + (double)B * NL * (8192.0 * L + 4.0 * 8 * D);
+    Op op{"flow.layers", [f](hipStream_t s) { flow_lm(f, s); }, fl, by};
+    // an isolated replay reads its own set again: empty it first (time_op, overlap_probe)
+    float* wsc = f.ws;
+    op.prep = [wsc, set](hipStream_t s) { PTTS_HIP(hipMemsetD32Async(wsc, 0xFFFFFFFFu, set, s)); };
+    ops.push_back(op);
+  } else {
+    flow_layers(ops, B, RowMap{0, 1, 0, fpos_}, 1, true, "flow");
+  }
   // ---- flow head (mlp.rs:215-383): cond_embed | out_eos, EOS bookkeeping, noise
   linear_split(ops, "head.cond_eos_gemm", h_, D, B, W(L_.cond_eos_w), NCOND, D, &S);
   PTTS_REQUIRE(S <= FLOW_COND_MAX_SLABS, "head.flow_cond sums at most 16 split-K slabs");
@@ -1297,8 +1378,10 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
     sync();
     *h_err_ = 0;
     PTTS_HIP(hipMemsetAsync(herr_, 0, sizeof(int), stream_));
+    // a timed-out launch leaves its hand-off regions part-filled: empty every set again
+    if (flm_ws_) PTTS_HIP(hipMemsetD32Async(flm_ws_, 0xFFFFFFFFu, NHB * flow_lm_set_floats(), stream_));
     PTTS_HIP(hipStreamSynchronize(stream_));
-    throw Error(PTTS_ERR_HIP, "flow-head persistent launch: an in-launch hand-off wait timed out");
+    throw Error(PTTS_ERR_HIP, "persistent launch (FlowLM layers / flow head): an in-launch hand-off wait timed out");
   }
   const float* hl = h_meta_[q];
   const FrameFlags* hf = (const FrameFlags*)(h_meta_[q] + (size_t)max_slots_ * LDIM);
@@ -1357,6 +1440,8 @@ double Engine::time_op(int B, const std::string& name, int reps) {
     PTTS_HIP(hipEventSynchronize(e1));
     PTTS_HIP(hipEventElapsedTime(&prep, e0, e1));
     ms = both - prep;
+    sel->prep(stream_);  // leave the op's state as a step finds it (flow.layers: its set empty)
+    PTTS_HIP(hipStreamSynchronize(stream_));
   } else {
     sel->fn(stream_);  // warm
     PTTS_HIP(hipEventRecord(e0, stream_));
@@ -1393,7 +1478,11 @@ void Engine::overlap_probe(int B, int reps, double* us) {
   for (int part = 0; part < 2; ++part) {  // as captured for pipelined stepping (back part capped)
     PTTS_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
     set_wg_cap(part == 1 ? back_cap_ : 0);
-    for (size_t i = part ? cut : 0; i < (part ? ops.size() : cut); ++i) ops[i].fn(stream_);
+    for (size_t i = part ? cut : 0; i < (part ? ops.size() : cut); ++i) {
+      // each replay of the persistent FlowLM launch needs its hand-off set empty
+      if (ops[i].name == "flow.layers") ops[i].prep(stream_);
+      ops[i].fn(stream_);
+    }
     set_wg_cap(0);
     PTTS_HIP(hipStreamEndCapture(stream_, &g[part]));
     PTTS_HIP(hipGraphInstantiate(&ge[part], g[part], nullptr, nullptr, 0));

@@ -12,6 +12,8 @@
 #include <cmath>
 #include <stdexcept>
 
+#include "devfn.h"
+
 namespace ptts {
 
 // Measurement probes (PTTS_PROBES builds only, tools/): GemmArgs::probe bit 0 skips the MFMAs,
@@ -37,25 +39,6 @@ static size_t cap_lds(K kernel, int cap) {
   return need > fa.sharedSizeBytes ? need - fa.sharedSizeBytes : 0;
 }
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ float gelu_tanh(float x) {
-  // candle Tensor::gelu (tanh approximation), transformer.rs:85
-  return 0.5f * x * (1.0f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
-}
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
-__device__ __forceinline__ float elu1(float x) { return x >= 0.f ? x : expf(x) - 1.0f; }
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
 
 // Sum over S (<= 16) split-K slabs p[z * stride] in z order, every load issued before the first
 // add (a runtime-bounded loop waited on each load in turn: one L2 round trip per slab).
@@ -1636,23 +1619,9 @@ void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* pac
 // =============================================================================================
 // Row reduce + epilogue + LayerNorm/modulate. One workgroup per row.
 // =============================================================================================
-__device__ __forceinline__ float block_sum(float v, float* sh) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) sh[wave] = v;
-  __syncthreads();
-  return (sh[0] + sh[1]) + (sh[2] + sh[3]);
-}
 
 // One workgroup per (row, 1024-column block); each thread owns 4 consecutive columns (float4).
 // The S partial slabs are summed in z order (deterministic) with 4 independent loads in flight.
-__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-__device__ __forceinline__ float4 f4mul(float4 a, float4 b) {
-  return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
-}
 __device__ __forceinline__ float act1(float x, int act) {
   return act == ACT_GELU ? gelu_tanh(x) : (act == ACT_SILU ? silu(x) : (act == ACT_ELU ? elu1(x) : x));
 }
@@ -1829,16 +1798,6 @@ void layernorm(const float* x, long ldx, float* y, long ldy, int M, int N, const
 // =============================================================================================
 // QKV (+ split-K reduce) -> RoPE -> KV append. One thread per (row, head, rotation pair).
 // =============================================================================================
-__device__ __forceinline__ void row_slot_pos(const RowMap& mp, int row, int& slot, int& pos) {
-  if (mp.tab) {
-    const int v = mp.tab[row];
-    slot = v < 0 ? -1 : v >> 16;
-    pos = v < 0 ? 0 : v & 0xFFFF;
-    return;
-  }
-  slot = mp.slot0 + row / mp.rps;
-  pos = (mp.pos_arr ? mp.pos_arr[slot] : mp.p0) + row % mp.rps;
-}
 
 __global__ __launch_bounds__(256) void k_qkv_rope(const float* P, int S, const float* dense, int M, int nh,
                                                   RowMap mp, KvStore kv, float* Q) {
@@ -2248,15 +2207,6 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
 // sums its 192 q|k|v columns over the S slabs, rotates q and k (rope.rs:18-60), appends k, v at
 // the row's position and attends over the cached keys 0..pos-1 plus the new key from LDS.
 // ---------------------------------------------------------------------------------------------
-// Sum over each 16-lane row of the wave with DPP (quad_perm xor 1, xor 2, row_half_mirror,
-// row_mirror); every lane of the row ends with the row's sum.
-__device__ __forceinline__ float row16_sum(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true));
-  return v;
-}
 
 // Decode attention of the FlowLM step fused with the QKV slab sum, RoPE and KV append
 // (attention.rs:104-283 with the single-query mask skip of sdpa.rs:3-18). One 256-thread
@@ -3050,7 +3000,6 @@ void resample(const float* x, int n_in, const float* taps, const ResamplePlan& p
 // v_mfma_f32_16x16x4_f32 fragments as in k_attn16: lane (c = l & 15, G = l >> 4) supplies
 // A[row c][k] and B[k][col c] for k = 64*wave + FH_KJ*(s/4) + 4*G + s%4 at step s (FH_KJ below); D reg g -> row 4G+g, col c.
 // =============================================================================================
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int FH_WAVES = 8;  // FH_D, FH_L, FH_DEPTH: kernels.h
 // k layout of a lane's 16 values: float4 j of lane group G holds k = 64 wave + FH_KJ j + 4 G ..+3,
 // so the 4 lane groups of a row read 64 contiguous bytes per load instruction (16 rows x 64 B
@@ -3061,50 +3010,7 @@ constexpr int FH_KJ = 16;
 // group's 16x16 tile, 1 KB on
 constexpr int FH_SJ = 16 * 16 * 4;
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t fh_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ float4 fh_ld(__amdgpu_buffer_rsrc_t r, int byte_off) {  // sc1 load
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ __forceinline__ void fh_st(__amdgpu_buffer_rsrc_t r, int byte_off, float4 f) {  // sc1 store
-  const u32x4 v = {__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
-}
-// storing wave: drain its sc1 stores, then one lane signals
-__device__ __forceinline__ void fh_publish(int* ctr) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// whole workgroup: thread 0 polls until ctr >= target (bounded: a timeout sets *err and stops
-// waiting for the rest of the launch), then the barrier releases every wave's sc1 loads
-__device__ __forceinline__ void fh_wait(int* ctr, int target, int* err, bool& dead) {
-  if (threadIdx.x == 0 && !dead) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 20)) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        dead = true;
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
-}
 __device__ __forceinline__ float4 f4ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
-// a handed-off value never carries the empty pattern: a NaN is stored as the canonical quiet NaN
-// (the result stays NaN, as in the reference, and no consumer waits for it)
-__device__ __forceinline__ float fh_canon(float x) { return x != x ? __uint_as_float(0x7FC00000u) : x; }
-__device__ __forceinline__ void fh_put(__amdgpu_buffer_rsrc_t r, int byte_off, float4 f) {
-  fh_st(r, byte_off, make_float4(fh_canon(f.x), fh_canon(f.y), fh_canon(f.z), fh_canon(f.w)));
-}
-__device__ __forceinline__ bool fh_empty(float4 v) {
-  return ((int)(__float_as_uint(v.x) == ~0u) | (int)(__float_as_uint(v.y) == ~0u) |
-          (int)(__float_as_uint(v.z) == ~0u) | (int)(__float_as_uint(v.w) == ~0u)) != 0;
-}
 // consumer: this lane's 16 values of a region (byte offset `off`), re-read until none is empty.
 // The loop condition is wave-uniform; a timeout sets *err and stops waiting for the rest of the
 // launch (the frame is poisoned, fetch() reports it).

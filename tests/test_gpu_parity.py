@@ -227,8 +227,10 @@ def test_generate_convenience(gpu_engine):
 
 def test_plan_and_kernel_timer(gpu_engine):
     names = gpu_engine.plan_ops(8)
-    assert "flow.l0.qkv_gemm" in names and "seanet.conv0" in names and names[-1] == "commit"
-    assert gpu_engine.time_kernel(8, "flow.l0.ff1_gemm", reps=5) > 0
+    # B <= 32: the six FlowLM layers are one persistent launch (k_flow_lm)
+    assert "flow.layers" in names and "flow.l0.qkv_gemm" not in names
+    assert "seanet.conv0" in names and names[-1] == "commit"
+    assert gpu_engine.time_kernel(8, "flow.layers", reps=5) > 0
 
 
 def test_pipelined_stepping_matches_oracle(oracle):
