@@ -212,6 +212,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
     PTTS_HIP(hipEventRecord(ev_back_[q], stream_));
   }
   PTTS_HIP(hipEventCreateWithFlags(&ev_admit_, hipEventDisableTiming));
+  PTTS_HIP(hipEventCreateWithFlags(&ev_be_tail_, hipEventDisableTiming));
+  PTTS_HIP(hipEventRecord(ev_admit_, stream_));
   pipeline_ = cfg.pipeline != 0;
   head_resident_ = flow_head_max_resident(dev_);
   flm_resident_ = flow_lm_max_resident(dev_);
@@ -242,6 +244,7 @@ Engine::~Engine() {
     if (ev_back_[q]) (void)hipEventDestroy(ev_back_[q]);
   }
   if (ev_admit_) (void)hipEventDestroy(ev_admit_);
+  if (ev_be_tail_) (void)hipEventDestroy(ev_be_tail_);
   if (stream_be_) (void)hipStreamDestroy(stream_be_);
   for (void* p : allocs_) (void)hipFree(p);
   for (int q = 0; q < NHB; ++q) {
@@ -1857,7 +1860,14 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
       PTTS_REQUIRE(ids[total_ids + j] >= 0 && ids[total_ids + j] < VOCAB, "token id out of range");
     total_ids += n_ids[i];
   }
-  sync();
+  // Stream-ordered admission (no drain of the pipeline: a full sync() here stalled the front part
+  // at every admission, a large share of the serving path's time): the host waits only until the
+  // previous admission has consumed the pinned staging buffers (its event), and stream_ waits on
+  // the GPU for the back parts already queued on stream_be_, which may still decode a frame of a
+  // slot's previous utterance (they write its histories and Mimi position).
+  PTTS_HIP(hipEventSynchronize(ev_admit_));
+  PTTS_HIP(hipEventRecord(ev_be_tail_, stream_be_));
+  PTTS_HIP(hipStreamWaitEvent(stream_, ev_be_tail_, 0));
   // copy-on-admit of the immutable voice prefixes
   for (int i = 0; i < n; ++i) {
     const ptts_voice* v = voices[i];
@@ -1885,7 +1895,7 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
   }
   // staged through pinned buffers so the copies are truly asynchronous: admission returns with
   // the prefill still running and the caller's first step queued right behind it (no host
-  // round trip in between); the sync() above guarantees the staging is free again
+  // round trip in between); the event wait above guarantees the staging is free again
   memcpy(h_slots_, slots, sizeof(int) * n);
   memcpy(h_st_, st.data(), sizeof(SlotState) * n);
   memcpy(h_fp_, fp.data(), sizeof(int) * n);

@@ -188,6 +188,7 @@ class Engine {
   // admission / slot_close / set_latent write slot state on stream_ after the last front part the
   // next back part decodes: that back part (stream_be_) waits for this event first
   hipEvent_t ev_admit_ = nullptr;
+  hipEvent_t ev_be_tail_ = nullptr;  // stream_be_'s queue at an admission (stream_ waits for it)
   bool admit_pending_ = false;
   void mark_admission();
   long long k_ = 0;          // steps issued

@@ -168,6 +168,7 @@ class BatchScheduler:
         self.cv = threading.Condition()
         self.running = True
         self.steps = 0
+        self.row_frames = 0  # frames delivered (valid rows summed over steps)
         self.trace = bool(os.environ.get("PTTS_SERVE_TRACE"))
         self.thread = threading.Thread(target=self._loop, name="ptts-scheduler", daemon=True)
         self.thread.start()
@@ -196,26 +197,32 @@ class BatchScheduler:
         self.thread.join()
 
     # -- driver thread
-    def _admit(self):
+    def _take(self) -> list[Request]:
+        """(under self.cv) waiting requests that fit the free slots, slots assigned and reserved"""
         free = [s for s in range(self.max_rows) if s not in self.active]
         batch = []
         while self.waiting and free:
             req = self.waiting.popleft()
             req.slot = free.pop(0)
+            self.active[req.slot] = req
             batch.append(req)
-        if batch:
-            self.engine.open_many([r.slot for r in batch], [r.voice for r in batch], [r.ids for r in batch],
-                                  [r.params for r in batch])
-            now = time.time()
-            for r in batch:
-                r.times["admit"] = now
-                self.active[r.slot] = r
+        return batch
+
+    def _admit(self, batch: list[Request]):
+        """(outside self.cv: submit() runs on the HTTP event loop and must never wait for an
+        admission's engine call) one batched admission of the taken requests"""
+        self.engine.open_many([r.slot for r in batch], [r.voice for r in batch], [r.ids for r in batch],
+                              [r.params for r in batch])
+        now = time.time()
+        for r in batch:
+            r.times["admit"] = now
 
     def _deliver(self, res, rows) -> list[int]:
         done = []
         for slot, req in list(self.active.items()):
             if slot < rows and res.valid[slot]:
                 req.frames += 1
+                self.row_frames += 1
                 if req.frames == 1:
                     req.times["first"] = time.time()
                 req.put(res.pcm[slot])  # a view: fetch() returns fresh arrays every step
@@ -223,7 +230,10 @@ class BatchScheduler:
                     req.times["last"] = time.time()
                     if self.trace:
                         t = req.times
-                        print(f"ptts-serve slot {slot} frames {req.frames} admit_wait_ms "
+                        t0 = t.get("route", t["submit"])
+                        print(f"ptts-serve slot {slot} route_to_submit_ms {1e3 * (t['submit'] - t0):.1f} "
+                              f"first_to_chunk0_ms {1e3 * (t.get('chunk0', t['first']) - t['first']):.1f} "
+                              f"frames {req.frames} admit_wait_ms "
                               f"{1e3 * (t['admit'] - t['submit']):.1f} first_ms {1e3 * (t['first'] - t['submit']):.1f} "
                               f"last_ms {1e3 * (t['last'] - t['submit']):.1f} steps {self.steps}", flush=True)
                     req.put(None)
@@ -242,8 +252,10 @@ class BatchScheduler:
                         self.cv.wait()
                     if not self.running:
                         break
-                    self._admit()
+                    batch = self._take()
                     rows = max(self.active) + 1 if self.active else 0
+                if batch:
+                    self._admit(batch)
                 if rows:
                     self.engine.step_async(rows)
                 if pending is not None:
@@ -252,8 +264,8 @@ class BatchScheduler:
                         for slot in done:
                             del self.active[slot]
                     pending = None
-                if rows:
-                    self.engine.sync()
+                if rows:  # fetch waits for this call's frame only (a pipelined engine's next
+                    # front part keeps running; a sync() here drained the pipeline every step)
                     pending = (self.engine.fetch(rows), rows)
                     self.steps += 1
         except BaseException as e:  # deliver the failure to every waiting client
@@ -411,6 +423,8 @@ async def pcm_chunks(r: Request):
                 raise item
             batch.append(item)
         if batch:
+            if "chunk0" not in r.times:
+                r.times["chunk0"] = time.time()
             yield pcm_i16_le_bytes(batch[0] if len(batch) == 1 else np.concatenate(batch))
         if done:
             return
@@ -439,7 +453,9 @@ def create_app(service: TTSService):
 
     @app.get("/health")
     def health():
-        return JSONResponse({"status": "healthy", "version": VERSION, "worker": worker}, headers=hdr)
+        sch = getattr(service, "scheduler", None)
+        stats = {"steps": sch.steps, "frames": sch.row_frames} if isinstance(sch, BatchScheduler) else {}
+        return JSONResponse({"status": "healthy", "version": VERSION, "worker": worker, **stats}, headers=hdr)
 
     @app.post("/generate")
     def generate(req: GenerateRequest):
@@ -448,8 +464,11 @@ def create_app(service: TTSService):
 
     @app.post("/stream")
     async def stream(req: GenerateRequest):
+        t_route = time.time()
         r = submit(**req.model_dump())
-        return StreamingResponse(pcm_chunks(r), media_type="audio/pcm", headers=hdr)
+        r.times["route"] = t_route
+        return StreamingResponse(pcm_chunks(r), media_type="audio/pcm",
+                                 headers={**hdr, "X-PTTS-Route-Time": f"{t_route:.6f}"})
 
     @app.post("/v1/audio/speech")
     def openai_speech(req: OpenAIRequest):
@@ -522,7 +541,11 @@ def _listen_socket(host: str, port: int):
     and the kernel spreads incoming connections over them (no proxy process in the data path)."""
     import socket
 
-    so = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    # proto IPPROTO_TCP explicitly: asyncio sets TCP_NODELAY only on transports whose socket says
+    # so (proto 0 left Nagle on: every chunk written behind the response headers waited for the
+    # client's delayed ACK, ~20 ms on a stream's first chunk); the listener's NODELAY is inherited
+    so = socket.socket(socket.AF_INET, socket.SOCK_STREAM, socket.IPPROTO_TCP)
+    so.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
     so.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     so.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
     so.bind((host, port))

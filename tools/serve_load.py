@@ -60,11 +60,14 @@ def client(port, first, n, t_go, seconds):
             body = {"token_ids": ids(first + j + 97 * len(reqs)), "words": 20, "eos_threshold": 1e9}
             with clients[j].stream("POST", base + "/stream", json=body) as r:
                 r.raise_for_status()
+                t_hdr = time.time()
+                t_route = float(r.headers.get("X-PTTS-Route-Time", "nan"))
                 for chunk in r.iter_bytes():
                     if t_first is None and chunk:
                         t_first = time.time()
                     nbytes += len(chunk)
-            reqs.append({"start": t0, "first": t_first, "end": time.time(), "samples": nbytes // 2})
+            reqs.append({"start": t0, "first": t_first, "end": time.time(), "samples": nbytes // 2,
+                         "route": t_route, "headers": t_hdr})
         out[j] = reqs
 
     ts = [threading.Thread(target=one, args=(j,)) for j in range(n)]
@@ -112,16 +115,19 @@ def main():
         for rnd in range(args.rounds):
             procs, first = [], 0
             t_go = time.time() + 3.0  # client processes start, import httpx and connect first
+            h0 = httpx.get(base + "/health", timeout=5.0).json()
             for n in per:
                 procs.append(subprocess.Popen([sys.executable, __file__, "client", str(args.port), str(first), str(n),
                                                repr(t_go), repr(args.seconds)], stdout=subprocess.PIPE, text=True))
                 first += n
             streams = []
+            h1 = None
             for p in procs:
                 o, _ = p.communicate(timeout=600)
                 if p.returncode != 0:
                     raise SystemExit(f"client failed ({p.returncode})")
                 streams += json.loads(o.strip().splitlines()[-1])
+            h1 = httpx.get(base + "/health", timeout=5.0).json()
             reqs = [q for st in streams for q in st]
             t0 = min(q["start"] for q in reqs)
             wall = max(q["end"] for q in reqs) - t0
@@ -134,6 +140,17 @@ def main():
                    "frames_per_request": reqs[0]["samples"] // 1920,
                    "ttfc_burst_p50_ms": pct(burst, 0.5), "ttfc_burst_p90_ms": pct(burst, 0.9),
                    "ttfc_steady_p50_ms": pct(steady, 0.5), "ttfc_steady_p90_ms": pct(steady, 0.9)}
+            lat = [(q["route"] - q["start"], q["headers"] - q["start"], q["first"] - q["route"]) for st in streams
+                   for q in st[1:] if q["route"] == q["route"]]
+            if lat:  # where a steady request's time to first chunk goes (client and server share a clock)
+                med3 = np.median(np.array(lat), axis=0)
+                rec.update({"steady_start_to_route_ms": round(1e3 * med3[0], 2),
+                            "steady_start_to_headers_ms": round(1e3 * med3[1], 2),
+                            "steady_route_to_first_chunk_ms": round(1e3 * med3[2], 2)})
+            if "steps" in h0:  # the scheduler's own counters over the round (3-s start-up included)
+                ds, df = h1["steps"] - h0["steps"], h1["frames"] - h0["frames"]
+                rec.update({"server_steps": ds, "server_rows_per_step": round(df / max(ds, 1), 2),
+                            "server_ms_per_step": round(1e3 * (wall) / max(ds, 1), 4)})
             result["rounds"].append(rec)
             print(json.dumps(rec), flush=True)
         med = lambda k: float(np.median([r[k] for r in result["rounds"] if r[k] is not None]))
