@@ -71,20 +71,21 @@ def measured_mfma():
     return json.load(open(path))["ops"] if path.exists() else {}
 
 
-def phase_rooflines(per_op, plan, B, K):
+def phase_rooflines(per_op, plan, B, K, back_frames=1):
     """SURVEY §8(d) per-phase rooflines over one batched step, from the per-op HIP-event times
     (each op timed alone; the plan lists every launch of the step, repeated ops counted per launch):
     - front (FlowLM step + flow head): HBM-bound; algorithmic bytes = the FlowLM per-step weights
       (84,527,137 f32) + per row the KV read of 49,152 B per cached position at the job's mean
       context L = prompt + text + K/2, and the 49,152-B append;
     - back (Mimi decode): MFMA-bound; algorithmic flops = 525.1 MFLOP per frame (GEMMs and convs)
-      + 65,536 per window key (W = 266) of window attention, per row."""
+      + 65,536 per window key (W = 266) of window attention, per row and frame; a back pass covers
+      back_frames frames."""
     us = {n: u for u, n, _, _ in per_op}
     front = sum(us[n] for n, _, _ in plan if n.startswith(("flow.", "head.", "front_commit")))
     back = sum(us[n] for n, _, _ in plan if n.startswith(("mimi.", "seanet.")) or n == "commit")
     L = PROMPT_FRAMES + TEXT_TOKENS + K / 2.0
     f_bytes = 84_527_137 * 4 + B * (49_152 * L + 49_152)
-    b_flops = B * (525.1e6 + 65_536 * 266)
+    b_flops = back_frames * B * (525.1e6 + 65_536 * 266)
     fa = f_bytes / (front * 1e-6) / 1e9
     ba = b_flops / (back * 1e-6) / 1e12
     mf = measured_mfma()  # rocprof MFMA busy over the back ops, against 1,024 SIMDs at 2.4 GHz
@@ -151,6 +152,9 @@ class _SelftestEngine:
         self.frames = {s: 0 for s in slots}
         self.max = {s: p.max_frames for s, p in zip(slots, params)}
 
+    def frame_lag(self):
+        return 0, 0
+
     def step_async(self, n):
         time.sleep(2e-4)
         for s in self.frames:
@@ -214,6 +218,9 @@ def main():
     ap.add_argument("--no-op-times", action="store_true", help="skip the per-op HIP-event pass (PMC runs)")
     ap.add_argument("--no-quant-variant", action="store_true",
                     help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM) and fp8_gemm engines")
+    ap.add_argument("--back-frames", type=int, default=1, choices=(1, 2),
+                    help="frames per Mimi-decode pass of pipelined stepping (ptts_engine_config.back_frames; "
+                         "2 measured slower: 0.600 vs 0.588 ms per step, DESIGN.md section 4)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sequential stepping (no FlowLM / Mimi overlap across consecutive frames)")
     ap.add_argument("--profile-frames", type=int, default=0,
@@ -254,7 +261,7 @@ def main():
     K = args.profile_frames if args.profile_frames > 0 else UTT_FRAMES
     jobs = max(MIN_JOBS, -(-args.steps // K)) if args.profile_frames <= 0 else 1
     pipeline = not args.no_pipeline
-    calls = K + (1 if pipeline else 0)  # overlapped stepping returns each frame one call later
+    back_frames = args.back_frames if pipeline else 1
     max_ctx = PROMPT_FRAMES + TEXT_TOKENS + K + 8
 
     def params(round_id, b, n_frames):
@@ -264,13 +271,14 @@ def main():
     # ---- engine (+ one RCCL broadcast of the packed weights at load time)
     if dist is None:
         eng = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
-                        pipeline=pipeline)
+                        pipeline=pipeline, back_frames=back_frames)
     else:
         import torch
 
         blob = torch.empty(pt.Engine.weight_blob_bytes() // 4, dtype=torch.float32, device=dev)
         eng = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
-                        weight_blob=blob.data_ptr(), defer_weights=(rank != 0), pipeline=pipeline)
+                        weight_blob=blob.data_ptr(), defer_weights=(rank != 0), pipeline=pipeline,
+                        back_frames=back_frames)
         if not selftest:
             torch.cuda.synchronize()
         broadcast_weights(dist, blob)
@@ -300,7 +308,7 @@ def main():
 
         # warmup: a short job on the same rows (graph capture, caches), then the rows are re-admitted
         admit(0, max(1, W))
-        for _ in range(max(1, W) + (1 if pipeline else 0)):
+        for _ in range(max(1, W) + sum(eng.frame_lag())):  # a frame arrives frame_lag() calls late
             eng.step_async(B)
         eng.sync()
         barrier()
@@ -313,6 +321,7 @@ def main():
             admit(1 + j, K)
             eng.sync()
             admit_s += time.perf_counter() - ta0
+            calls = K + sum(eng.frame_lag())  # the K frames, then the calls that drain the last one
             for _ in range(calls):
                 eng.step_async(B)
             eng.sync()
@@ -372,7 +381,7 @@ def main():
         roof["algorithmic_flops"] = fl
         top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
         sum_ops_ms = round(sum(u for u, _, _, _ in per_op) / 1000.0, 3)
-        roof["phases"] = phase_rooflines(per_op, plan, B, K)
+        roof["phases"] = phase_rooflines(per_op, plan, B, K, back_frames)
         if args.ops_out:
             with open(args.ops_out, "w") as f:
                 json.dump({"n_rows": B, "plan": [n for n, _, _ in plan],
@@ -406,7 +415,7 @@ def main():
     eng.close()  # one engine on the GPU at a time
     if not args.no_quant_variant and world == 1:
         eq = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
-                       pipeline=pipeline, weight_quant=pt.QUANT_FLOW_LM)
+                       pipeline=pipeline, back_frames=back_frames, weight_quant=pt.QUANT_FLOW_LM)
         q_el, q_ad, _ = timed_job(eq)
         quant = {"value": round(jobs * B * K * 1920 / 24000.0 / q_el, 2), "unit": "audio-sec/wall-sec",
                  "ms_per_step": round(1000.0 * q_el / steps, 4),
@@ -415,7 +424,7 @@ def main():
                  "int8_matrices": eq.int8_matrices}
         eq.close()
         ef = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
-                       pipeline=pipeline, fp8_gemm=True)
+                       pipeline=pipeline, back_frames=back_frames, fp8_gemm=True)
         f_el, f_ad, _ = timed_job(ef)
         fp8 = {"value": round(jobs * B * K * 1920 / 24000.0 / f_el, 2), "unit": "audio-sec/wall-sec",
                "ms_per_step": round(1000.0 * f_el / steps, 4),
@@ -465,7 +474,9 @@ def main():
                                "(BASELINE configs[2])",
                    "global_batch": B * world, "utterance_frames": K, "jobs": jobs, "prompt_frames": PROMPT_FRAMES,
                    "text_tokens": TEXT_TOKENS, "temp": 0.7, "parallelism": f"replicas x{world}",
-                   "stepping": "pipelined (Mimi decode of frame k overlaps FlowLM step k+1)" if pipeline
+                   "stepping": ("pipelined, frame pairs (one Mimi decode pass per two frames, overlapping "
+                                "FlowLM steps k and k+1)" if back_frames == 2 else
+                                "pipelined (Mimi decode of frame k overlaps FlowLM step k+1)") if pipeline
                    else "sequential",
                    "pcm_to_host": "every frame, async D2H into pinned memory inside the step graphs"},
         "per_job": per_job,

@@ -31,9 +31,10 @@ extern "C" {
 #define PTTS_ERR_IO 4      /* weights file missing or malformed */
 
 /* ABI version of this header. Bumped whenever a struct below changes layout (3: cfg_yaml was
- * appended to ptts_engine_config). A caller checks ptts_abi_version() == PTTS_ABI_VERSION before
- * passing any struct: a library built from another header reads a different layout. */
-#define PTTS_ABI_VERSION 3
+ * appended to ptts_engine_config; 4: back_frames). A caller checks ptts_abi_version() ==
+ * PTTS_ABI_VERSION before passing any struct: a library built from another header reads a
+ * different layout. */
+#define PTTS_ABI_VERSION 4
 int ptts_abi_version(void);
 /* Build id of the loaded library: the first 16 hex digits of the sha256 over the sources it was
  * built from (pocket-tts_amd/Makefile, BUILD_ID), with "+probes" appended for a measurement build
@@ -82,6 +83,13 @@ typedef struct ptts_engine_config {
                                be present and equal them, or creation fails (PTTS_ERR_INVALID,
                                naming the key): another variant is a rebuild. Checked, not read
                                for shapes. ptts_config_check() is the same check alone. */
+  int back_frames;          /* pipelined engines only: frames per Mimi-decode pass, 1 (default;
+                               0 means 1) or 2. With 2, frames 2j and 2j+1 of every row are
+                               decoded by ONE back pass (the streaming codec state advances as for
+                               two passes; PCM identical within float rounding), a call returns the
+                               frame computed three calls earlier, and rows admitted at an odd
+                               call start one call later (an utterance's frames pair up from its
+                               first). ptts_frame_lag() reports both delays. */
 } ptts_engine_config;
 
 #define PTTS_QUANT_NONE 0
@@ -203,6 +211,16 @@ int ptts_step_async(ptts_engine* e, int n_rows);
 int ptts_sync(ptts_engine* e);
 int ptts_fetch(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
                float* eos_logits, float* latents);
+/* Calls by which a frame trails the call that computed its FlowLM step: 0 (sequential), 1
+ * (pipelined), 3 (pipelined, back_frames = 2). *admit_delay (may be NULL): 1 if the rows of the
+ * latest admission start one call late (back_frames = 2, admitted at an odd call), else 0. A row
+ * admitted before call k returns its first frame from call k + lag + admit_delay. */
+int ptts_frame_lag(const ptts_engine* e, int* admit_delay);
+/* ptts_fetch of an earlier call: calls_back = 0 is the latest call (= ptts_fetch), 1 the call
+ * before it. Lets a driver keep one call in flight (issue call k+1, then fetch call k) so that the
+ * GPU always has the next step queued while the host hands out frames. calls_back <= 1. */
+int ptts_fetch_prev(ptts_engine* e, int calls_back, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
+                    float* eos_logits, float* latents);
 /* Test hook (teacher forcing): overwrite the backbone input latent of `slot`. */
 int ptts_slot_set_latent(ptts_engine* e, int slot, const float* latent32);
 /* MimiModel::decode_from_latent (mimi.rs:143-157) after the denorm + DummyQuantizer of

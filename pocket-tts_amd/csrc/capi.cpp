@@ -250,6 +250,18 @@ int ptts_fetch(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uin
   return guard([&] { eng(e).fetch(n_rows, pcm, frame_valid, last, eos_logits, latents); });
 }
 
+int ptts_fetch_prev(ptts_engine* e, int calls_back, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
+                    float* eos_logits, float* latents) {
+  return guard([&] { eng(e).fetch(n_rows, pcm, frame_valid, last, eos_logits, latents, calls_back); });
+}
+
+int ptts_frame_lag(const ptts_engine* e, int* admit_delay) {
+  if (!e || !e->impl) return -1;
+  const ptts::Engine& E = *e->impl;
+  if (admit_delay) *admit_delay = E.admit_delay();
+  return E.frame_lag();
+}
+
 int ptts_generate(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* ids, int n_ids,
                   const ptts_gen_params* p, float* pcm_out, int max_samples, int* n_samples) {
   return guard([&] {
@@ -260,12 +272,14 @@ int ptts_generate(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* 
     std::vector<float> pcm((size_t)B * ptts::FRAME);
     std::vector<uint8_t> valid(B), last(B);
     int total = 0;
-    // pipelined engines return each frame one call later: one extra call drains the last one
-    for (int it = 0; it < p->max_frames + 1; ++it) {
+    // a frame arrives frame_lag() calls after its step (+1 when the admission started a call late):
+    // that many extra calls drain the last one
+    const int lead = E.frame_lag() + E.admit_delay();
+    for (int it = 0; it < p->max_frames + lead; ++it) {
       E.step_async(B);
       E.fetch(B, pcm.data(), valid.data(), last.data(), nullptr, nullptr);
       if (!valid[slot]) {
-        if (it == 0 && E.pipelined()) continue;
+        if (it < lead) continue;
         break;
       }
       const int take = std::max(0, std::min(ptts::FRAME, max_samples - total));

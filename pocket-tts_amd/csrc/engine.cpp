@@ -80,6 +80,9 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_REQUIRE(cfg.fp8_gemm == 0 || cfg.fp8_gemm == 1, "fp8_gemm must be 0 or 1");
   PTTS_REQUIRE(!(cfg.fp8_gemm && cfg.weight_quant != QUANT_NONE), "fp8_gemm and weight_quant are exclusive");
   fp8_ = cfg.fp8_gemm;
+  PTTS_REQUIRE(cfg.back_frames >= 0 && cfg.back_frames <= 2, "back_frames must be 0, 1 or 2");
+  nfr_ = cfg.pipeline && cfg.back_frames == 2 ? 2 : 1;
+  nhb_ = nfr_ == 2 ? NHB : 3;
   int ndev = 0;
   PTTS_HIP(hipGetDeviceCount(&ndev));
   PTTS_REQUIRE(dev_ >= 0 && dev_ < ndev, "HIP device ordinal out of range");
@@ -117,9 +120,15 @@ Engine::Engine(const ptts_engine_config& cfg) {
     eos_out_[q] = meta_[q] + (size_t)B * (LDIM + 2);
     pcm_[q] = dalloc((size_t)B * FRAME);
   }
+  if (nfr_ == 2)
+    for (int p = 0; p < NHB / 2; ++p) {
+      pcmp_[p] = dalloc((size_t)B * 2 * FRAME);
+      PTTS_HIP(hipHostMalloc((void**)&h_pcmp_[p], sizeof(float) * B * 2 * FRAME, hipHostMallocDefault));
+    }
+  PTTS_HIP(hipHostMalloc((void**)&h_act_, sizeof(SlotState) * B, hipHostMallocDefault));
   // back part's own split-K slabs: up to 8 slices of the Mimi / conv0 rows (B * 16 x 512), 4 of the
-  // stage-0 transposed conv (B * 16 x 6 * 256)
-  mpcap_ = std::max({(size_t)8 * B * UP * MD, (size_t)4 * B * UP * RATIOS[0] * (MD / 2)});
+  // stage-0 transposed conv (B * 16 x 6 * 256), per frame of a pass
+  mpcap_ = (size_t)nfr_ * std::max({(size_t)8 * B * UP * MD, (size_t)4 * B * UP * RATIOS[0] * (MD / 2)});
   mpartial_ = dalloc(mpcap_);
 
   // streaming conv histories (SEANetDecoder, seanet.rs:307-402): source T, channels, rows kept
@@ -171,21 +180,22 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_HIP(hipDeviceSynchronize());                    // null-stream memset: see dalloc
   hctr_ = (int*)dalloc(4 * ((B + 15) / 16) + 4);
   herr_ = (int*)dalloc(4);
-  mx_ = dalloc((size_t)B * UP * MD);
-  mh_ = dalloc((size_t)B * UP * MD);
-  mq_ = dalloc((size_t)B * UP * MD);
-  mo_ = dalloc((size_t)B * UP * MD);
-  mqkv_ = dalloc((size_t)B * UP * 3 * MD);
-  mu_ = dalloc((size_t)B * UP * MFF);
-  a0_ = dalloc((size_t)B * 16 * 512);
+  const size_t BF = (size_t)B * nfr_;  // utterance frames of one back-part pass
+  mx_ = dalloc(BF * UP * MD);
+  mh_ = dalloc(BF * UP * MD);
+  mq_ = dalloc(BF * UP * MD);
+  mo_ = dalloc(BF * UP * MD);
+  mqkv_ = dalloc(BF * UP * 3 * MD);
+  mu_ = dalloc(BF * UP * MFF);
+  a0_ = dalloc(BF * 16 * 512);
   int T = 16, ch = 512;
   for (int i = 0; i < 3; ++i) {
     T *= RATIOS[i];
     ch /= 2;
-    cb_[i] = dalloc((size_t)B * T * ch);
-    ce_[i] = dalloc((size_t)B * T * ch);
-    cv_[i] = dalloc((size_t)B * T * (ch / 2));
-    ca_[i] = dalloc((size_t)B * T * ch);
+    cb_[i] = dalloc(BF * T * ch);
+    ce_[i] = dalloc(BF * T * ch);
+    cv_[i] = dalloc(BF * T * (ch / 2));
+    ca_[i] = dalloc(BF * T * ch);
     trb_[i] = dalloc((size_t)RATIOS[i] * ch);
   }
   temb_ = dalloc((size_t)lsd_ * FD);
@@ -213,15 +223,19 @@ Engine::Engine(const ptts_engine_config& cfg) {
   }
   PTTS_HIP(hipEventCreateWithFlags(&ev_admit_, hipEventDisableTiming));
   PTTS_HIP(hipEventCreateWithFlags(&ev_be_tail_, hipEventDisableTiming));
+  PTTS_HIP(hipEventCreateWithFlags(&ev_act_, hipEventDisableTiming));
+  PTTS_HIP(hipEventRecord(ev_act_, stream_));
   PTTS_HIP(hipEventRecord(ev_admit_, stream_));
   pipeline_ = cfg.pipeline != 0;
   head_resident_ = flow_head_max_resident(dev_);
   flm_resident_ = flow_lm_max_resident(dev_);
   // k_flow_lm hand-off regions: one set per front hand-off buffer, all empty (0xFFFFFFFF); the
   // launch of step k reads set k % 3 and empties set (k + 1) % 3
-  flm_ws_ = dalloc((size_t)NHB * flow_lm_set_floats());
-  PTTS_HIP(hipMemset(flm_ws_, 0xFF, sizeof(float) * NHB * flow_lm_set_floats()));
-  PTTS_HIP(hipDeviceSynchronize());  // null-stream memset: see dalloc
+  if (probe_env("PTTS_FLM_ON")) {  // probe builds only (use_flow_lm)
+    flm_ws_ = dalloc((size_t)NHB * flow_lm_set_floats());
+    PTTS_HIP(hipMemset(flm_ws_, 0xFF, sizeof(float) * NHB * flow_lm_set_floats()));
+    PTTS_HIP(hipDeviceSynchronize());  // null-stream memset: see dalloc
+  }
 
   if (!cfg.defer_weights) {
     std::unique_ptr<TensorSource> src = cfg.weights_path && cfg.weights_path[0]
@@ -245,12 +259,16 @@ Engine::~Engine() {
   }
   if (ev_admit_) (void)hipEventDestroy(ev_admit_);
   if (ev_be_tail_) (void)hipEventDestroy(ev_be_tail_);
+  if (ev_act_) (void)hipEventDestroy(ev_act_);
   if (stream_be_) (void)hipStreamDestroy(stream_be_);
   for (void* p : allocs_) (void)hipFree(p);
   for (int q = 0; q < NHB; ++q) {
     if (h_pcm_[q]) (void)hipHostFree(h_pcm_[q]);
     if (h_meta_[q]) (void)hipHostFree(h_meta_[q]);
   }
+  for (int p = 0; p < NHB / 2; ++p)
+    if (h_pcmp_[p]) (void)hipHostFree(h_pcmp_[p]);
+  if (h_act_) (void)hipHostFree(h_act_);
   if (h_err_) (void)hipHostFree(h_err_);
   for (void* hp : {(void*)h_slots_, (void*)h_st_, (void*)h_fp_, (void*)h_ids_, (void*)h_tab_})
     if (hp) (void)hipHostFree(hp);
@@ -347,15 +365,15 @@ void Engine::derive_flow_lm() {
   PTTS_HIP(hipStreamSynchronize(stream_));
 }
 
-// The six FlowLM layers of a step as one persistent launch: B <= 32 rows, f32 weights, the
-// launch's 256 workgroups co-resident (each waits for data the others store), and sequential
-// stepping only: in a pipelined step the concurrent back part's workgroups share every CU, and a
-// phase of the persistent launch waits for its slowest workgroup (steady step 0.584 -> 0.640 ms at
-// B = 32, while alone the launch matched the 48 launches it replaces, 312 vs 304 us).
+// The six FlowLM layers of a step as one persistent launch (B <= 32 rows, f32 weights, the
+// launch's 256 workgroups co-resident: each waits for data the others store). Measured slower
+// than the 48 launches it replaces in every mode (sequential B = 32 step 0.829 vs
+// 0.809 ms, B = 1 0.561 vs 0.520 ms; pipelined 0.640 vs 0.584 ms, the concurrent back part
+// stretching every phase's slowest workgroup), so it runs only in probe builds on request
+// (PTTS_FLM_ON, tools/flm_ab.py, tools/flm_stamps.py).
 bool Engine::use_flow_lm(int B) const {
-  if (pipeline_ || !flm_pack_ || !flm_ws_ || nhb_ != NHB || !flow_lm_fits(B) || flow_lm_grid() > flm_resident_)
-    return false;
-  return !probe_env("PTTS_FLM_OFF");  // probe builds: the 48-launch form for A/B runs
+  if (!flm_pack_ || !flm_ws_ || !flow_lm_fits(B) || flow_lm_grid() > flm_resident_) return false;
+  return probe_env("PTTS_FLM_ON") != nullptr;
 }
 
 void Engine::finalize() {
@@ -363,7 +381,7 @@ void Engine::finalize() {
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   if (fp8_ && f8map_.empty()) derive_fp8();
   if (wq_ == QUANT_NONE && !fp8_ && gvmap_.empty()) derive_gemv();
-  if (wq_ == QUANT_NONE && !fp8_ && !flm_pack_) derive_flow_lm();
+  if (wq_ == QUANT_NONE && !fp8_ && !flm_pack_ && probe_env("PTTS_FLM_ON")) derive_flow_lm();
   if (!inw_t_) {  // every element is written by the transpose below: no (null-stream) memset
     void* p = nullptr;
     PTTS_HIP(hipMalloc(&p, sizeof(float) * LDIM * D));
@@ -801,7 +819,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     f.rope = rope_;
     const size_t set = flow_lm_set_floats();
     f.ws = flm_ws_ + set * hb;
-    f.ws_next = flm_ws_ + set * ((hb + 1) % NHB);
+    f.ws_next = flm_ws_ + set * ((hb + 1) % nhb_);
     f.err = herr_;
     f.dbg = probe_env("PTTS_FLM_DBG") ? (unsigned long long*)strtoull(probe_env("PTTS_FLM_DBG"), nullptr, 0) : nullptr;
     // per row and layer: 2 (4 D^2 + 2 D FF) GEMM flops + 4,096 L attention flops; bytes: the
@@ -1034,7 +1052,9 @@ static BackTile back_tile(const std::string& op, bool pipeline) {
 
 // BACK part of a step: Mimi decode of the frames the front part left in buffer `hb`; `qp` is the
 // frame's parity for the quantizer history (the previous frame's quantizer output is in qp ^ 1).
-void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
+void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
+  PTTS_REQUIRE(nfr >= 1 && nfr <= nfr_, "frames per back pass out of range");
+  const int hb2 = (hb + 1) % nhb_;  // the second frame's hand-off buffer (nfr == 2)
   const bool big = B >= 16;  // B * 16 >= 256 Mimi rows: the LDS-DMA tiles fill the chip
   auto tile = [&](const std::string& op, int small_splits) {
     BackTile t = big ? back_tile(op, pipeline_) : BackTile{0, small_splits};
@@ -1043,20 +1063,26 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   };
   // ---- Mimi decode (mimi.rs:143-157): quantize + upsample, decoder transformer, SEANet decoder
   {
-    const float *lat = lat_out_[hb], *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w),
-                *wu = W(L_.up_w);
+    const float *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w), *wu = W(L_.up_w);
     const float *lw = W(L_.mdec[0].n1w), *lb = W(L_.mdec[0].n1b);
     const float* qin = qprev_ + (size_t)(qp ^ 1) * max_slots_ * MD;
     float* qout = qprev_ + (size_t)qp * max_slots_ * MD;
     float *x = mx_, *h = mh_;
-    const FrameFlags* fl = flags_[hb];
+    const float* lat0 = lat_out_[hb];
+    const float* lat1 = lat_out_[hb2];
+    const FrameFlags* fl0 = flags_[hb];
+    const FrameFlags* fl1 = flags_[hb2];
     ops.push_back({"mimi.quant_upsample",
-                   [=](hipStream_t s) { quant_upsample(lat, B, sd, mn, wq, wu, qin, qout, fl, x, h, lw, lb, s); },
-                   (double)B * (2.0 * MD * LDIM + 2.0 * MD * 2 * UP + 8.0 * UP * MD),
-                   4.0 * ((double)B * (LDIM + 2 * MD + 2.0 * UP * MD) + 2.0 * MD * LDIM + MD * 2.0 * UP + 2.0 * MD)});
+                   [=](hipStream_t s) {
+                     const float* lat[2] = {lat0, lat1};
+                     const FrameFlags* fl[2] = {fl0, fl1};
+                     quant_upsample(lat, fl, nfr, B, sd, mn, wq, wu, qin, qout, x, h, lw, lb, s);
+                   },
+                   (double)B * nfr * (2.0 * MD * LDIM + 2.0 * MD * 2 * UP + 8.0 * UP * MD),
+                   4.0 * ((double)B * nfr * (LDIM + 2 * MD + 2.0 * UP * MD) + 2.0 * MD * LDIM + MD * 2.0 * UP + 2.0 * MD)});
   }
-  const int MR = B * UP;
-  RowMap mmap{0, UP, 0, mpos_};
+  const int MR = B * UP * nfr;  // Mimi rows of the pass: 16 per frame per utterance
+  RowMap mmap{0, UP * nfr, 0, mpos_};
   // a split-K GEMM into the back part's own slab buffer, its epilogue in a row reduce
   auto split_gemm = [&](const std::string& name, const float* X, int M, const float* Wt, int N, int K, BackTile t) {
     PTTS_REQUIRE(t.splits >= 1 && t.splits <= 16, name + ": split-K 1..16");
@@ -1091,9 +1117,19 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
       // queries), its 16 QKV rows in, the 16 output rows, the appended K/V; 16 queries x W keys x
       // 8 heads x 64 x 4 flops = 65,536 W
       const double Wn = plan_win_ > 0 ? plan_win_ : (double)(MCTX + UP - 1);
-      ops.push_back({p + ".attention", [=](hipStream_t s) { attention16_qkv(qkv, MR, MNH, mmap, kv, MCTX, O, s); },
-                     (double)B * 65536.0 * Wn,
-                     (double)B * (4.0 * 2 * MNH * 64 * Wn + 4.0 * UP * (3.0 * MD + MD + 2.0 * MD))});
+      if (nfr == 1) {
+        ops.push_back({p + ".attention", [=](hipStream_t s) { attention16_qkv(qkv, MR, MNH, mmap, kv, MCTX, O, s); },
+                       (double)B * 65536.0 * Wn,
+                       (double)B * (4.0 * 2 * MNH * 64 * Wn + 4.0 * UP * (3.0 * MD + MD + 2.0 * MD))});
+      } else {  // two frames: the second frame's queries see the first frame's keys, appended by
+        // other workgroups, so the append (with RoPE) is its own launch ahead of the attention
+        float* Q = mq_;
+        ops.push_back({p + ".qkv_rope", [=](hipStream_t s) { qkv_rope_append(nullptr, 0, qkv, MR, MNH, mmap, kv, Q, s); },
+                       0.0, 4.0 * MR * (3.0 * MD + 3.0 * MD)});
+        ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, MR, MNH, mmap, kv, MCTX, 16, O, s); },
+                       (double)B * nfr * 65536.0 * Wn,
+                       (double)B * nfr * (4.0 * 2 * MNH * 64 * Wn + 4.0 * UP * (MD + MD))});
+      }
     }
     {  // out projection, split-K; LayerScale + residual and this layer's norm2 in the reduce
       const BackTile to = tile("mimi.out", 4);
@@ -1158,12 +1194,12 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
      // at B = 1 the unsplit launch had 16 workgroups, 27.4 us)
     const BackTile tc = tile("seanet.conv0", 8);
     const int s_c0 = std::max(tc.splits, 2);
-    conv_op(ops, "seanet.conv0", mx_, B, 16, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
-            nullptr, 16, 1, big ? tc.layout : 6, 0, nullptr, s_c0);
+    conv_op(ops, "seanet.conv0", mx_, B, 16 * nfr, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
+            nullptr, 16 * nfr, 1, big ? tc.layout : 6, 0, nullptr, s_c0);
     RowReduceArgs r{};
     r.P = mpartial_;
     r.S = s_c0;
-    r.M = B * 16;
+    r.M = B * 16 * nfr;
     r.N = 512;
     r.bias = W(L_.dc0_b);
     r.act = ACT_ELU;
@@ -1172,7 +1208,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
     ops.push_back(rr_op("seanet.conv0_reduce", r));
   }
   const float* cin_buf = a0_;
-  int T = 16, ch = 512;
+  int T = 16 * nfr, ch = 512;
   for (int i = 0; i < 3; ++i) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
@@ -1221,18 +1257,21 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
   }
   {
     const float *X = ca_[2], *H = hist_[7], *w = W(L_.dfin_w), *b = W(L_.dfin_b);
-    float* Y = pcm_[hb];
-    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, FRAME, 64, 3, w, b, Y, 0, s); },
-                   2.0 * B * FRAME * 3 * 64, 4.0 * ((double)B * FRAME * 64 + B * 2.0 * 64 + B * FRAME + 3 * 64 + 1)});
+    float* Y = nfr == 1 ? pcm_[hb] : pcmp_[hb / 2];  // a pair's PCM is [B][2][1920]
+    const int TF = FRAME * nfr;
+    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, TF, 64, 3, w, b, Y, 0, s); },
+                   2.0 * B * TF * 3 * 64, 4.0 * ((double)B * TF * 64 + B * 2.0 * 64 + B * TF + 3 * 64 + 1)});
   }
   // ---- commit of the back part: conv histories and Mimi positions of rows with a frame
   {
     CommitArgs c{};
     const float* srcs[8] = {mx_, a0_, ce_[0], ca_[0], ce_[1], ca_[1], ce_[2], ca_[2]};
-    for (int i = 0; i < 8; ++i) c.h[i] = HistDesc{srcs[i], hist_[i], hist_T_[i], hist_C_[i], hist_P_[i]};
+    for (int i = 0; i < 8; ++i) c.h[i] = HistDesc{srcs[i], hist_[i], hist_T_[i] * nfr, hist_C_[i], hist_P_[i]};
     c.nh = 8;
     c.B = B;
     c.flags = flags_[hb];
+    c.flags1 = flags_[hb2];
+    c.nfr = nfr;
     c.mpos = mpos_;
     double hb_bytes = 0;  // every history row is read from its activation and stored
     for (int i = 0; i < 8; ++i) hb_bytes += 8.0 * B * hist_P_[i] * hist_C_[i];
@@ -1244,7 +1283,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int qp) {
 std::vector<Op> Engine::build_step(int B) {
   std::vector<Op> ops;
   build_front(ops, B, 0);
-  build_back(ops, B, 0, 0);
+  build_back(ops, B, 0, nfr_, 0);
   return ops;
 }
 
@@ -1279,7 +1318,7 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
   if (it != graphs_.end()) return it->second;
   std::vector<Op> ops;
   if (part == 0) build_front(ops, B, hb);
-  else build_back(ops, B, hb, qp);
+  else build_back(ops, B, hb, nfr_, qp);
   hipGraph_t g = nullptr;
   // captured on the stream it is launched on (the back part of a pipelined step: stream_be_)
   hipStream_t cs = part == 1 && pipeline_ ? stream_be_ : stream_;
@@ -1301,6 +1340,14 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
     }
     if (part == 0) {  // the hand-off timeout word, read by fetch() without a device round trip
       PTTS_HIP(hipMemcpyAsync(h_err_, herr_, sizeof(int), hipMemcpyDeviceToHost, cs));
+      // frame pairs: a pass covers the larger row count of its two frames, so this frame's rows
+      // past B carry no frame
+      if (nfr_ == 2 && B < max_slots_)
+        PTTS_HIP(hipMemsetAsync(flags_[hb] + B, 0, sizeof(FrameFlags) * (max_slots_ - B), cs));
+    } else if (nfr_ == 2) {  // both frames of the pair leave HBM inside the pass
+      PTTS_HIP(hipMemcpyAsync(h_pcmp_[hb / 2], pcmp_[hb / 2], sizeof(float) * B * 2 * FRAME, hipMemcpyDeviceToHost, cs));
+      for (int q : {hb, (hb + 1) % nhb_})
+        PTTS_HIP(hipMemcpyAsync(h_meta_[q], meta_[q], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost, cs));
     } else {  // the frame of this buffer leaves HBM inside the step (fetch() reads host memory)
       PTTS_HIP(hipMemcpyAsync(h_pcm_[hb], pcm_[hb], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, cs));
       PTTS_HIP(hipMemcpyAsync(h_meta_[hb], meta_[hb], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
@@ -1331,6 +1378,8 @@ void Engine::step_async(int B) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
   PTTS_HIP(hipSetDevice(dev_));
+  prev_hb_ = out_hb_;
+  prev_rows_ = out_rows_;
   const int hb = (int)(k_ % nhb_), qp = (int)(k_ & 1);
   hipGraphExec_t front = part_graph(0, B, hb, 0);
   if (!pipeline_) {
@@ -1339,6 +1388,37 @@ void Engine::step_async(int B) {
     PTTS_HIP(hipGraphLaunch(back, stream_));
     out_hb_ = hb;
     out_rows_ = B;
+  } else if (nfr_ == 2) {
+    // Frame pairs: call k runs front(k) into buffer k % 6; at even k >= 2 one back pass decodes
+    // frames k-2 and k-1 (buffers (k-2) % 6 and + 1, quantizer parity (k-2)/2 & 1) on stream_be_,
+    // concurrently with the next fronts. Front(k) waits only for the pass over frame k-6, the
+    // last reader of its buffer. The call's frame is k-3 (its pass was launched by call k-1 or
+    // k-2; fetch() waits for it).
+    rows_hb_[hb] = B;
+    if (!act_slots_.empty() && (k_ & 1) == 0) {  // rows admitted at an odd call start now
+      for (size_t i = 0; i < act_slots_.size(); ++i)
+        PTTS_HIP(hipMemcpyAsync(st_ + act_slots_[i], h_act_ + act_slots_[i], sizeof(SlotState), hipMemcpyHostToDevice,
+                                stream_));
+      PTTS_HIP(hipEventRecord(ev_act_, stream_));
+      act_slots_.clear();
+    }
+    PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
+    PTTS_HIP(hipGraphLaunch(front, stream_));
+    PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
+    if ((k_ & 1) == 0 && k_ >= 2) {
+      const int h0 = (int)((k_ - 2) % nhb_), h1 = (h0 + 1) % nhb_, pq = (int)(((k_ - 2) / 2) & 1);
+      hipGraphExec_t back = part_graph(1, std::max(rows_hb_[h0], rows_hb_[h1]), h0, pq);
+      PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[h1], 0));
+      if (admit_pending_) {
+        PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
+        admit_pending_ = false;
+      }
+      PTTS_HIP(hipGraphLaunch(back, stream_be_));
+      PTTS_HIP(hipEventRecord(ev_back_[h0], stream_be_));
+      PTTS_HIP(hipEventRecord(ev_back_[h1], stream_be_));
+    }
+    out_hb_ = (int)((k_ + nhb_ - 3) % nhb_);
+    out_rows_ = k_ >= 3 ? rows_hb_[out_hb_] : 0;
   } else {
     const int prev_rows = k_ > 0 ? front_rows_ : B;
     const int hb1 = (hb + nhb_ - 1) % nhb_, qp1 = qp ^ 1;  // frame k-1
@@ -1368,15 +1448,18 @@ void Engine::sync() {
 
 // Outputs of the last call's frame (see step_async); rows past the rows that frame covered
 // report no frame. The step's graphs already copied the frame into pinned host memory.
-void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat) {
+void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat, int calls_back) {
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
+  PTTS_REQUIRE(calls_back == 0 || calls_back == 1, "calls_back must be 0 or 1");
+  // the host copies of a call's frame stay intact for two more calls (three hand-off buffers)
+  const int q = calls_back ? prev_hb_ : out_hb_;
+  const int rows = calls_back ? prev_rows_ : out_rows_;
   // Pipelined: wait only for the back part that produced this call's frame. The front part of
   // the next frame keeps running, so the front stream never idles across calls (the next call's
   // front graph is queued behind it while this one still runs).
-  if (pipeline_) PTTS_HIP(hipEventSynchronize(ev_back_[out_hb_]));
+  if (pipeline_) PTTS_HIP(hipEventSynchronize(ev_back_[q]));
   else sync();
-  const int q = out_hb_;
-  const int n = std::min(B, out_rows_);
+  const int n = std::min(B, rows);
   if (*h_err_) {  // k_flow_head's bounded hand-off waits: a timeout poisons the frame, fail loudly
     sync();
     *h_err_ = 0;
@@ -1389,12 +1472,16 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
   const float* hl = h_meta_[q];
   const FrameFlags* hf = (const FrameFlags*)(h_meta_[q] + (size_t)max_slots_ * LDIM);
   const float* he = h_meta_[q] + (size_t)max_slots_ * (LDIM + 2);
+  // a pair's PCM is [B][2][1920] (the frame of buffer q is half q % 2)
+  auto pcm_row = [&](int b) {
+    return nfr_ == 2 ? h_pcmp_[q / 2] + ((size_t)b * 2 + (q & 1)) * FRAME : h_pcm_[q] + (size_t)b * FRAME;
+  };
   for (int b = 0; b < B; ++b) {
     const bool ok = b < n && hf[b].valid;
     if (valid) valid[b] = ok;
     if (last) last[b] = ok && hf[b].last;
     if (pcm) {
-      if (b < n) memcpy(pcm + (size_t)b * FRAME, h_pcm_[q] + (size_t)b * FRAME, sizeof(float) * FRAME);
+      if (b < n) memcpy(pcm + (size_t)b * FRAME, pcm_row(b), sizeof(float) * FRAME);
       else memset(pcm + (size_t)b * FRAME, 0, sizeof(float) * FRAME);
     }
     if (eos) eos[b] = b < n ? he[b] : 0.f;
@@ -1866,6 +1953,7 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
   // the GPU for the back parts already queued on stream_be_, which may still decode a frame of a
   // slot's previous utterance (they write its histories and Mimi position).
   PTTS_HIP(hipEventSynchronize(ev_admit_));
+  PTTS_HIP(hipEventSynchronize(ev_act_));  // pending start-of-utterance copies read h_act_
   PTTS_HIP(hipEventRecord(ev_be_tail_, stream_be_));
   PTTS_HIP(hipStreamWaitEvent(stream_, ev_be_tail_, 0));
   // copy-on-admit of the immutable voice prefixes
@@ -1896,6 +1984,15 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
   // staged through pinned buffers so the copies are truly asynchronous: admission returns with
   // the prefill still running and the caller's first step queued right behind it (no host
   // round trip in between); the event wait above guarantees the staging is free again
+  // frame pairs: an utterance's frames pair up from its first, so rows admitted before an odd
+  // call stay inactive for that call and start at the next (their state is written then)
+  admit_delay_ = nfr_ == 2 && (k_ & 1) ? 1 : 0;
+  if (admit_delay_)
+    for (int i = 0; i < n; ++i) {
+      h_act_[slots[i]] = st[i];
+      act_slots_.push_back(slots[i]);
+      st[i].active = 0;
+    }
   memcpy(h_slots_, slots, sizeof(int) * n);
   memcpy(h_st_, st.data(), sizeof(SlotState) * n);
   memcpy(h_fp_, fp.data(), sizeof(int) * n);
@@ -1922,9 +2019,7 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     r.st = st_;
     r.fpos = fpos_;
     r.mpos = mpos_;
-    r.flags0 = flags_[0];
-    r.flags1 = flags_[1];
-    r.flags2 = flags_[2];
+    for (int q = 0; q < NHB; ++q) r.flags[q] = flags_[q];
     slot_reset(r, stream_);
     PTTS_HIP(hipGetLastError());
   }
@@ -2016,9 +2111,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
     r.st = st_;
     r.fpos = fpos_;
     r.mpos = mpos_;
-    r.flags0 = flags_[0];
-    r.flags1 = flags_[1];
-    r.flags2 = flags_[2];
+    for (int q = 0; q < NHB; ++q) r.flags[q] = flags_[q];
     slot_reset(r, stream_);
     PTTS_HIP(hipGetLastError());
   }
@@ -2033,7 +2126,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
                             hipMemcpyHostToDevice, stream_));
     PTTS_HIP(hipMemcpyAsync(flags_[par] + slot, &on, sizeof on, hipMemcpyHostToDevice, stream_));
     std::vector<Op> ops;
-    build_back(ops, slot + 1, par, par);
+    build_back(ops, slot + 1, par, 1, par);
     size_t j = 0;
     for (; j < ops.size(); ++j) {
       if (ops[j].name == "seanet.conv0" && tr) rows16(tr + (size_t)i * UP * MD, mx_);
@@ -2057,6 +2150,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
 void Engine::slot_close(int slot) {
   PTTS_REQUIRE(slot >= 0 && slot < max_slots_, "slot out of range");
   sync();
+  act_slots_.erase(std::remove(act_slots_.begin(), act_slots_.end(), slot), act_slots_.end());
   SlotState s{};
   s.eos_step = -1;
   memcpy(h_st_, &s, sizeof s);  // pinned staging (free: sync() above)

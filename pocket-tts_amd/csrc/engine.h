@@ -40,6 +40,10 @@ class Engine {
   float* blob() { return blob_; }
   int max_slots() const { return max_slots_; }
   bool pipelined() const { return pipeline_; }
+  // calls by which a frame trails its FlowLM step (ptts_frame_lag) and the latest admission's
+  // start delay
+  int frame_lag() const { return !pipeline_ ? 0 : (nfr_ == 2 ? 3 : 1); }
+  int admit_delay() const { return admit_delay_; }
 
   ptts_voice* voice_from_prompt(const float* prompt, int F);
   ptts_voice* voice_from_pcm(const float* pcm, int n) { return voice_from_audio(pcm, n, PTTS_SAMPLE_RATE, 0); }
@@ -54,7 +58,8 @@ class Engine {
 
   void step_async(int B);
   void sync();
-  void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat);
+  // the frame of the call calls_back (0 or 1) calls before the latest
+  void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat, int calls_back = 0);
 
   double time_op(int B, const std::string& name, int reps);
   void overlap_probe(int B, int reps, double* us);
@@ -74,7 +79,8 @@ class Engine {
   // hb: front -> back hand-off buffer (frame index mod NHB); qp: parity of the back part's
   // quantizer history (frame index mod 2; the back part reads the previous frame's half)
   void build_front(std::vector<Op>& ops, int B, int hb);
-  void build_back(std::vector<Op>& ops, int B, int hb, int qp);
+  // back part over nfr consecutive frames from hand-off buffers hb, hb + 1
+  void build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp);
   hipGraphExec_t part_graph(int part, int B, int hb, int qp);
   void push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r);
   void flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag);
@@ -167,8 +173,21 @@ class Engine {
   // front -> back hand-off per step parity, and the back part's own split-K slabs
   // Up to three hand-off buffers: front(k) writes buffer k % nhb_ and waits only for back(k - nhb_)
   // (nhb_ = 3 lets front and back drift a step apart instead of running in lockstep).
-  static constexpr int NHB = 3;
-  int nhb_ = 3;  // buffers in use
+  // Six hand-off buffers with frame pairs (back_frames = 2): the pair (2j, 2j+1) occupies two
+  // while the fronts of the next four frames fill the others (the front part may run two passes
+  // ahead of the back part).
+  static constexpr int NHB = 6;
+  int nhb_ = 3;  // buffers in use: 3, or 4 with frame pairs
+  int nfr_ = 1;  // frames per back-part pass (ptts_engine_config.back_frames)
+  int rows_hb_[NHB] = {};  // rows of the front part that filled each hand-off buffer
+  // frame-pair mode: PCM of one pair [B][2][1920] per pair parity, and its pinned host copy
+  float* pcmp_[NHB / 2] = {};
+  float* h_pcmp_[NHB / 2] = {};
+  // rows admitted at an odd call under frame pairs start one call later: their SlotState (active)
+  // is written right before the next front part (pinned staging)
+  SlotState* h_act_ = nullptr;
+  std::vector<int> act_slots_;
+  int admit_delay_ = 0;
   // positions the attention ops' algorithmic costs are stated for (plan_names; 0 = a default)
   double plan_ctx_ = 0, plan_win_ = 0;
   float* lat_out_[NHB] = {};
@@ -189,11 +208,13 @@ class Engine {
   // next back part decodes: that back part (stream_be_) waits for this event first
   hipEvent_t ev_admit_ = nullptr;
   hipEvent_t ev_be_tail_ = nullptr;  // stream_be_'s queue at an admission (stream_ waits for it)
+  hipEvent_t ev_act_ = nullptr;      // after the latest start-of-utterance copies from h_act_
   bool admit_pending_ = false;
   void mark_admission();
   long long k_ = 0;          // steps issued
   int out_hb_ = 0;           // hand-off buffer of the frame the last call produced
   int out_rows_ = 0;         // rows that frame covers
+  int prev_hb_ = 0, prev_rows_ = 0;  // the same for the call before (fetch with calls_back = 1)
   int front_rows_ = 0;       // rows of the last front part
   float *temb_ = nullptr, *temb_tmp_ = nullptr;
   float* rope_ = nullptr;  // FlowLM RoPE cos/sin table [max_ctx][32][2]

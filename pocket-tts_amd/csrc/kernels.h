@@ -321,15 +321,19 @@ struct FrontCommitArgs {
 };
 void front_commit(const FrontCommitArgs& a, hipStream_t s);
 
-// Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0.
-// latent [B][32] -> x [B*16][512], h = LN(x); the overlap-add history [B][512] is read from
-// qprev_in and written to qprev_out (frame-parity double buffer; carried over for invalid rows).
-void quant_upsample(const float* latent, int B, const float* emb_std, const float* emb_mean,
-                    const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
-                    const FrameFlags* fl, float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s);
+// Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0, for
+// nfr (1 or 2) consecutive frames of every row: latent[f] [B][32] -> x [B][16 nfr][512] (frame f
+// at rows 16 f..), h = LN(x). The overlap-add history [B][512] is read from qprev_in (frame 0;
+// frame 1 overlaps frame 0) and the last valid frame's quantized row is written to qprev_out
+// (parity double buffer; carried over for rows without a valid frame).
+void quant_upsample(const float* const latent[2], const FrameFlags* const fl[2], int nfr, int B, const float* emb_std,
+                    const float* emb_mean, const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
+                    float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s);
 
 // End of the back part, for rows with a valid frame: copy the last P rows of each conv input
-// into its history, advance the Mimi position.
+// into its history, advance the Mimi position. A launch over nfr frames (T rows per row of a
+// buffer = nfr frames of T / nfr rows) commits through the row's last valid frame: its valid
+// frames are a prefix (an utterance starts at a frame-pair boundary and ends with its last frame).
 struct HistDesc {
   const float* src;  // [B][T][C]
   float* dst;        // [B][P][C]
@@ -339,8 +343,10 @@ struct CommitArgs {
   HistDesc h[10];
   int nh;
   int B;
-  const FrameFlags* flags;
-  int* mpos;  // Mimi decoder positions, += 16
+  const FrameFlags* flags;   // frame 0
+  const FrameFlags* flags1;  // frame 1 (nfr == 2)
+  int nfr;
+  int* mpos;  // Mimi decoder positions, += 16 per committed frame
 };
 void step_commit(const CommitArgs& a, hipStream_t s);
 
@@ -357,9 +363,8 @@ struct ResetArgs {
   const float* bos;
   const SlotState* st_src;
   const int* fpos_src;
-  FrameFlags* flags0;  // every hand-off buffer: an undrained frame of the slot's previous
-  FrameFlags* flags1;  // utterance is discarded
-  FrameFlags* flags2;
+  FrameFlags* flags[6];  // every hand-off buffer: an undrained frame of the slot's previous
+                         // utterance is discarded (null entries skipped)
   SlotState* st;
   int* fpos;
   int* mpos;

@@ -2485,13 +2485,21 @@ void flow_cond(const float* P, int S, int B, const float* bias, const float* tem
 // per wave. The overlap-add history is double-buffered by frame parity (read qprev_in, write
 // qprev_out), so the four workgroups of a row never race on it; a row without a valid frame
 // carries its history over unchanged.
-__global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, const float* emb_std,
-                                                        const float* emb_mean, const float* wq, const float* wup,
-                                                        const float* qprev_in, float* qprev_out, const FrameFlags* fl,
-                                                        float* x, float* h, const float* ln_w, const float* ln_b) {
-  __shared__ float sz[32];
+struct QuantUpArgs {
+  const float* latent[2];
+  const FrameFlags* fl[2];
+  int nfr;
+  const float *emb_std, *emb_mean, *wq, *wup, *qprev_in;
+  float* qprev_out;
+  float *x, *h;
+  const float *ln_w, *ln_b;
+};
+// grid (B, 4 nfr): rows 4 (y % 4).. of frame y / 4 of row b
+__global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
+  __shared__ float sz[2][32];
   __shared__ float sx[4 * 512];
-  const int b = blockIdx.x, r0 = blockIdx.y * 4, tid = threadIdx.x;
+  const int b = blockIdx.x, f = blockIdx.y >> 2, r0 = (blockIdx.y & 3) * 4, tid = threadIdx.x;
+  const int T = 16 * a.nfr;
   // every operand load of the thread's two channels is issued before the arithmetic
   float4 wqr[2][8], wur[2][2];
   float qpv[2];
@@ -2499,30 +2507,38 @@ __global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, con
   for (int u = 0; u < 2; ++u) {
     const int c = tid + 256 * u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) wqr[u][i] = *reinterpret_cast<const float4*>(wq + c * 32 + 4 * i);
-    wur[u][0] = *reinterpret_cast<const float4*>(wup + c * 32 + r0);
-    wur[u][1] = *reinterpret_cast<const float4*>(wup + c * 32 + 16 + r0);
-    qpv[u] = qprev_in[(long)b * 512 + c];
+    for (int i = 0; i < 8; ++i) wqr[u][i] = *reinterpret_cast<const float4*>(a.wq + c * 32 + 4 * i);
+    wur[u][0] = *reinterpret_cast<const float4*>(a.wup + c * 32 + r0);
+    wur[u][1] = *reinterpret_cast<const float4*>(a.wup + c * 32 + 16 + r0);
+    qpv[u] = a.qprev_in[(long)b * 512 + c];
   }
-  if (tid < 32) sz[tid] = latent[b * 32 + tid] * emb_std[tid] + emb_mean[tid];
+  if (tid < 32 * a.nfr) {
+    const int g = tid >> 5, k = tid & 31;
+    sz[g][k] = a.latent[g][b * 32 + k] * a.emb_std[k] + a.emb_mean[k];
+  }
   __syncthreads();
-  const bool upd = fl[b].valid != 0;
+  const bool v0 = a.fl[0][b].valid != 0, v1 = a.nfr > 1 && a.fl[1][b].valid != 0;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = tid + 256 * u;
     const float* wqf = reinterpret_cast<const float*>(wqr[u]);
     const float* w0 = reinterpret_cast<const float*>(&wur[u][0]);
     const float* w1 = reinterpret_cast<const float*>(&wur[u][1]);
-    float q = 0.f;
+    float q[2] = {0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 32; ++k) q += wqf[k] * sz[k];
+    for (int g = 0; g < 2; ++g)
+      if (g < a.nfr) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) q[g] += wqf[k] * sz[g][k];
+      }
+    const float cur = f == 0 ? q[0] : q[1], prev = f == 0 ? qpv[u] : q[0];  // frame 1 overlaps frame 0
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float v = q * w0[r] + qpv[u] * w1[r];
+      const float v = cur * w0[r] + prev * w1[r];
       sx[r * 512 + c] = v;
-      x[((long)b * 16 + r0 + r) * 512 + c] = v;
+      a.x[((long)b * T + 16 * f + r0 + r) * 512 + c] = v;
     }
-    if (blockIdx.y == 0) qprev_out[(long)b * 512 + c] = upd ? q : qpv[u];
+    if (blockIdx.y == 0) a.qprev_out[(long)b * 512 + c] = v1 ? q[1] : (v0 ? q[0] : qpv[u]);
   }
   __syncthreads();
   const int lane = tid & 63, r = tid >> 6;  // one row per wave
@@ -2540,15 +2556,17 @@ __global__ __launch_bounds__(256) void k_quant_upsample(const float* latent, con
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = lane + 64 * i;
-    h[((long)b * 16 + r0 + r) * 512 + n] = (v[i] - mean) / den * ln_w[n] + ln_b[n];
+    a.h[((long)b * T + 16 * f + r0 + r) * 512 + n] = (v[i] - mean) / den * a.ln_w[n] + a.ln_b[n];
   }
 }
 
-void quant_upsample(const float* latent, int B, const float* emb_std, const float* emb_mean, const float* wq,
-                    const float* wup, const float* qprev_in, float* qprev_out, const FrameFlags* fl, float* x,
-                    float* h, const float* ln_w, const float* ln_b, hipStream_t s) {
-  hipLaunchKernelGGL(k_quant_upsample, dim3(B, 4), dim3(256), cap_lds(k_quant_upsample, g_wg_cap), s, latent, emb_std, emb_mean, wq, wup, qprev_in,
-                     qprev_out, fl, x, h, ln_w, ln_b);
+void quant_upsample(const float* const latent[2], const FrameFlags* const fl[2], int nfr, int B, const float* emb_std,
+                    const float* emb_mean, const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
+                    float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s) {
+  if (nfr < 1 || nfr > 2) throw std::runtime_error("quant_upsample: 1 or 2 frames");
+  QuantUpArgs a{{latent[0], nfr > 1 ? latent[1] : latent[0]}, {fl[0], nfr > 1 ? fl[1] : fl[0]}, nfr, emb_std, emb_mean,
+                wq, wup, qprev_in, qprev_out, x, h, ln_w, ln_b};
+  hipLaunchKernelGGL(k_quant_upsample, dim3(B, 4 * nfr), dim3(256), cap_lds(k_quant_upsample, g_wg_cap), s, a);
 }
 
 // =============================================================================================
@@ -2556,16 +2574,18 @@ void quant_upsample(const float* latent, int B, const float* emb_std, const floa
 // =============================================================================================
 __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
   const int b = blockIdx.y;
-  if (!a.flags[b].valid) return;
+  const int nv = !a.flags[b].valid ? 0 : (a.nfr > 1 && a.flags1[b].valid ? 2 : 1);  // valid frames: a prefix
+  if (nv == 0) return;
   if ((int)blockIdx.x < a.nh) {
     const HistDesc& hd = a.h[blockIdx.x];
     const long n = (long)hd.P * hd.C;
-    const float* src = hd.src + ((long)b * hd.T + (hd.T - hd.P)) * hd.C;
+    const int tv = hd.T / a.nfr * nv;  // rows through the last valid frame
+    const float* src = hd.src + ((long)b * hd.T + (tv - hd.P)) * hd.C;
     float* dst = hd.dst + (long)b * n;
     for (long e = threadIdx.x; e < n; e += 256) dst[e] = src[e];
     return;
   }
-  if (threadIdx.x == 0) a.mpos[b] += 16;
+  if (threadIdx.x == 0) a.mpos[b] += 16 * nv;
 }
 
 // one 64-thread block per row
@@ -2617,9 +2637,8 @@ __global__ __launch_bounds__(256) void k_slot_reset(ResetArgs a) {
     a.st[slot] = a.st_src[i];
     a.fpos[slot] = a.fpos_src[i];
     a.mpos[slot] = 0;
-    a.flags0[slot] = FrameFlags{0, 0};
-    a.flags1[slot] = FrameFlags{0, 0};
-    a.flags2[slot] = FrameFlags{0, 0};
+    for (int q = 0; q < 6; ++q)
+      if (a.flags[q]) a.flags[q][slot] = FrameFlags{0, 0};
   }
 }
 

@@ -18,7 +18,7 @@ LDIM = 32
 DIM = 1024
 SAMPLE_RATE = 24000
 QUANT_NONE, QUANT_FLOW_LM, QUANT_ALL = 0, 1, 2
-ABI_VERSION = 3  # PTTS_ABI_VERSION of include/pocket_tts.h that the structs below mirror
+ABI_VERSION = 4  # PTTS_ABI_VERSION of include/pocket_tts.h that the structs below mirror
 
 F32P = C.POINTER(C.c_float)
 U8P = C.POINTER(C.c_uint8)
@@ -39,6 +39,7 @@ class EngineConfig(C.Structure):
         ("weight_quant", C.c_int),
         ("fp8_gemm", C.c_int),
         ("cfg_yaml", C.c_char_p),
+        ("back_frames", C.c_int),
     ]
 
 
@@ -88,6 +89,8 @@ SIGNATURES = [
     ("ptts_step_async", C.c_int, [C.c_void_p, C.c_int]),
     ("ptts_sync", C.c_int, [C.c_void_p]),
     ("ptts_fetch", C.c_int, [C.c_void_p, C.c_int, F32P, U8P, U8P, F32P, F32P]),
+    ("ptts_frame_lag", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    ("ptts_fetch_prev", C.c_int, [C.c_void_p, C.c_int, C.c_int, F32P, U8P, U8P, F32P, F32P]),
     ("ptts_slot_set_latent", C.c_int, [C.c_void_p, C.c_int, F32P]),
     ("ptts_decode_latents", C.c_int, [C.c_void_p, C.c_int, F32P, C.c_int, F32P, F32P, F32P, F32P]),
     ("ptts_generate", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, I32P, C.c_int, C.POINTER(GenParams), F32P, C.c_int,

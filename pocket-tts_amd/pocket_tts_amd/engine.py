@@ -68,17 +68,19 @@ class Engine:
     def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
                  seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
                  defer_weights: bool = False, pipeline: bool = False, weight_quant: int = 0, fp8_gemm: bool = False,
-                 cfg_yaml: str | None = None):
+                 cfg_yaml: str | None = None, back_frames: int = 1):
         """pipeline=True: overlapped stepping, each step() returns the frame produced by the
         previous call (see ptts_engine_config.pipeline). weight_quant: QUANT_NONE / QUANT_FLOW_LM /
         QUANT_ALL, the reference's simulated int8 weight quantization (quantize.rs), with the
         FlowLM step GEMMs streaming int8 codes. fp8_gemm=True: the large FlowLM step GEMMs run as
         fp8 W8A8 MFMA (accuracy-gated; see ptts_engine_config.fp8_gemm). cfg_yaml: the reference's
-        model config (config/b6369a24.yaml), checked against the compiled dimensions."""
+        model config (config/b6369a24.yaml), checked against the compiled dimensions.
+        back_frames=2 (pipelined only): two frames per Mimi-decode pass; a step() returns the frame
+        computed three calls earlier (`frame_lag`)."""
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
                            weight_blob or None, int(defer_weights), int(pipeline), int(weight_quant),
-                           int(fp8_gemm), cfg_yaml.encode() if cfg_yaml else None)
+                           int(fp8_gemm), cfg_yaml.encode() if cfg_yaml else None, int(back_frames))
         h = C.c_void_p()
         check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
         self.handle = h
@@ -87,6 +89,14 @@ class Engine:
         self.max_ctx = max_ctx
         self.lsd_decode_steps = lsd_decode_steps
         self.pipeline = bool(pipeline)
+        self.back_frames = int(back_frames) if pipeline else 1
+
+    def frame_lag(self) -> tuple[int, int]:
+        """(lag, admit_delay): a frame arrives `lag` calls after the call that computed it; the
+        rows of the latest admission start `admit_delay` calls late (ptts_frame_lag)."""
+        d = C.c_int(0)
+        lag = int(lib().ptts_frame_lag(self.handle, C.byref(d)))
+        return lag, int(d.value)
 
     @staticmethod
     def check_config(cfg_yaml: str) -> None:
@@ -236,11 +246,13 @@ class Engine:
     def sync(self):
         check(lib().ptts_sync(self.handle))
 
-    def fetch(self, n_rows: int) -> StepResult:
-        r = StepResult(np.zeros((n_rows, FRAME), np.float32), np.zeros(n_rows, np.uint8), np.zeros(n_rows, np.uint8),
+    def fetch(self, n_rows: int, calls_back: int = 0) -> StepResult:
+        """Outputs of the latest call (calls_back = 0) or of the call before it (1: a driver that
+        keeps one call in flight)."""
+        r = StepResult(np.empty((n_rows, FRAME), np.float32), np.zeros(n_rows, np.uint8), np.zeros(n_rows, np.uint8),
                        np.zeros(n_rows, np.float32), np.zeros((n_rows, LDIM), np.float32))
-        check(lib().ptts_fetch(self.handle, n_rows, fptr(r.pcm), u8ptr(r.valid), u8ptr(r.last), fptr(r.eos_logits),
-                               fptr(r.latents)))
+        check(lib().ptts_fetch_prev(self.handle, calls_back, n_rows, fptr(r.pcm), u8ptr(r.valid), u8ptr(r.last),
+                                    fptr(r.eos_logits), fptr(r.latents)))
         r.valid = r.valid.astype(bool)
         r.last = r.last.astype(bool)
         return r

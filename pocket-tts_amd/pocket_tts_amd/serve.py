@@ -241,14 +241,16 @@ class BatchScheduler:
         return done
 
     def _loop(self):
-        # step k is launched (step_async) before the frames of step k-1 are handed out, so the
-        # host-side delivery overlaps the GPU; a finished row is released one step later (its
-        # extra step is computed and discarded: frame_valid = 0)
-        pending = None
+        # One call in flight: call k+1 is issued (step_async) before the frames of call k are
+        # fetched and handed out, so the GPU always has the next step queued while this thread
+        # waits for the GIL (the HTTP event loop shares it) and delivers frames. A finished row is
+        # released when its last frame is delivered (later calls compute it as inactive:
+        # frame_valid = 0).
+        issued: deque[int] = deque()  # rows of the calls issued and not fetched yet (<= 2)
         try:
             while True:
                 with self.cv:
-                    while self.running and not self.waiting and not self.active and pending is None:
+                    while self.running and not self.waiting and not self.active and not issued:
                         self.cv.wait()
                     if not self.running:
                         break
@@ -258,16 +260,15 @@ class BatchScheduler:
                     self._admit(batch)
                 if rows:
                     self.engine.step_async(rows)
-                if pending is not None:
-                    done = self._deliver(*pending)
-                    with self.cv:
-                        for slot in done:
-                            del self.active[slot]
-                    pending = None
-                if rows:  # fetch waits for this call's frame only (a pipelined engine's next
-                    # front part keeps running; a sync() here drained the pipeline every step)
-                    pending = (self.engine.fetch(rows), rows)
+                    issued.append(rows)
                     self.steps += 1
+                if len(issued) == 2 or (issued and not rows):
+                    res = self.engine.fetch(issued[0], calls_back=len(issued) - 1)
+                    done = self._deliver(res, issued.popleft())
+                    if done:
+                        with self.cv:
+                            for slot in done:
+                                del self.active[slot]
         except BaseException as e:  # deliver the failure to every waiting client
             with self.cv:
                 self.running = False
@@ -518,6 +519,7 @@ class StandInEngine:
                 if last[s]:
                     del self.rows[s]
         prev, self.pending = self.pending, (pcm, valid, last)
+        self.prev_out = getattr(self, "out", None)
         self.out = (np.zeros((n, FRAME), np.float32), np.zeros(n, bool), np.zeros(n, bool))
         if prev is not None:  # the previous call's frame, over this call's rows
             m = min(n, prev[1].size)
@@ -527,10 +529,11 @@ class StandInEngine:
     def sync(self):
         pass
 
-    def fetch(self, n):
+    def fetch(self, n, calls_back=0):
         from types import SimpleNamespace
 
-        return SimpleNamespace(pcm=self.out[0], valid=self.out[1], last=self.out[2])
+        out = self.out if calls_back == 0 else self.prev_out
+        return SimpleNamespace(pcm=out[0], valid=out[1], last=out[2])
 
     def close(self):
         pass

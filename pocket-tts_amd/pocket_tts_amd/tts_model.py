@@ -162,15 +162,16 @@ class TTSModel:
         if self.lsd_decode_steps != self.engine.lsd_decode_steps:
             raise ValueError("lsd_decode_steps is fixed at engine creation")
         self.engine.open(0, voice_state, ids, self._params(max_frames, frames_after_eos))
-        first = True
+        lag, delay = self.engine.frame_lag()  # overlapped stepping: frames arrive lag (+ delay) calls late
+        lead = lag + delay
         while True:
             r = self.engine.step(1)
             if not r.valid[0]:
-                if first and self.engine.pipeline:  # overlapped stepping: frames arrive one call late
-                    first = False
+                if lead > 0:
+                    lead -= 1
                     continue
                 return
-            first = False
+            lead = 0
             yield r.pcm[0].reshape(1, 1, FRAME).copy()
             if r.last[0]:
                 return

@@ -1,6 +1,6 @@
 """GPU parity at the benchmark's own shape (BASELINE configs[2]): f32 engine, 32 rows, 125-frame
-voice prompts, 40 text tokens, 132 free-running frames at temperature 0, pipelined stepping (the
-bench's mode). The FlowLM context of every row grows 165 -> 297 positions, so the step attention
+voice prompts, 40 text tokens, 132 free-running frames at temperature 0, pipelined stepping with
+frame pairs (the bench's mode: one Mimi decode pass per two frames) and with one frame per pass. The FlowLM context of every row grows 165 -> 297 positions, so the step attention
 (k_attn_decode_qkv) takes its second 256-key round for the last 40 frames, and the Mimi decoder's
 250-key window slides over 2,112 ring positions (four wraps of the 512-slot ring).
 
@@ -54,6 +54,30 @@ def _oracle_run(oracle, prompt, ids, n):
     return out
 
 
+def _engine_frames(pt, inputs, back_frames):
+    eng = pt.Engine(device=0, max_slots=B, max_ctx=320, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
+                    back_frames=back_frames)
+    try:
+        voices = [eng.voice_from_prompt(p) for p, _ in inputs]
+        params = pt.GenerationParams(temp=0.0, eos_threshold=float("inf"), frames_after_eos=3,
+                                     max_frames=FRAMES, seed=1)
+        eng.open_many(list(range(B)), voices, [i for _, i in inputs], [params] * B)
+        lag, delay = eng.frame_lag()
+        assert (lag, delay) == ((3, 0) if back_frames == 2 else (1, 0))
+        frames = []
+        for _ in range(lag + delay):  # pipelined: the first calls return no frame
+            assert not eng.step(B).valid.any()
+        for i in range(FRAMES):
+            r = eng.step(B)
+            assert r.valid.all(), i
+            assert bool(r.last.all()) == (i == FRAMES - 1) and not (r.last.any() and i < FRAMES - 1), i
+            frames.append([(float(r.eos_logits[b]), r.latents[b].copy(), r.pcm[b].copy()) for b in range(B)])
+        assert not eng.step(B).valid.any()
+        return frames
+    finally:
+        eng.close()
+
+
 def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
     import pocket_tts_amd as pt
 
@@ -62,23 +86,7 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
     workers = max(1, min(16, len(os.sched_getaffinity(0))))
     with ThreadPoolExecutor(workers) as ex:  # the oracle runs free (temp 0): precompute them
         futs = {b: ex.submit(_oracle_run, oracle, *inputs[b], FRAMES) for b in range(B)}
-        eng = pt.Engine(device=0, max_slots=B, max_ctx=320, lsd_decode_steps=1, seed=0x5EED, pipeline=True)
-        try:
-            voices = [eng.voice_from_prompt(p) for p, _ in inputs]
-            params = pt.GenerationParams(temp=0.0, eos_threshold=float("inf"), frames_after_eos=3,
-                                         max_frames=FRAMES, seed=1)
-            eng.open_many(list(range(B)), voices, [i for _, i in inputs], [params] * B)
-            frames = []
-            r = eng.step(B)
-            assert not r.valid.any()  # pipelined: the first call returns no frame
-            for i in range(FRAMES):
-                r = eng.step(B)
-                assert r.valid.all(), i
-                assert bool(r.last.all()) == (i == FRAMES - 1) and not (r.last.any() and i < FRAMES - 1), i
-                frames.append([(float(r.eos_logits[b]), r.latents[b].copy(), r.pcm[b].copy()) for b in range(B)])
-            assert not eng.step(B).valid.any()
-        finally:
-            eng.close()
+        runs = {bf: _engine_frames(pt, inputs, bf) for bf in (2, 1)}
         ref = {b: f.result() for b, f in futs.items()}
 
     worst = {"golden": [0.0, 0.0, 0.0], "oracle": [0.0, 0.0, 0.0]}
@@ -88,9 +96,10 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
         worst[kind] = [max(a, b) for a, b in zip(worst[kind], e)]
         assert e[0] <= LAT_TOL and e[1] <= LAT_TOL and e[2] <= PCM_TOL, (kind, where, e)
 
-    for i in range(FRAMES):
-        for b in range(B):
-            cmp("oracle", frames[i][b], ref[b][i], (i, b))
-        if i < d["latent"].shape[0]:
-            cmp("golden", frames[i][0], (d["eos_logit"][i], d["latent"][i], d["pcm"][i]), (i, 0))
-    print(f"worst |d| eos/latent/pcm: vs golden {worst['golden']}, vs oracle {worst['oracle']}")
+    for bf, frames in runs.items():
+        for i in range(FRAMES):
+            for b in range(B):
+                cmp("oracle", frames[i][b], ref[b][i], (bf, i, b))
+            if i < d["latent"].shape[0]:
+                cmp("golden", frames[i][0], (d["eos_logit"][i], d["latent"][i], d["pcm"][i]), (bf, i, 0))
+        print(f"back_frames={bf}: worst |d| eos/latent/pcm: vs golden {worst['golden']}, vs oracle {worst['oracle']}")

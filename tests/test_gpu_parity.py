@@ -227,10 +227,8 @@ def test_generate_convenience(gpu_engine):
 
 def test_plan_and_kernel_timer(gpu_engine):
     names = gpu_engine.plan_ops(8)
-    # B <= 32: the six FlowLM layers are one persistent launch (k_flow_lm)
-    assert "flow.layers" in names and "flow.l0.qkv_gemm" not in names
-    assert "seanet.conv0" in names and names[-1] == "commit"
-    assert gpu_engine.time_kernel(8, "flow.layers", reps=5) > 0
+    assert "flow.l0.qkv_gemm" in names and "seanet.conv0" in names and names[-1] == "commit"
+    assert gpu_engine.time_kernel(8, "flow.l0.ff1_gemm", reps=5) > 0
 
 
 def test_pipelined_stepping_matches_oracle(oracle):
@@ -288,6 +286,67 @@ def test_pipelined_stepping_matches_oracle(oracle):
         eng.close()
 
 
+def test_frame_pairs_continuous_batching_matches_oracle(oracle):
+    """back_frames=2: one Mimi decode pass per two frames, a call returns the frame computed three
+    calls earlier. Rows admitted at an even call, rows admitted at an odd call (they start one call
+    later, so that an utterance's frames pair up from its first), a row whose utterance ends on the
+    first frame of a pair (odd length: the pass commits its codec state through that frame only)
+    and a row re-admitted after it finished must all equal their oracle runs frame for frame."""
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    rng = np.random.default_rng(7)
+    eng = pt.Engine(device=0, max_slots=4, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
+                    back_frames=2)
+    try:
+        orc, lat, got, want = {}, {}, {}, {}
+
+        def admit(slots, n_frames):
+            ids_l, vs = [], []
+            for b in slots:
+                F = 6 + 2 * b
+                prompt = (d["prompt"][:F] * (1.0 + 0.05 * b)).astype(np.float32)
+                ids = rng.integers(0, 4000, size=4 + 3 * b).astype(np.int32)
+                vs.append(eng.voice_from_prompt(prompt))
+                ids_l.append(ids)
+                s = oracle.new_state(256)
+                s.prefill(prompt)
+                s.prefill_tokens(ids)
+                orc[b], lat[b], got[b], want[b] = s, None, 0, n_frames
+            eng.open_many(slots, vs, ids_l, [params(max_frames=n_frames)] * len(slots))
+            return eng.frame_lag()
+
+        def step_check():
+            r = eng.step(4)
+            for b in list(orc):
+                if not r.valid[b]:
+                    continue
+                o = orc[b].step(lat[b])
+                lat[b] = o["latent"]
+                got[b] += 1
+                assert got[b] <= want[b], b
+                assert bool(r.last[b]) == (got[b] == want[b]), (b, got[b])
+                assert abs(r.eos_logits[b] - o["eos_logit"]) <= LAT_TOL
+                np.testing.assert_allclose(r.latents[b], o["latent"], atol=LAT_TOL)
+                assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL
+            return r
+
+        assert admit([0, 1], 5) == (3, 0)  # call 0 (even); row 0/1 end on the first frame of a pair
+        for _ in range(3):
+            assert not step_check().valid.any()
+        assert admit([2, 3], 4) == (3, 1)  # before call 3 (odd): rows 2/3 start at call 4
+        for _ in range(6):
+            step_check()
+        assert got[0] == 5 and got[1] == 5  # frames 0..4 of rows 0/1 arrived by call 7
+        admit([0], 3)  # re-admission of a finished row (call 9: odd)
+        for _ in range(12):
+            step_check()
+        assert got[0] == 3 and got[2] == 4 and got[3] == 4
+        assert not eng.step(4).valid.any()
+    finally:
+        eng.close()
+
+
 def test_long_utterance_wraps_mimi_ring(gpu_engine, oracle):
     """70 frames: the Mimi decoder ring (512 positions = 32 frames) wraps twice and the 250-key
     window slides across the wrap; the FlowLM cache grows to voice + text + 70 positions. Every
@@ -313,7 +372,8 @@ def test_long_utterance_wraps_mimi_ring(gpu_engine, oracle):
     assert worst <= PCM_TOL, worst
 
 
-def test_batch_scheduler_matches_oracle(oracle):
+@pytest.mark.parametrize("back_frames", [1, 2])
+def test_batch_scheduler_matches_oracle(oracle, back_frames):
     """Serving front end (f1) on the real pipelined engine: 6 requests of different lengths through
     3 slots (continuous admission into recycled slots); every request's audio equals its own
     oracle run."""
@@ -321,7 +381,8 @@ def test_batch_scheduler_matches_oracle(oracle):
     from pocket_tts_amd.serve import BatchScheduler
 
     d = load_golden("e2e_lsd1.safetensors")
-    eng = pt.Engine(device=0, max_slots=3, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True)
+    eng = pt.Engine(device=0, max_slots=3, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
+                    back_frames=back_frames)
     sch = BatchScheduler(eng)
     try:
         rng = np.random.default_rng(3)

@@ -40,13 +40,14 @@ class SentenceTokenizer:
         return 40
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
-def test_streaming_matches_batch_over_multiple_chunks(oracle, pipeline):
+@pytest.mark.parametrize("pipeline,back_frames", [(False, 1), (True, 1), (True, 2)])
+def test_streaming_matches_batch_over_multiple_chunks(oracle, pipeline, back_frames):
     import pocket_tts_amd as pt
     from pocket_tts_amd.text import prepare_text_prompt
 
     tok = SentenceTokenizer(synthetic_tokenizer())
-    eng = pt.Engine(device=0, max_slots=1, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=pipeline)
+    eng = pt.Engine(device=0, max_slots=1, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=pipeline,
+                    back_frames=back_frames)
     try:
         m = pt.TTSModel(eng, temp=0.0, lsd_decode_steps=1, eos_threshold=float("inf"), noise_clamp=None, tokenizer=tok)
         prompt = (0.11 * np.random.default_rng(11).standard_normal((8, 1024))).astype(np.float32)
@@ -74,6 +75,6 @@ def test_streaming_matches_batch_over_multiple_chunks(oracle, pipeline):
                 e = float(np.abs(stream[c * FRAMES + i][0, 0] - ref["pcm"]).max())
                 worst = max(worst, e)
                 assert e <= PCM_TOL, (c, i, e)
-        print(f"pipeline={pipeline}: worst PCM |d| vs oracle {worst:.3g}")
+        print(f"pipeline={pipeline} back_frames={back_frames}: worst PCM |d| vs oracle {worst:.3g}")
     finally:
         eng.close()

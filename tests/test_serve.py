@@ -59,15 +59,15 @@ class FakeEngine:
         r.pcm[:m], r.valid[:m], r.last[:m] = prev["pcm"][:m], prev["valid"][:m], prev["last"][:m]
         return r
 
-    # split form of step() (ptts_step_async / ptts_sync / ptts_fetch), used by the scheduler
+    # split form of step() (ptts_step_async / ptts_sync / ptts_fetch[_prev]), used by the scheduler
     def step_async(self, n):
-        self._issued = (self.step(n), n)
+        self._issued = getattr(self, "_issued", [])[-1:] + [(self.step(n), n)]
 
     def sync(self):
         pass
 
-    def fetch(self, n):
-        r, m = self._issued
+    def fetch(self, n, calls_back=0):
+        r, m = self._issued[-1 - calls_back]
         assert m == n
         return r
 

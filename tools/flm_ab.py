@@ -1,4 +1,4 @@
-"""A/B of the persistent FlowLM launch (k_flow_lm) against the 48-launch form (PTTS_FLM_OFF, probe
+"""A/B of the persistent FlowLM launch (k_flow_lm) against the 48-launch form (without PTTS_FLM_ON, probe
 build: PTTS_LIB=pocket-tts_amd/lib-probes/libpocket_tts_hip.so): steady step time of pipelined and
 sequential engines at B = 32 and of a sequential B = 1 engine (the first-chunk path), medians of
 REPS alternating rounds."""
@@ -14,9 +14,9 @@ import pocket_tts_amd as pt  # noqa: E402
 
 def step_us(B, pipeline, off, n=60):
     if off:
-        os.environ["PTTS_FLM_OFF"] = "1"
+        os.environ.pop("PTTS_FLM_ON", None)
     else:
-        os.environ.pop("PTTS_FLM_OFF", None)
+        os.environ["PTTS_FLM_ON"] = "1"
     eng = pt.Engine(device=0, max_slots=B, max_ctx=320, seed=0x5EED, pipeline=pipeline)
     rng = np.random.default_rng(0)
     v = eng.voice_from_prompt((0.11 * rng.standard_normal((125, 1024))).astype(np.float32))

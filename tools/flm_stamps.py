@@ -10,6 +10,7 @@ import torch
 
 buf = torch.zeros(3 * 128, dtype=torch.int64, device="cuda:0")
 os.environ["PTTS_FLM_DBG"] = str(buf.data_ptr())
+os.environ["PTTS_FLM_ON"] = "1"
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "pocket-tts_amd"))
 import numpy as np  # noqa: E402
 
