@@ -297,7 +297,8 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
 // the qkv / linear1 versions on any tile slow the concurrent back part more than they gain.
 void Engine::derive_gemv() {
   // sequential stepping (the B = 1 first-chunk path, no concurrent back part): every matrix
-  const int mask = pipeline_ ? 2 | 8 | 16 : 31;
+  int mask = pipeline_ ? 2 | 8 | 16 : 31;
+  if (probe_env("PTTS_GEMV_MASK")) mask = atoi(probe_env("PTTS_GEMV_MASK"));  // probe builds: A/B runs
   gemv_mask_ = mask;
   struct M {
     const float* w;

@@ -29,12 +29,15 @@
 // GEMM units are those of k_gemv (kernels.hip): 4 waves split the unit's K slice, each a
 // v_mfma_f32_32x32x2f32 chain over its fragment, the 4 partials summed through LDS in wave order.
 // Split-K partials are summed by their consumers in slice order: deterministic results.
+// Measured slower than the launches it replaces, so it is compiled only into the
+// -DPTTS_PROBES measurement build; the product library carries the stubs at the end of this file.
 #include <stdexcept>
 
 #include "devfn.h"
 #include "kernels.h"
 
 namespace ptts {
+#ifdef PTTS_PROBES
 namespace {
 
 constexpr int D = 1024, NH = 16, FF = 4096, NL = FL_NL, GRID = 256, ROWS = 32;
@@ -453,5 +456,12 @@ void flow_lm(const FlowLmArgs& a, hipStream_t s) {
   if (!flow_lm_fits(a.B)) throw std::runtime_error("flow_lm: B out of range");
   hipLaunchKernelGGL(k_flow_lm, dim3(GRID), dim3(256), 0, s, a);
 }
+#else   // product build: no persistent FlowLM launch (Engine::use_flow_lm never selects it)
+bool flow_lm_fits(int) { return false; }
+size_t flow_lm_set_floats() { return 0; }
+int flow_lm_grid() { return 0; }
+int flow_lm_max_resident(int) { return 0; }
+void flow_lm(const FlowLmArgs&, hipStream_t) { throw std::runtime_error("flow_lm: probe builds only"); }
+#endif
 
 }  // namespace ptts
