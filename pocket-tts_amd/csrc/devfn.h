@@ -11,6 +11,24 @@ namespace ptts {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Issue priority of a front-part wave (s_setprio) where front (FlowLM / flow-head) and back (Mimi
+// decode) waves share a SIMD: probe builds only (PTTS_FRONT_PRIO, set_front_prio; s_setprio
+// takes an immediate). Measured: with frame pairs, priority 3 took the steady
+// step from 0.602 to 0.580 ms, but with one frame per pass (the back part bounds the step) it
+// cost 5 % (0.583 -> 0.613 ms), and pairs + priority beat the product's one-frame passes by
+// 0.5 % only (same-box A/B, tools/bf_ab.sh): not adopted.
+#ifdef PTTS_PROBES
+extern __device__ int g_front_prio;
+__device__ __forceinline__ void front_prio() {
+  const int p = __builtin_amdgcn_readfirstlane(g_front_prio);
+  if (p >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+}
+#else
+__device__ __forceinline__ void front_prio() {}
+#endif
+
 __device__ __forceinline__ float gelu_tanh(float x) {
   // candle Tensor::gelu (tanh approximation), transformer.rs:85
   return 0.5f * x * (1.0f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));

@@ -166,6 +166,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   // it: steady step 0.6370 -> 0.6321 ms (medians of 4; when the front was the longer part, 3
   // buffers measured 0.5% slower).
   if (probe_env("PTTS_BACK_WG_CAP")) back_cap_ = atoi(probe_env("PTTS_BACK_WG_CAP"));
+  if (probe_env("PTTS_FRONT_PRIO")) set_front_prio(atoi(probe_env("PTTS_FRONT_PRIO")));
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
   mods_ = dalloc((size_t)lsd_ * B * NADA);
   xf_ = dalloc((size_t)B * FD);
@@ -591,6 +592,7 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   // FlowLM / flow-head step weights are read once per step: non-temporal loads on the LDS-DMA
   // tiles (step -1.1 %; the 32x32 register tile keeps default-policy loads)
   a.w_nt = M <= 64 && layout != 0;
+  a.front = 1;  // FlowLM / flow-head GEMMs (and the prefill passes, on the same stream)
   ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
                  (w8 || wf8 ? (double)N * K + 4.0 * N : 4.0 * N * K) + 4.0 * ((double)M * K + (double)S * M * N)});
   *S_out = S;
@@ -617,7 +619,9 @@ static Op rr_op(const std::string& name, const RowReduceArgs& a) {
 // combine by the last-arriving workgroup measured slower on every front GEMM: ff2 43 vs 13 us with
 // the LayerNorm row finisher, ff1 15.6 vs 11.4 us tile-local).
 void Engine::push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r) {
-  ops.push_back(rr_op(name, r));
+  RowReduceArgs a = r;
+  a.front = 1;  // the FlowLM / flow-head reduces (the back part's go through rr_op directly)
+  ops.push_back(rr_op(name, a));
 }
 
 void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float* X, int M, const float* Wt, int N,

@@ -61,6 +61,7 @@ struct RowReduceArgs {
   const float *x0_cur, *x0_w, *x0_b;
   float* x0_hx;
   int x0_B;
+  int front;  // 1: a launch of the front part (issue priority, set_front_prio)
 };
 struct GemmArgs {
   int mode;    // 0 dense, 1 conv
@@ -91,6 +92,8 @@ struct GemmArgs {
   int max_wg_per_cu;
   // 1: the weight stream is read with non-temporal loads (once-read FlowLM step weights)
   int w_nt;
+  // 1: a launch of the front part (FlowLM / flow head): its waves take the front issue priority
+  int front;
   // measurement probe, -DPTTS_PROBES builds only (tools/; PTTS_BACK_PROBE: back-part launches of a
   // pipelined step, PTTS_FRONT_PROBE: all other tiled launches; results are wrong): bit 0 skips
   // the MFMAs, bit 1 the operand loads of the K loop. Ignored by product builds.
@@ -253,6 +256,9 @@ struct FlowHeadArgs {
 // Launches issued while a cap > 0 is set reserve dynamic LDS so that at most `cap` workgroups of
 // each kernel share a CU (0 = no cap). Per host thread; the engine sets it around graph capture.
 void set_wg_cap(int cap);
+// Issue priority of the front part's waves (s_setprio 0..3) when they share a SIMD with back-part
+// waves: probe builds only (PTTS_FRONT_PRIO), for A/B runs; a no-op in product builds.
+void set_front_prio(int prio);
 // conv operand rows as an explicit [B * T_in / stride][taps * cin] matrix (cin % 4 == 0)
 void im2col(const float* X, const float* H, int B, int T_in, int stride, int P, int cin, int taps, float* A,
             hipStream_t s);

@@ -30,6 +30,15 @@ namespace ptts {
 // Per host thread: engines of one process (serve --gpus N threads) capture graphs concurrently.
 static thread_local int g_wg_cap = 0;
 void set_wg_cap(int cap) { g_wg_cap = cap; }
+#ifdef PTTS_PROBES
+__device__ int g_front_prio = 0;
+void set_front_prio(int prio) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_front_prio), &prio, sizeof prio) != hipSuccess)
+    throw std::runtime_error("set_front_prio failed");
+}
+#else
+void set_front_prio(int) {}  // product builds: no front priority
+#endif
 template <typename K>
 static size_t cap_lds(K kernel, int cap) {
   if (cap <= 0) return 0;
@@ -192,6 +201,7 @@ struct Lay {
 
 template <int MODE, int LAYOUT>
 __global__ __launch_bounds__(64 * Lay<LAYOUT>::NW) void k_gemm(GemmArgs a) {
+  if (a.front) front_prio();
   constexpr bool KS = Lay<LAYOUT>::KSPLIT;
   constexpr int NW = Lay<LAYOUT>::NW;
   __shared__ float red[KS ? NW * 16 * 64 : 1];
@@ -590,6 +600,7 @@ __device__ __forceinline__ unsigned lds_addr(const float* p) {
 // of its 64 issue cycles free, so the DMA issue (60-185 cycles each) hides behind the matrix pipe.
 template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1, int MINB = 1, bool ILV = false>
 __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
+  if (a.front) front_prio();
   constexpr int TM = 32 * WM * TMW, TN = 32 * WN * TNW, ROWS = TM + TN;
   constexpr int CPR = BK / 4;        // 16-byte columns per LDS row
   constexpr int RPI = 64 / CPR;      // rows per 1-KiB wave instruction
@@ -1521,6 +1532,7 @@ __global__ void k_pack_gemv(const float* __restrict__ W, int N, int K, int wn, i
 template <int WN, int KW>
 __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long ldx, int M, int N,
                                               const float* __restrict__ P, float* __restrict__ partial) {
+  front_prio();
   constexpr int WK = 4 / WN, KS = KW * WK, NV = KW / 8, LDA = KS + 4;  // +4: conflict-free b128 rows
   __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
   __shared__ __attribute__((aligned(16))) float red[WK > 1 ? 4 * 16 * 64 : 1];
@@ -1727,6 +1739,7 @@ void flow_head_x0(const float* cur, const float* w_t, const float* bias, float* 
 
 template <int SMAX>
 __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
+  if (a.front) front_prio();
   __shared__ float sh[4];
   if (a.fill) {
     const long nthr = (long)gridDim.x * gridDim.y * 256;
@@ -2221,6 +2234,7 @@ template <int NW, int KQ, bool NT = false>
 __global__ __launch_bounds__(64 * NW) void k_attn_decode_qkv(const float* __restrict__ P, int S, int M, int nh, RowMap mp,
                                                          KvStore kv, const float* __restrict__ rope,
                                                          float* __restrict__ O) {
+  front_prio();
   constexpr int BLK = 4 * KQ * NW;  // keys per round: NW waves x KQ loads of 4 keys
   __shared__ float s_m[NW], s_l[NW];
   __shared__ __attribute__((aligned(16))) float s_o[NW][64];
@@ -2419,6 +2433,7 @@ __device__ float normal_at(unsigned long long seed, int step, int k, int attempt
 __global__ __launch_bounds__(256) void k_flow_cond(const float* P, int S, int B, const float* bias, const float* temb,
                                                    int lsd, const SlotState* st, float* ysilu, float* cur,
                                                    float* eos_out) {
+  front_prio();
   const int b = blockIdx.x, tid = threadIdx.x;
   const int NC = 513;  // cond_embed (512) | out_eos (1)
   // every load of the thread first (its two columns' slabs, thread 0's EOS slabs, the slot
@@ -2590,6 +2605,7 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
 
 // one 64-thread block per row
 __global__ __launch_bounds__(64) void k_front_commit(FrontCommitArgs a) {
+  front_prio();
   const int b = blockIdx.x, t = threadIdx.x;
   SlotState& ss = a.st[b];
   const int valid = ss.active;
@@ -3139,6 +3155,7 @@ struct FhOps {
 };
 
 __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
+  front_prio();
   __shared__ float s_st[2][FH_WAVES][16];
   __shared__ __attribute__((aligned(16))) float s_red2[2][FH_WAVES][16][16];
   __shared__ __attribute__((aligned(16))) float s_ln[FH_DEPTH][2][FH_D];  // ResBlock LayerNorm affines
@@ -3321,6 +3338,7 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
 __global__ __launch_bounds__(256) void k_input_ln(const float* __restrict__ lat, const float* __restrict__ Wt,
                                                   const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                   float* __restrict__ x, float* __restrict__ h) {
+  front_prio();
   __shared__ float sh[4];
   const int m = blockIdx.x, n = 4 * threadIdx.x;  // N = 1024
   float4 lv[8];
