@@ -112,6 +112,7 @@ struct GemmArgs {
   int* tickets;
   int tickets_cap;
   int tail_full, tiles_n;  // set by gemm()
+  int tiles_m, units_z;    // persistent tiles (layout 40): tile grid rows and z units, set by gemm()
   // epilogue (S == 1)
   const float* bias;
   int act;
