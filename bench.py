@@ -218,9 +218,9 @@ def main():
     ap.add_argument("--no-op-times", action="store_true", help="skip the per-op HIP-event pass (PMC runs)")
     ap.add_argument("--no-quant-variant", action="store_true",
                     help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM) and fp8_gemm engines")
-    ap.add_argument("--back-frames", type=int, default=1, choices=(1, 2),
+    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2),
                     help="frames per Mimi-decode pass of pipelined stepping (ptts_engine_config.back_frames; "
-                         "2 measured slower: 0.600 vs 0.588 ms per step, DESIGN.md section 4)")
+                         "2, the throughput configuration: 0.559 vs 0.584 ms per steady step, DESIGN.md section 1)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sequential stepping (no FlowLM / Mimi overlap across consecutive frames)")
     ap.add_argument("--profile-frames", type=int, default=0,

@@ -297,8 +297,13 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
 // pipelined step only out + linear2 + adaLN pay (steady step 0.6595 -> 0.6326 ms, medians of 3):
 // the qkv / linear1 versions on any tile slow the concurrent back part more than they gain.
 void Engine::derive_gemv() {
-  // sequential stepping (the B = 1 first-chunk path, no concurrent back part): every matrix
-  int mask = pipeline_ ? 2 | 8 | 16 : 31;
+  // sequential stepping (the B = 1 first-chunk path, no concurrent back part) and frame-pair
+  // pipelined stepping (the front part bounds the step): every matrix. Single-frame pipelined
+  // stepping (the back part bounds it): qkv and linear1 stay on the LDS-DMA tile, whose smaller
+  // register footprint crowds the concurrent back part less (same-box product bench,
+  // tools/gpu_gemv_ab.sh: pairs 4,093 -> 4,395x with every matrix register-resident, single
+  // frames 4,228 -> 4,170x)
+  int mask = pipeline_ && nfr_ == 1 ? 2 | 8 | 16 : 31;
   if (probe_env("PTTS_GEMV_MASK")) mask = atoi(probe_env("PTTS_GEMV_MASK"));  // probe builds: A/B runs
   gemv_mask_ = mask;
   struct M {
