@@ -64,6 +64,20 @@ def measured_traffic(op):
     return t["ops"][op]["hbm_bytes_per_launch"], t.get("source")
 
 
+def measured_in_step(op):
+    """Average duration (us) of `op`'s launches inside the pipelined step, where it shares the CUs
+    with the other part, from the committed rocprofv3 --kernel-trace of the bench
+    (profiles/op_stats.csv, tools/prof_ops.py piped); None if absent."""
+    path = ROOT / "profiles" / "op_stats.csv"
+    if not path.exists():
+        return None
+    import csv
+    for r in csv.DictReader(open(path)):
+        if r["op"] == op:
+            return float(r["rocprof_avg_us"])
+    return None
+
+
 def measured_mfma():
     """Per-op MFMA busy cycles from the committed rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES pass
     (tools/prof_ops.py mfma), {} if absent."""
@@ -377,6 +391,15 @@ def main():
         roof["rocprof_mfma_busy_frac"] = mf["util_peak_clock"] if mf else None
         roof["kernel"] = name
         roof["avg_us"] = round(us, 2)
+        # the same op inside the measured step (committed rocprof trace of this bench): longer,
+        # since the front and back parts share every CU there
+        ius = measured_in_step(name)
+        if ius:
+            ach = by / (ius * 1e-6) / 1e9 if roof["unit"] == "GB/s" else fl / (ius * 1e-6) / 1e12
+            roof["in_step"] = {"avg_us": round(ius, 2), "achieved": round(ach, 2 if roof["unit"] != "GB/s" else 1),
+                               "frac": round(ach / roof["peak"], 4),
+                               "source": "profiles/op_stats.csv (rocprofv3 --kernel-trace of bench.py, "
+                                         "tools/prof_ops.py piped)"}
         roof["algorithmic_bytes"] = by
         roof["algorithmic_flops"] = fl
         top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
