@@ -1,4 +1,5 @@
 # FlowLM step attention splits (probe build, PTTS_ATTN_VAR: 1 = 4 waves x 64 keys, 2 = 8 x 32,
+# (the PTTS_ATTN_VAR knob was a temporary probe-build patch, removed after this measurement)
 # 3 = 4 x 48, 4 = 8 x 16; default 4 x 32) under frame-pair stepping, where the front part bounds
 set -e
 export PTTS_LIB=pocket-tts_amd/lib-probes/libpocket_tts_hip.so
