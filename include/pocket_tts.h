@@ -89,7 +89,9 @@ typedef struct ptts_engine_config {
                                two passes; PCM identical within float rounding), a call returns the
                                frame computed three calls earlier, and rows admitted at an odd
                                call start one call later (an utterance's frames pair up from its
-                               first). ptts_frame_lag() reports both delays. */
+                               first). ptts_frame_lag() reports both delays. 2 is the
+                               throughput setting (bench.py's default: 0.561 against 0.583 ms per
+                               steady step at B = 32), 1 the low-latency one. */
 } ptts_engine_config;
 
 #define PTTS_QUANT_NONE 0
