@@ -231,7 +231,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   head_resident_ = flow_head_max_resident(dev_);
   flm_resident_ = flow_lm_max_resident(dev_);
   // k_flow_lm hand-off regions: one set per front hand-off buffer, all empty (0xFFFFFFFF); the
-  // launch of step k reads set k % 3 and empties set (k + 1) % 3
+  // launch of step k reads set k % nhb_ and empties set (k + 1) % nhb_
   if (probe_env("PTTS_FLM_ON")) {  // probe builds only (use_flow_lm)
     flm_ws_ = dalloc((size_t)NHB * flow_lm_set_floats());
     PTTS_HIP(hipMemset(flm_ws_, 0xFF, sizeof(float) * NHB * flow_lm_set_floats()));
@@ -1388,6 +1388,11 @@ void Engine::step_async(int B) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
   PTTS_HIP(hipSetDevice(dev_));
+  // Frame pairs: one back pass decodes a row's frames of the pair as a prefix (frame 2j, then
+  // 2j+1). A row the even call did not cover must not produce the pair's second frame alone, so
+  // an odd call covers at most the even call's rows; rows past that are paused for the call, as
+  // rows past n_rows are.
+  if (pipeline_ && nfr_ == 2 && (k_ & 1)) B = std::min(B, rows_hb_[(k_ - 1) % nhb_]);
   prev_hb_ = out_hb_;
   prev_rows_ = out_rows_;
   const int hb = (int)(k_ % nhb_), qp = (int)(k_ & 1);

@@ -113,9 +113,6 @@ class Engine {
   std::map<const float*, Gemv> gvmap_;
   int gemv_mask_ = 0;  // matrices that take the register-resident GEMM
   void derive_gemv();
-  // rocBLAS handle for the plain fp32 GEMMs of the text / voice prefill passes (M >= 256 rows,
-  // eager, never captured): the library's tiles run at 117-149 TF/s on those shapes, twice the
-  // hand-written 64x64 tile; the step's GEMMs stay hand-written (PTTS_BLAS=0 disables it)
   bool own_blob_ = true, ready_ = false;
   hipStream_t stream_ = nullptr;
   Layout L_{};
@@ -177,7 +174,7 @@ class Engine {
   // while the fronts of the next four frames fill the others (the front part may run two passes
   // ahead of the back part).
   static constexpr int NHB = 6;
-  int nhb_ = 3;  // buffers in use: 3, or 4 with frame pairs
+  int nhb_ = 3;  // buffers in use: 3, or NHB = 6 with frame pairs
   int nfr_ = 1;  // frames per back-part pass (ptts_engine_config.back_frames)
   int rows_hb_[NHB] = {};  // rows of the front part that filled each hand-off buffer
   // frame-pair mode: PCM of one pair [B][2][1920] per pair parity, and its pinned host copy

@@ -260,9 +260,6 @@ void set_wg_cap(int cap);
 // Issue priority of the front part's waves (s_setprio 0..3) when they share a SIMD with back-part
 // waves: probe builds only (PTTS_FRONT_PRIO), for A/B runs; a no-op in product builds.
 void set_front_prio(int prio);
-// conv operand rows as an explicit [B * T_in / stride][taps * cin] matrix (cin % 4 == 0)
-void im2col(const float* X, const float* H, int B, int T_in, int stride, int P, int cin, int taps, float* A,
-            hipStream_t s);
 bool flow_head_fits(int B);
 // x0 = cur W_in^T + b_in into hand-off region 0 as its own launch (the adaLN reduce's side job,
 // for replaying k_flow_head alone)

@@ -885,213 +885,8 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
 }
 
 #ifdef PTTS_PROBES
-// ---------------------------------------------------------------------------------------------
-// Persistent form of the 64x64 three-buffer ILV tile (layout 40; 4 waves, 32x32 each). Units are
-// (tile, z) pairs, z a K slice (split-K) or a polyphase index as in k_gemm_glds; workgroup g of G
-// takes units g, g + G, ... and streams the K chunks of all of them through ONE ring of NBUF LDS
-// buffers, so the DMAs of the next unit's first chunks are issued between the MFMAs of this unit's
-// last chunks and its tile start (address set-up, first-chunk latency, workgroup launch) hides
-// behind matrix work. Under the back part's one-workgroup-per-CU cap there is no second
-// workgroup on the CU to hide that start, which is what the non-persistent tile relies on.
-// The waits stay counted: LDS-DMA loads return in order, and chunk `seq` is older than the
-// DMAs of every chunk issued after it, whatever epilogue stores sit between them.
-// Bit-identical to layout 32 (same MFMA order per tile), but the pipelined step gains under 1 %
-// (DESIGN.md §4): the capped back part is not bound by tile starts, so this stays a probe.
-// ---------------------------------------------------------------------------------------------
-template <int MODE, int NBUF, int MINB>
-__global__ __launch_bounds__(256, MINB) void k_gemm_glds_per(GemmArgs a) {
-  constexpr int WN = 2, BK = 32, TM = 64, TN = 64, ROWS = TM + TN;
-  constexpr int CPR = BK / 4, RPI = 64 / CPR, NINS = ROWS / RPI, IPW = NINS / 4, DIST = NBUF - 1;
-  static_assert(NBUF >= 2 && NBUF <= 5 && IPW == 4, "counted waits below: at most four chunks in flight");
-  __shared__ __attribute__((aligned(16))) float lds[NBUF * ROWS * BK];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int r = lane & 31, h = lane >> 5;
-  const int gx = a.tiles_n, gy = a.tiles_m, T = gx * gy, U = T * a.units_z;
-  const int G = gridDim.x, nchunks = a.K / BK;
-  // unit u -> tile origin and z; the tile of u is placed as xcd_tile places hardware id u (G is
-  // a multiple of 8 or covers every unit, so unit u runs on XCD u % 8 like workgroup u would)
-  auto unit = [&](int u, int& m0, int& n0, int& z) {
-    z = u / T;
-    const int L = u - z * T, pn = a.xcd_pn;
-    int bx, by;
-    if ((T & 7) == 0 && pn > 0) {
-      const int pm = 8 / pn, xcd = L & 7, j = L >> 3, tnx = gx / pn;
-      bx = (xcd % pn) * tnx + j % tnx;
-      by = (xcd / pn) * (gy / pm) + j / tnx;
-    } else {
-      const int t = (T & 7) == 0 ? (L & 7) * (T >> 3) + (L >> 3) : L;
-      bx = t % gx;
-      by = t / gx;
-    }
-    m0 = by * TM;
-    n0 = bx * TN;
-  };
-  auto krange = [&](int z, int& cb, int& ce, int& phase) {
-    cb = 0, ce = nchunks, phase = 0;
-    if (MODE == 0 || a.S > 1) {
-      cb = (int)((long)nchunks * z / a.S);
-      ce = (int)((long)nchunks * (z + 1) / a.S);
-    } else {
-      phase = z;
-    }
-  };
-  const unsigned lds_base = lds_addr(lds);
-  // issue cursor: unit iu, chunk ic of [ic, ice), and this lane's DMA sources for that unit
-  // (as in k_gemm_glds: A rows or W rows per wave-uniform instruction)
-  int iu = blockIdx.x, ic = 0, ice = 0;
-  const float* src_base[IPW];
-  const float* src_hist[IPW];
-  int src_qs[IPW];
-  auto setup = [&](int u) {
-    int m0, n0, z, ph;
-    unit(u, m0, n0, z);
-    krange(z, ic, ice, ph);
-    const float* Wp = a.W + (long)ph * a.w_phase_stride;
-#pragma unroll
-    for (int ins = 0; ins < IPW; ++ins) {
-      const int j = wave + 4 * ins;
-      const int row = j * RPI + lane / CPR;
-      const int lcol = (lane % CPR) ^ swz<BK>(row);
-      if (j * RPI < TM) {
-        const int m = min(m0 + row, a.M - 1);  // rows >= M only feed output rows that are never stored
-        if (MODE == 0) {
-          src_base[ins] = a.X + (long)m * a.ldx + 4 * lcol;
-        } else {
-          const int bq = m / a.Tq;
-          const int qq = m - bq * a.Tq;
-          src_qs[ins] = qq * a.stride_in - a.P;
-          src_base[ins] = a.X + (long)bq * a.T_in * a.ldx + 4 * lcol;
-          src_hist[ins] = a.H + ((long)bq * a.P + a.P) * a.cin + 4 * lcol;
-        }
-      } else {
-        const int n = min(n0 + row - TM, a.Nw - 1);
-        src_base[ins] = Wp + (long)n * a.K + 4 * lcol;
-      }
-    }
-  };
-  // next chunk to issue: past the unit's end to the next unit with a non-empty K range
-  auto advance = [&]() {
-    ++ic;
-    while (ic >= ice) {
-      iu += G;
-      if (iu >= U) return;
-      setup(iu);
-    }
-  };
-  const long ldx = a.ldx, hld = a.cin;
-  auto dma_src = [&](int c, int ins) -> const float* {
-    const int j = wave + 4 * ins;
-    const int k0 = c * BK;
-    if (MODE != 0 && j * RPI < TM) {
-      const int tap = k0 / a.cin;  // scalar
-      const int ci = k0 - tap * a.cin;
-      const int t = src_qs[ins] + tap;
-      const float* px = src_base[ins] + t * ldx + ci;
-      const float* ph = src_hist[ins] + t * hld + ci;
-      return t >= 0 ? px : ph;
-    }
-    return src_base[ins] + k0;
-  };
-  auto dma = [&](const float* src, int buf, int ins) {
-    const int j = wave + 4 * ins;
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)((buf * ROWS * BK + j * RPI * BK) * 4));
-    if (a.w_nt && j * RPI >= TM) glds16_nt(src, dst);
-    else glds16(src, dst);
-  };
-  constexpr bool elu = MODE == 2;
-  const int arow = 32 * wm + r, brow = TM + 32 * wn + r;
-  // prologue: the first DIST chunks of the stream
-  int issued = 0;
-  if (iu < U) {
-    setup(iu);
-    if (ic >= ice) {
-      --ic;
-      advance();
-    }
-  }
-  for (int d = 0; d < DIST; ++d) {
-    if (iu >= U) break;
-#pragma unroll
-    for (int ins = 0; ins < IPW; ++ins) dma(dma_src(ic, ins), issued % NBUF, ins);
-    ++issued;
-    advance();
-  }
-  int seq = 0;
-  for (int cu = blockIdx.x; cu < U; cu += G) {
-    int m0, n0, z, cb, ce, phase;
-    unit(cu, m0, n0, z);
-    krange(z, cb, ce, phase);
-    floatx16 acc;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
-    for (int c = cb; c < ce; ++c, ++seq) {
-      {  // chunk seq landed once only the younger chunks' DMAs remain outstanding
-        const int younger = issued - seq - 1;
-        if (younger >= 3) PTTS_WAIT_VM(3 * IPW);
-        else if (younger == 2) PTTS_WAIT_VM(2 * IPW);
-        else if (younger == 1) PTTS_WAIT_VM(IPW);
-        else PTTS_WAIT_VM(0);
-      }
-      // every wave's DMAs of chunk seq have landed, and every wave is done with chunk seq-1's
-      // buffer, which the DMA issued next (stream position seq + DIST) overwrites
-      __syncthreads();
-      const bool pf = iu < U;
-      const int pbuf = issued % NBUF;
-      const float* nsrc[IPW];
-#pragma unroll
-      for (int ins = 0; ins < IPW; ++ins) {
-        nsrc[ins] = dma_src(pf ? ic : 0, ins);
-        asm volatile("" : "+v"(nsrc[ins]));
-      }
-      const int buf = seq % NBUF;
-      float af[16], bf[16];
-      {
-        const float* la = lds + buf * ROWS * BK + arow * BK;
-        const float* lb = lds + buf * ROWS * BK + brow * BK;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int lc = 4 * h + i;
-          const float4 x = *reinterpret_cast<const float4*>(la + 4 * (lc ^ swz<BK>(arow)));
-          af[4 * i + 0] = x.x; af[4 * i + 1] = x.y; af[4 * i + 2] = x.z; af[4 * i + 3] = x.w;
-          const float4 y = *reinterpret_cast<const float4*>(lb + 4 * (lc ^ swz<BK>(brow)));
-          bf[4 * i + 0] = y.x; bf[4 * i + 1] = y.y; bf[4 * i + 2] = y.z; bf[4 * i + 3] = y.w;
-        }
-        if (elu) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) af[j] = elu1(af[j]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
-        if (pf && (j & 3) == 3) dma(nsrc[j >> 2], pbuf, j >> 2);
-      }
-      if (pf) {
-        ++issued;
-        advance();
-      }
-    }
-    const bool ident = gemm_ident(a, MODE, phase);
-    const int tm0 = m0 + 32 * wm, tn0 = n0 + 32 * wn;
-    if (ident && !a.partial && tm0 + 32 <= a.M && tn0 + 32 <= a.N) {
-      gemm_store_tile(a, acc, tm0, tn0, h, r);
-    } else {
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int row = tm0 + (g & 3) + 8 * (g >> 2) + 4 * h;
-        const int col = tn0 + r;
-        if (row < a.M && col < a.N) {
-          const float v = acc[g];
-          if (a.partial) a.partial[((long)z * a.M + row) * a.N + col] = v;
-          else gemm_store(a, row, col, phase, ident, v);
-        }
-      }
-    }
-  }
-}
-#endif  // PTTS_PROBES
+#include "../probes/gemm_per.inc"  // persistent back-part tiles (layouts 40-42), measurement builds only
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Register-blocked K-split GEMM: each wave accumulates a (32*TM) x (32*TN) block (TM*TN
@@ -1773,8 +1568,13 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
                                               const float* __restrict__ P, float* __restrict__ partial) {
   front_prio();
   constexpr int WK = 4 / WN, KS = KW * WK, NV = KW / 8, LDA = KS + 4;  // +4: conflict-free b128 rows
-  __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
-  __shared__ __attribute__((aligned(16))) float red[WK > 1 ? 4 * 16 * 64 : 1];
+  // X's slice and (WK > 1) the cross-wave reduction share one LDS block (a barrier between the
+  // last fragment read and the first partial write): 33 KB instead of 49 KB for linear2, so two
+  // workgroups fit beside a capped back-part workgroup on a CU
+  constexpr int SA = 32 * LDA, RED = WK > 1 ? 4 * 16 * 64 : 0;
+  __shared__ __attribute__((aligned(16))) float smem[SA > RED ? SA : RED];
+  float* const sA = smem;
+  float* const red = smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = blockIdx.x, z = blockIdx.y, S = gridDim.y, m0 = 32 * blockIdx.z;  // z: K slice; blockIdx.z: 32-row block
@@ -1823,6 +1623,7 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   }
   // WK > 1: the WK waves of column block c (waves c, c + WN, ..) hold partials over their k
   // ranges; the 16 * WN (block, register) outputs are dealt 4 * WN per wave and summed in k order
+  __syncthreads();  // every wave's fragment reads of sA are done before red overwrites it
 #pragma unroll
   for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[g];
   __syncthreads();
@@ -3625,29 +3426,6 @@ void transpose(const float* src, int rows, int cols, float* dst, hipStream_t s) 
   hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, cols, dst);
 }
 
-// Implicit-GEMM conv operand made explicit (for a library GEMM): A[m][j cin + c] with m = b Tq + q
-// is input time t = q stride + j - P of utterance b: X[b T_in + t][c] for t >= 0, else the
-// history H[b][P + t][c] (the same rule as k_gemm_glds's MODE 1 operand loader).
-__global__ void k_im2col(const float* __restrict__ X, const float* __restrict__ H, int T_in, int Tq, int stride, int P,
-                         int cin, int taps, long n4, float4* __restrict__ A) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= n4) return;
-  const int K4 = taps * cin / 4;
-  const long m = e / K4;
-  const int k = (int)(e - m * K4) * 4;
-  const int j = k / cin, c = k - j * cin;
-  const int b = (int)(m / Tq), q = (int)(m - (long)b * Tq);
-  const int t = q * stride + j - P;
-  const float* src = t >= 0 ? X + ((long)b * T_in + t) * cin + c : H + ((long)b * P + (P + t)) * cin + c;
-  A[e] = *reinterpret_cast<const float4*>(src);
-}
-
-void im2col(const float* X, const float* H, int B, int T_in, int stride, int P, int cin, int taps, float* A,
-            hipStream_t s) {
-  const long n4 = (long)B * (T_in / stride) * taps * cin / 4;
-  hipLaunchKernelGGL(k_im2col, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, X, H, T_in, T_in / stride, stride,
-                     P, cin, taps, n4, reinterpret_cast<float4*>(A));
-}
 
 bool flow_head_fits(int B) { return B >= 1 && B <= 128; }
 

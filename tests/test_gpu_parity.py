@@ -347,6 +347,52 @@ def test_frame_pairs_continuous_batching_matches_oracle(oracle):
         eng.close()
 
 
+def test_frame_pairs_with_varying_rows_per_call_match_oracle(oracle):
+    """back_frames=2 with n_rows changing between the two calls of a pair: a row the
+    even call left out must not produce the pair's second frame alone (the pass decodes a row's
+    frames of a pair as a prefix), so an odd call covers at most the even call's rows and the row
+    pauses for the pair. Every frame a row does get must equal its oracle run, in order."""
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    rng = np.random.default_rng(13)
+    n_frames = 6
+    eng = pt.Engine(device=0, max_slots=4, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
+                    back_frames=2)
+    try:
+        orc, lat, got, ids_l, vs = {}, {}, {}, [], []
+        for b in range(4):
+            F = 5 + 2 * b
+            prompt = (d["prompt"][:F] * (1.0 + 0.03 * b)).astype(np.float32)
+            ids = rng.integers(0, 4000, size=3 + 2 * b).astype(np.int32)
+            vs.append(eng.voice_from_prompt(prompt))
+            ids_l.append(ids)
+            s = oracle.new_state(256)
+            s.prefill(prompt)
+            s.prefill_tokens(ids)
+            orc[b], lat[b], got[b] = s, None, 0
+        eng.open_many(list(range(4)), vs, ids_l, [params(max_frames=n_frames)] * 4)
+        # (even, odd) row counts per pair: odd > even leaves rows [even, odd) paused for the pair
+        pattern = [(1, 4), (4, 4), (2, 3), (3, 1), (4, 2), (1, 4)] + [(4, 4)] * 8
+        for ne, no in pattern:
+            for n in (ne, no):
+                eng.step_async(n)
+                r = eng.fetch(4)  # the frame three calls back may cover more rows than n
+                for b in range(4):
+                    if not r.valid[b]:
+                        continue
+                    o = orc[b].step(lat[b])
+                    lat[b] = o["latent"]
+                    got[b] += 1
+                    assert bool(r.last[b]) == (got[b] == n_frames), (b, got[b])
+                    assert abs(r.eos_logits[b] - o["eos_logit"]) <= LAT_TOL
+                    np.testing.assert_allclose(r.latents[b], o["latent"], atol=LAT_TOL)
+                    assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL, (b, got[b])
+        assert all(got[b] == n_frames for b in range(4)), got
+    finally:
+        eng.close()
+
+
 def test_long_utterance_wraps_mimi_ring(gpu_engine, oracle):
     """70 frames: the Mimi decoder ring (512 positions = 32 frames) wraps twice and the 250-key
     window slides across the wrap; the FlowLM cache grows to voice + text + 70 positions. Every
