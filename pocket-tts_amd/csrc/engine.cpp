@@ -109,7 +109,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
   st_ = (SlotState*)dalloc((sizeof(SlotState) * B + 3) / 4);
   lat_in_ = dalloc((size_t)B * LDIM);
   cur_ = dalloc((size_t)B * LDIM);
-  qprev_ = dalloc((size_t)2 * B * MD);  // [parity][slot][512], see quant_upsample
+  // overlap-add history [slot][512] (the last committed frame's quantizer output) and the
+  // pass's quantizer outputs [slot][2][512], copied into it by the commit (quant_upsample)
+  qprev_ = dalloc((size_t)3 * B * MD);
+  qcur_ = qprev_ + (size_t)B * MD;
   eos_ = dalloc(B);
   static_assert(sizeof(FrameFlags) == 2 * sizeof(float), "FrameFlags packs into two floats");
   meta_floats_ = (size_t)B * (LDIM + 1 + 2);
@@ -1075,8 +1078,8 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   {
     const float *sd = W(L_.emb_std), *mn = W(L_.emb_mean), *wq = W(L_.quant_w), *wu = W(L_.up_w);
     const float *lw = W(L_.mdec[0].n1w), *lb = W(L_.mdec[0].n1b);
-    const float* qin = qprev_ + (size_t)(qp ^ 1) * max_slots_ * MD;
-    float* qout = qprev_ + (size_t)qp * max_slots_ * MD;
+    const float* qin = qprev_;
+    float* qout = qcur_;
     float *x = mx_, *h = mh_;
     const float* lat0 = lat_out_[hb];
     const float* lat1 = lat_out_[hb2];
@@ -1283,6 +1286,8 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     c.flags1 = flags_[hb2];
     c.nfr = nfr;
     c.mpos = mpos_;
+    c.qcur = qcur_;
+    c.qprev = qprev_;
     double hb_bytes = 0;  // every history row is read from its activation and stored
     for (int i = 0; i < 8; ++i) hb_bytes += 8.0 * B * hist_P_[i] * hist_C_[i];
     ops.push_back({"commit", [c](hipStream_t s) { step_commit(c, s); }, 0.0, hb_bytes + 16.0 * B});
@@ -2020,11 +2025,9 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
       r.buf[i] = hist_[i];
       r.per_slot[i] = (long)hist_P_[i] * hist_C_[i];
     }
-    r.buf[8] = qprev_;  // both parity halves of the overlap-add history
+    r.buf[8] = qprev_;  // the overlap-add history
     r.per_slot[8] = MD;
-    r.buf[9] = qprev_ + (size_t)max_slots_ * MD;
-    r.per_slot[9] = MD;
-    r.nb = 10;
+    r.nb = 9;
     r.slots = admit_slots_;
     r.n = n;
     r.lat_in = lat_in_;
@@ -2114,9 +2117,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
     }
     r.buf[8] = qprev_;
     r.per_slot[8] = MD;
-    r.buf[9] = qprev_ + (size_t)max_slots_ * MD;
-    r.per_slot[9] = MD;
-    r.nb = 10;
+    r.nb = 9;
     r.slots = admit_slots_;
     r.n = 1;
     r.lat_in = lat_in_;
@@ -2154,7 +2155,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
       PTTS_HIP(hipMemcpyAsync(pcm + (size_t)i * FRAME, pcm_[par] + (size_t)slot * FRAME, sizeof(float) * FRAME,
                               hipMemcpyDeviceToHost, stream_));
     if (quant)
-      PTTS_HIP(hipMemcpyAsync(quant + (size_t)i * MD, qprev_ + ((size_t)par * max_slots_ + slot) * MD,
+      PTTS_HIP(hipMemcpyAsync(quant + (size_t)i * MD, qcur_ + (size_t)slot * 2 * MD,
                               sizeof(float) * MD, hipMemcpyDeviceToHost, stream_));
     PTTS_HIP(hipMemcpyAsync(flags_[par] + slot, &off, sizeof off, hipMemcpyHostToDevice, stream_));
     PTTS_HIP(hipStreamSynchronize(stream_));

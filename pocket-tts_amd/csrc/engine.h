@@ -127,7 +127,7 @@ class Engine {
   int* fpos_ = nullptr;
   int* mpos_ = nullptr;
   SlotState* st_ = nullptr;
-  float *lat_in_ = nullptr, *cur_ = nullptr, *qprev_ = nullptr, *eos_ = nullptr;
+  float *lat_in_ = nullptr, *cur_ = nullptr, *qprev_ = nullptr, *qcur_ = nullptr, *eos_ = nullptr;
   float* hist_[8] = {};
   int hist_T_[8] = {}, hist_C_[8] = {}, hist_P_[8] = {};
 

@@ -328,14 +328,16 @@ void front_commit(const FrontCommitArgs& a, hipStream_t s);
 // Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0, for
 // nfr (1 or 2) consecutive frames of every row: latent[f] [B][32] -> x [B][16 nfr][512] (frame f
 // at rows 16 f..), h = LN(x). The overlap-add history [B][512] is read from qprev_in (frame 0;
-// frame 1 overlaps frame 0) and the last valid frame's quantized row is written to qprev_out
-// (parity double buffer; carried over for rows without a valid frame).
+// frame 1 overlaps frame 0); the quantized rows of the pass go to qprev_out [B][2][512], and the
+// commit copies the last valid frame's into the history (rows without a frame, or outside the
+// pass, keep theirs).
 void quant_upsample(const float* const latent[2], const FrameFlags* const fl[2], int nfr, int B, const float* emb_std,
                     const float* emb_mean, const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
                     float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s);
 
 // End of the back part, for rows with a valid frame: copy the last P rows of each conv input
-// into its history, advance the Mimi position. A launch over nfr frames (T rows per row of a
+// into its history and the last valid frame's quantizer output into the overlap-add history,
+// advance the Mimi position. A launch over nfr frames (T rows per row of a
 // buffer = nfr frames of T / nfr rows) commits through the row's last valid frame: its valid
 // frames are a prefix (an utterance starts at a frame-pair boundary and ends with its last frame).
 struct HistDesc {
@@ -351,6 +353,8 @@ struct CommitArgs {
   const FrameFlags* flags1;  // frame 1 (nfr == 2)
   int nfr;
   int* mpos;  // Mimi decoder positions, += 16 per committed frame
+  const float* qcur;  // the pass's quantizer outputs [B][2][512] (quant_upsample)
+  float* qprev;       // overlap-add history [B][512] <- qcur[b][last valid frame]
 };
 void step_commit(const CommitArgs& a, hipStream_t s);
 

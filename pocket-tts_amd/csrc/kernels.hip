@@ -2537,9 +2537,9 @@ void flow_cond(const float* P, int S, int B, const float* bias, const float* tem
 // (conv.rs:315-346: frame row r = q*w[r] + qprev*w[16+r], the overlap-add of the previous frame's
 // tail) + norm1 of Mimi layer 0. One workgroup per (row b, 4 of the 16 output rows): 4x the
 // workgroups of a per-row kernel, each loading only its rows' upsample taps, one LayerNorm row
-// per wave. The overlap-add history is double-buffered by frame parity (read qprev_in, write
-// qprev_out), so the four workgroups of a row never race on it; a row without a valid frame
-// carries its history over unchanged.
+// per wave. The pass's quantizer outputs go to a scratch (qprev_out [B][2][512]) and the commit
+// moves the last valid frame's into the history, so the four workgroups of a row never race on
+// it, and a row without a frame in the pass (or outside it) keeps its history unchanged.
 struct QuantUpArgs {
   const float* latent[2];
   const FrameFlags* fl[2];
@@ -2572,7 +2572,6 @@ __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
     sz[g][k] = a.latent[g][b * 32 + k] * a.emb_std[k] + a.emb_mean[k];
   }
   __syncthreads();
-  const bool v0 = a.fl[0][b].valid != 0, v1 = a.nfr > 1 && a.fl[1][b].valid != 0;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = tid + 256 * u;
@@ -2593,7 +2592,10 @@ __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
       sx[r * 512 + c] = v;
       a.x[((long)b * T + 16 * f + r0 + r) * 512 + c] = v;
     }
-    if (blockIdx.y == 0) a.qprev_out[(long)b * 512 + c] = v1 ? q[1] : (v0 ? q[0] : qpv[u]);
+    if (blockIdx.y == 0) {
+      a.qprev_out[(long)b * 1024 + c] = q[0];
+      if (a.nfr > 1) a.qprev_out[(long)b * 1024 + 512 + c] = q[1];
+    }
   }
   __syncthreads();
   const int lane = tid & 63, r = tid >> 6;  // one row per wave
@@ -2640,6 +2642,8 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
     for (long e = threadIdx.x; e < n; e += 256) dst[e] = src[e];
     return;
   }
+  // the overlap-add history of the next pass: the last valid frame's quantizer output
+  for (int c = threadIdx.x; c < 512; c += 256) a.qprev[(long)b * 512 + c] = a.qcur[((long)b * 2 + nv - 1) * 512 + c];
   if (threadIdx.x == 0) a.mpos[b] += 16 * nv;
 }
 

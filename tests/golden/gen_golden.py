@@ -102,11 +102,18 @@ def build_models(torch):
     return flm, mimi, speaker_proj
 
 
-def run_e2e(torch, flm, mimi, F, S, N, lsd_steps, tag):
+def run_e2e(torch, flm, mimi, F, S, N, lsd_steps, tag, ids=None, eos_threshold=-4.0, frames_after_eos=None):
+    """N frames at temp 0 from a synthetic F-frame voice prompt and S text ids (random unless
+    `ids` is given). frames_after_eos set: the Rust segment's stop rule (tts_model.rs:1055-1063):
+    the frame at eos_step + frames_after_eos is the last, N is max_gen_len."""
     from pocket_tts.modules.stateful_module import increment_steps, init_states
 
     prompt = synth.gaussian(1, f"{tag}/prompt", F * 1024, 0.11).reshape(F, 1024)
-    ids = (synth.uniform01(2, f"{tag}/ids", S) * 4000).astype(np.int32)
+    if ids is None:
+        ids = (synth.uniform01(2, f"{tag}/ids", S) * 4000).astype(np.int32)
+    ids = np.asarray(ids, np.int32)
+    S = ids.size
+    eos_step = None
     caps = {}
     h1 = flm.out_norm.register_forward_hook(lambda m, i, o: caps.__setitem__("tout", o[:, -1].clone()))
     h2 = flm.out_eos.register_forward_hook(lambda m, i, o: caps.__setitem__("eos", o.clone()))
@@ -123,8 +130,8 @@ def run_e2e(torch, flm, mimi, F, S, N, lsd_steps, tag):
         empty = torch.empty((1, 0, 1024))
         touts, eos, lats, pcms, quant, ups, trs = [], [], [], [], [], [], []
         for step in range(N):
-            lat, _ = flm._sample_next_latent(backbone, empty, model_state=state, lsd_decode_steps=lsd_steps,
-                                             temp=0.0, noise_clamp=None, eos_threshold=-4.0)
+            lat, is_eos = flm._sample_next_latent(backbone, empty, model_state=state, lsd_decode_steps=lsd_steps,
+                                                  temp=0.0, noise_clamp=None, eos_threshold=eos_threshold)
             increment_steps(flm, state, increment=1)
             touts.append(caps["tout"][0].numpy().copy())
             eos.append(float(caps["eos"][0, 0]))
@@ -141,6 +148,11 @@ def run_e2e(torch, flm, mimi, F, S, N, lsd_steps, tag):
                 ups.append(up[0].numpy().copy())
                 trs.append(tr_out[0].numpy().copy())
             backbone = lat[:, None, :]
+            if frames_after_eos is not None:
+                if bool(is_eos) and eos_step is None:
+                    eos_step = step
+                if eos_step is not None and step >= eos_step + frames_after_eos:
+                    break
     h1.remove()
     h2.remove()
     out.update(
@@ -149,6 +161,9 @@ def run_e2e(torch, flm, mimi, F, S, N, lsd_steps, tag):
         after_decoder_transformer=np.stack(trs),
         meta=np.array([SEED, F, S, N, lsd_steps], np.int64),
     )
+    if frames_after_eos is not None:
+        out["stop"] = np.array([len(lats), -1 if eos_step is None else eos_step, frames_after_eos, N], np.int64)
+        out["eos_threshold"] = np.array([eos_threshold], np.float32)
     return out
 
 
@@ -270,6 +285,26 @@ def main():
         del fx["tout"]
         save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / "e2e_long.safetensors"))
         print("long fixture written to", HERE)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "hello":  # BASELINE configs[0] on synthetic weights
+        # "Hello, world!" through the Rust segment driver (tts_model.rs:935-1071): prepare_text_prompt
+        # gives "        Hello, world!" (2 words < 5: 8 spaces prepended), whose ids under the
+        # reference's tokenizer.json are text_ids.json reference.native_ids[1] (tokenizers library,
+        # gen_text_golden.py); temp 0, eos_threshold -4.0 (the CLI default), max_gen_len (2 + 2) * 13,
+        # frames_after_eos 5 (estimate_frames_after_eos: <= 4 words). Voice "alba" is unavailable
+        # offline: a synthetic 125-frame prompt stands in.
+        import json
+
+        tj = json.load(open(HERE / "text_ids.json"))
+        assert tj["texts"][1] == "        Hello, world!"
+        ids = tj["reference"]["native_ids"][1]
+        # also at a threshold above every logit of the run: the segment then ends at max_gen_len
+        for thr, name in ((-4.0, "hello_world"), (0.25, "hello_world_maxlen")):
+            fx = run_e2e(torch, flm, mimi, F=125, S=len(ids), N=(2 + 2) * 13, lsd_steps=1, tag="hello",
+                         ids=ids, eos_threshold=thr, frames_after_eos=5)
+            del fx["tout"]
+            save_file({k: np.ascontiguousarray(v) for k, v in fx.items()}, str(HERE / f"{name}.safetensors"))
+            print(name, "stop", fx["stop"], "eos logits", fx["eos_logit"].min(), fx["eos_logit"].max())
         return
     if len(sys.argv) > 1 and sys.argv[1] == "voice":  # only the voice-cloning front-end fixtures
         fx = run_encoder_chunked(torch, mimi, speaker_proj, n_frames=5, chunk_frames=2, tag="encc5")

@@ -347,18 +347,21 @@ def test_frame_pairs_continuous_batching_matches_oracle(oracle):
         eng.close()
 
 
-def test_frame_pairs_with_varying_rows_per_call_match_oracle(oracle):
-    """back_frames=2 with n_rows changing between the two calls of a pair: a row the
-    even call left out must not produce the pair's second frame alone (the pass decodes a row's
-    frames of a pair as a prefix), so an odd call covers at most the even call's rows and the row
-    pauses for the pair. Every frame a row does get must equal its oracle run, in order."""
+@pytest.mark.parametrize("back_frames", [1, 2])
+def test_varying_rows_per_call_match_oracle(oracle, back_frames):
+    """Pipelined stepping with n_rows changing from call to call, so rows pause (outside n_rows)
+    and resume with their codec state intact: the overlap-add history, conv histories and Mimi
+    position of a row outside a pass must not move. back_frames=2: a row the even
+    call left out must not produce the pair's second frame alone (the pass decodes a row's frames
+    of a pair as a prefix), so an odd call covers at most the even call's rows and the row pauses
+    for the pair. Every frame a row does get must equal its oracle run, in order."""
     import pocket_tts_amd as pt
 
     d = load_golden("e2e_lsd1.safetensors")
     rng = np.random.default_rng(13)
     n_frames = 6
     eng = pt.Engine(device=0, max_slots=4, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
-                    back_frames=2)
+                    back_frames=back_frames)
     try:
         orc, lat, got, ids_l, vs = {}, {}, {}, [], []
         for b in range(4):
@@ -377,7 +380,7 @@ def test_frame_pairs_with_varying_rows_per_call_match_oracle(oracle):
         for ne, no in pattern:
             for n in (ne, no):
                 eng.step_async(n)
-                r = eng.fetch(4)  # the frame three calls back may cover more rows than n
+                r = eng.fetch(4)  # the frame of an earlier call may cover more rows than n
                 for b in range(4):
                     if not r.valid[b]:
                         continue

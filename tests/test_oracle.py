@@ -97,3 +97,28 @@ def test_oracle_long_context_matches_reference(oracle):
         np.testing.assert_allclose(r["pcm"], d["pcm"][i], atol=1e-6)
         if i < 3:
             np.testing.assert_allclose(r["after_tr"].T, d["after_decoder_transformer"][i], atol=2e-5)
+
+
+@pytest.mark.parametrize("fixture", ["hello_world.safetensors", "hello_world_maxlen.safetensors"])
+def test_oracle_hello_world_matches_reference(oracle, fixture):
+    """BASELINE configs[0] (gen_golden.py hello): "Hello, world!" as the reference tokenizer's ids
+    of the prepared prompt, temp 0, the Rust stop rule (tts_model.rs:1055-1063) at eos_threshold
+    -4.0 (6 frames: EOS at frame 0, 5 tail frames) and above every logit (max_gen_len 52)."""
+    d = load_golden(fixture)
+    n, eos_step, fae, max_len = (int(v) for v in d["stop"])
+    thr = float(d["eos_threshold"][0])
+    s = oracle.new_state(256)
+    s.prefill(d["prompt"])
+    s.prefill_tokens(d["text_ids"])
+    lat, stop_at = None, None
+    for i in range(max_len):
+        r = s.step(lat)
+        lat = r["latent"]
+        if r["eos_logit"] > thr and stop_at is None:
+            stop_at = i + fae
+        assert abs(r["eos_logit"] - d["eos_logit"][i]) < 2e-5, i
+        np.testing.assert_allclose(lat, d["latent"][i], atol=2e-5)
+        np.testing.assert_allclose(r["pcm"], d["pcm"][i], atol=1e-6)
+        if stop_at is not None and i >= stop_at:
+            break
+    assert i + 1 == n and (eos_step < 0 or stop_at == eos_step + fae)

@@ -16,7 +16,7 @@ from pathlib import Path
 
 import numpy as np
 import pytest
-from conftest import LAT_TOL, load_golden
+from conftest import LAT_TOL, PCM_TOL, load_golden, pcm_err
 
 REF_ASSETS = Path("/root/reference/assets")
 RATES = (48000, 44100, 16000, 22050, 8000)
@@ -190,6 +190,47 @@ def test_gpu_chunked_voice_matches_reference(gpu_engine):
     np.testing.assert_allclose(v4.conditioning(), e["conditioning"], atol=1e-5)
     for x in (v, v1, v4):
         x.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_frames,chunk", [(125, 120), (750, 180)])
+def test_gpu_long_voice_prompt_chunked_matches_oracle(oracle, n_frames, chunk):
+    """Voice prompts past one chunk through the adaptive chunked encoder (tts_model.rs:530-577:
+    120-frame chunks up to 600 frames, 180 up to 1800): a 10-s prompt (125 frames = 120 + 5, the
+    bench's prompt length) and a 60-s one (750 frames = 4 x 180 + 30, the reference's stress test,
+    tests/memory_usage.rs:7-39). Every chunk re-applies the downsample's replicate pad (the
+    quirk), so the conditioning must equal the oracle's encode with the same
+    chunking; then 4 generated frames from that voice against the oracle."""
+    import pocket_tts_amd as pt
+
+    pcm = (0.1 * np.random.default_rng(n_frames).standard_normal(n_frames * 1920)).astype(np.float32)
+    eng = pt.Engine(device=0, max_slots=1, max_ctx=n_frames + 64, lsd_decode_steps=1, seed=0x5EED)
+    try:
+        v = eng.voice_from_audio(pcm, 24000, 0)  # adaptive rule
+        assert v.n_frames == n_frames
+        cond, _, _, _ = oracle.encode(pcm, chunk)
+        err = float(np.abs(v.conditioning() - cond).max())
+        assert err <= 2e-5, err
+        # the quirk is exercised: the one-pass encode differs at the chunk starts
+        one, _, _, _ = oracle.encode(pcm, -1)
+        assert np.abs(one[chunk] - cond[chunk]).max() > 1e-4
+        ids = np.array([260, 2994, 262, 578, 682], np.int32)
+        eng.open(0, v, ids, pt.GenerationParams(temp=0.0, eos_threshold=float("inf"), max_frames=4))
+        s = oracle.new_state(n_frames + 64)
+        s.prefill(cond)
+        s.prefill_tokens(ids)
+        lat = None
+        for i in range(4):
+            r = eng.step(1)
+            ref = s.step(lat)
+            lat = ref["latent"]
+            assert r.valid[0]
+            np.testing.assert_allclose(r.latents[0], ref["latent"], atol=LAT_TOL)
+            assert pcm_err(r.pcm[0] - ref["pcm"]) <= PCM_TOL, i
+        v.close()
+        print(f"{n_frames}-frame prompt ({chunk}-frame chunks): conditioning max |d| {err:.3g}")
+    finally:
+        eng.close()
 
 
 @pytest.mark.gpu
