@@ -78,6 +78,45 @@ def measured_in_step(op):
     return None
 
 
+def measured_in_step_all():
+    """{op: average in-step duration (us)} from the committed kernel trace (profiles/op_stats.csv)."""
+    path = ROOT / "profiles" / "op_stats.csv"
+    if not path.exists():
+        return {}
+    import csv
+    return {r["op"]: float(r["rocprof_avg_us"]) for r in csv.DictReader(open(path)) if r["rocprof_avg_us"]}
+
+
+def step_roofline(plan, B, K, back_frames, steady_us):
+    """The roofline of the timed step (per frame): the front part's algorithmic bytes at the HBM peak
+    plus the back part's algorithmic flops at the fp32 MFMA peak (serial sum; the two parts overlap
+    in the pipelined step, so `overlap_floor_us`, the larger of the two, is the tighter floor), over
+    the measured steady step. The front / back in-step fractions divide the same bytes / flops by
+    the summed in-step durations of the part's launches (committed kernel trace of this bench)."""
+    L = PROMPT_FRAMES + TEXT_TOKENS + K / 2.0
+    f_bytes = 84_527_137 * 4 + B * (49_152 * L + 49_152)
+    b_flops = B * (525.1e6 + 65_536 * 266)  # per frame
+    f_us = f_bytes / (HBM_PEAK_GBS * 1e9) * 1e6
+    b_us = b_flops / (F32_PEAK_TFLOPS * 1e12) * 1e6
+    out = {"floor_us": round(f_us + b_us, 1), "front_floor_us": round(f_us, 1), "back_floor_us": round(b_us, 1),
+           "overlap_floor_us": round(max(f_us, b_us), 1), "measured_us": round(steady_us, 1),
+           "frac": round((f_us + b_us) / steady_us, 4), "frac_overlap": round(max(f_us, b_us) / steady_us, 4)}
+    ins = measured_in_step_all()
+    names = [n for n, _, _ in plan]
+    front = [n for n in names if n.startswith(("flow.", "head.", "front_commit"))]
+    back = [n for n in names if n.startswith(("mimi.", "seanet.")) or n == "commit"]
+    if ins and all(n in ins for n in front + back):
+        fu = sum(ins[n] for n in front)
+        bu = sum(ins[n] for n in back) / back_frames  # a back pass decodes back_frames frames
+        out["front_in_step"] = {"sum_launch_us": round(fu, 1), "achieved": round(f_bytes / (fu * 1e-6) / 1e9, 1),
+                                "unit": "GB/s", "frac": round(f_bytes / (fu * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        out["back_in_step"] = {"sum_launch_us_per_frame": round(bu, 1),
+                               "achieved": round(b_flops / (bu * 1e-6) / 1e12, 2), "unit": "TFLOP/s",
+                               "frac": round(b_flops / (bu * 1e-6) / 1e12 / F32_PEAK_TFLOPS, 4)}
+        out["source"] = "profiles/op_stats.csv (rocprofv3 --kernel-trace of bench.py, tools/prof_ops.py piped)"
+    return out
+
+
 def measured_mfma():
     """Per-op MFMA busy cycles from the committed rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES pass
     (tools/prof_ops.py mfma), {} if absent."""
@@ -390,21 +429,28 @@ def main():
         mf = measured_mfma().get(name)
         roof["rocprof_mfma_busy_frac"] = mf["util_peak_clock"] if mf else None
         roof["kernel"] = name
-        roof["avg_us"] = round(us, 2)
-        # the same op inside the measured step (committed rocprof trace of this bench): longer,
-        # since the front and back parts share every CU there
+        # `achieved` / `frac` / `avg_us`: the op INSIDE the timed step, where the front and back parts
+        # share every CU (committed rocprof trace of this bench, profiles/op_stats.csv); the same op
+        # replayed alone on the engine stream (HIP events, live in this run) is `*_alone`
+        roof["avg_us_alone"] = round(us, 2)
+        roof["achieved_alone"] = roof["achieved"]
+        roof["frac_alone"] = roof["frac"]
+        roof["avg_us"] = roof["avg_us_alone"]
+        roof["duration_source"] = "HIP events, op replayed alone (no committed in-step trace for it)"
         ius = measured_in_step(name)
         if ius:
             ach = by / (ius * 1e-6) / 1e9 if roof["unit"] == "GB/s" else fl / (ius * 1e-6) / 1e12
-            roof["in_step"] = {"avg_us": round(ius, 2), "achieved": round(ach, 2 if roof["unit"] != "GB/s" else 1),
-                               "frac": round(ach / roof["peak"], 4),
-                               "source": "profiles/op_stats.csv (rocprofv3 --kernel-trace of bench.py, "
-                                         "tools/prof_ops.py piped)"}
+            roof["avg_us"] = round(ius, 2)
+            roof["achieved"] = round(ach, 2 if roof["unit"] != "GB/s" else 1)
+            roof["frac"] = round(ach / roof["peak"], 4)
+            roof["duration_source"] = ("in-step average of its launches: profiles/op_stats.csv (rocprofv3 "
+                                       "--kernel-trace of bench.py, tools/prof_ops.py piped)")
         roof["algorithmic_bytes"] = by
         roof["algorithmic_flops"] = fl
         top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
         sum_ops_ms = round(sum(u for u, _, _, _ in per_op) / 1000.0, 3)
         roof["phases"] = phase_rooflines(per_op, plan, B, K, back_frames)
+        roof["step"] = step_roofline(plan, B, K, back_frames, 1000.0 * (elapsed - admit_s) / steps)
         if args.ops_out:
             with open(args.ops_out, "w") as f:
                 json.dump({"n_rows": B, "plan": [n for n, _, _ in plan],

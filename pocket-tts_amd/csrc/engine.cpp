@@ -1206,6 +1206,10 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   {  // conv0 (K = 7 x 512, M = 16 B rows): split-K fills the chip; bias + ELU in the reduce (every B:
      // at B = 1 the unsplit launch had 16 workgroups, 27.4 us)
     const BackTile tc = tile("seanet.conv0", 8);
+    if (big && tc.splits == 1) {  // unsplit: bias + ELU in the tile epilogue, no reduce launch
+      conv_op(ops, "seanet.conv0", mx_, B, 16 * nfr, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, W(L_.dc0_b),
+              nullptr, a0_, 16 * nfr, 1, tc.layout, 1, nullptr, 1);
+    } else {
     const int s_c0 = std::max(tc.splits, 2);
     conv_op(ops, "seanet.conv0", mx_, B, 16 * nfr, 512, hist_[0], 6, 1, 0, W(L_.dc0_w), 512, 7, 1, nullptr, nullptr,
             nullptr, 16 * nfr, 1, big ? tc.layout : 6, 0, nullptr, s_c0);
@@ -1219,6 +1223,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     r.Y = a0_;
     r.ldy = 512;
     ops.push_back(rr_op("seanet.conv0_reduce", r));
+    }
   }
   const float* cin_buf = a0_;
   int T = 16 * nfr, ch = 512;

@@ -1568,13 +1568,8 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
                                               const float* __restrict__ P, float* __restrict__ partial) {
   front_prio();
   constexpr int WK = 4 / WN, KS = KW * WK, NV = KW / 8, LDA = KS + 4;  // +4: conflict-free b128 rows
-  // X's slice and (WK > 1) the cross-wave reduction share one LDS block (a barrier between the
-  // last fragment read and the first partial write): 33 KB instead of 49 KB for linear2, so two
-  // workgroups fit beside a capped back-part workgroup on a CU
-  constexpr int SA = 32 * LDA, RED = WK > 1 ? 4 * 16 * 64 : 0;
-  __shared__ __attribute__((aligned(16))) float smem[SA > RED ? SA : RED];
-  float* const sA = smem;
-  float* const red = smem;
+  __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
+  __shared__ __attribute__((aligned(16))) float red[WK > 1 ? 4 * 16 * 64 : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = blockIdx.x, z = blockIdx.y, S = gridDim.y, m0 = 32 * blockIdx.z;  // z: K slice; blockIdx.z: 32-row block
@@ -1623,7 +1618,6 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   }
   // WK > 1: the WK waves of column block c (waves c, c + WN, ..) hold partials over their k
   // ranges; the 16 * WN (block, register) outputs are dealt 4 * WN per wave and summed in k order
-  __syncthreads();  // every wave's fragment reads of sA are done before red overwrites it
 #pragma unroll
   for (int g = 0; g < 16; ++g) red[(wave * 16 + g) * 64 + lane] = acc[g];
   __syncthreads();

@@ -170,6 +170,9 @@ class BatchScheduler:
         self.steps = 0
         self.row_frames = 0  # frames delivered (valid rows summed over steps)
         self.trace = bool(os.environ.get("PTTS_SERVE_TRACE"))
+        # called (under self.cv) with the new load whenever it changes: the multi-process server
+        # publishes it on its LoadBoard for the overflow redirect
+        self.on_load: Callable[[int], None] | None = None
         self.thread = threading.Thread(target=self._loop, name="ptts-scheduler", daemon=True)
         self.thread.start()
 
@@ -183,6 +186,8 @@ class BatchScheduler:
             if not self.running:
                 raise RuntimeError("scheduler stopped")
             self.waiting.append(req)
+            if self.on_load is not None:
+                self.on_load(len(self.active) + len(self.waiting))
             self.cv.notify()
         return req
 
@@ -269,6 +274,8 @@ class BatchScheduler:
                         with self.cv:
                             for slot in done:
                                 del self.active[slot]
+                            if self.on_load is not None:
+                                self.on_load(len(self.active) + len(self.waiting))
         except BaseException as e:  # deliver the failure to every waiting client
             with self.cv:
                 self.running = False
@@ -296,6 +303,63 @@ class MultiGpuScheduler:
     def close(self):
         for s in self.schedulers:
             s.close()
+
+
+class LoadBoard:
+    """Least-loaded dispatch for the multi-process server (BASELINE configs[3]: 256 streams over 8
+    GPUs). The kernel spreads connections over the workers of the shared SO_REUSEPORT port by a hash,
+    blind to load, and a keep-alive connection stays on its worker; so each worker publishes its
+    load (requests active + waiting) and the port of a private listener in one small file under
+    /dev/shm that every worker of the server maps, and a worker with no free slot answers a request
+    on the shared port with 307 (method and body kept) to the private port of the least-loaded peer
+    that has one. Requests on a private port are always served (a request is redirected at most
+    once). One int64 pair per rank: (load, private port)."""
+
+    def __init__(self, port: int, world: int, rank: int, max_rows: int, path: str | None = None):
+        import mmap
+
+        self.world, self.rank, self.max_rows = world, rank, max_rows
+        self.path = path or f"/dev/shm/ptts-serve-{port}-{world}.load"
+        size = 16 * world
+        fd = os.open(self.path, os.O_RDWR | os.O_CREAT, 0o600)
+        try:
+            if os.fstat(fd).st_size != size:
+                os.ftruncate(fd, size)
+            self._mm = mmap.mmap(fd, size)
+        finally:
+            os.close(fd)
+        self.v = np.frombuffer(self._mm, np.int64).reshape(world, 2)
+        self.private_port = 0
+
+    def publish(self, load: int):
+        self.v[self.rank, 0] = load
+
+    def set_private_port(self, port: int):
+        self.private_port = port
+        self.v[self.rank, 1] = port
+
+    def redirect_target(self, own_load: int) -> int | None:
+        """The private port of the least-loaded peer with a free slot, if this worker has none."""
+        if own_load < self.max_rows:
+            return None
+        loads, ports = self.v[:, 0].copy(), self.v[:, 1].copy()
+        best = None
+        for r in range(self.world):
+            if r != self.rank and ports[r] > 0 and loads[r] < self.max_rows and (best is None or loads[r] < loads[best]):
+                best = r
+        if best is None:
+            return None
+        self.v[best, 0] += 1  # claim the slot now: concurrent overflows spread instead of herding
+        return int(ports[best])
+
+    def close(self, unlink: bool = False):
+        self.v = None
+        self._mm.close()
+        if unlink:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
 
 
 # ---------------------------------------------------------------------------------------------
@@ -356,6 +420,7 @@ class TTSService:
 
 
 from pydantic import BaseModel  # noqa: E402  (request bodies; module level so FastAPI resolves them)
+from starlette.requests import Request as StarletteRequest  # noqa: E402
 
 
 class GenerateRequest(BaseModel):
@@ -451,6 +516,20 @@ def create_app(service: TTSService):
 
     worker = getattr(service, "worker", None) or {"rank": 0, "world": 1, "pid": os.getpid()}
     hdr = {"X-PTTS-Rank": str(worker["rank"])}
+    board: LoadBoard | None = getattr(service, "board", None)
+    shared_port = getattr(service, "shared_port", None)
+
+    def overflow(request):
+        """A 307 to the least-loaded peer's private port when this worker has no free slot and the
+        request came in on the shared port (LoadBoard); None to serve it here."""
+        if board is None or request.scope.get("server", (None, None))[1] != shared_port:
+            return None
+        from fastapi.responses import RedirectResponse
+
+        port = board.redirect_target(service.scheduler.load())
+        if port is None:
+            return None
+        return RedirectResponse(str(request.url.replace(port=port)), status_code=307, headers=hdr)
 
     @app.get("/health")
     def health():
@@ -459,20 +538,29 @@ def create_app(service: TTSService):
         return JSONResponse({"status": "healthy", "version": VERSION, "worker": worker, **stats}, headers=hdr)
 
     @app.post("/generate")
-    def generate(req: GenerateRequest):
+    def generate(req: GenerateRequest, request: StarletteRequest):
+        redirect = overflow(request)
+        if redirect is not None:
+            return redirect
         r = submit(**req.model_dump())
         return Response(wav_bytes(r.audio()), media_type="audio/wav", headers=hdr)
 
     @app.post("/stream")
-    async def stream(req: GenerateRequest):
+    async def stream(req: GenerateRequest, request: StarletteRequest):
         t_route = time.time()
+        redirect = overflow(request)
+        if redirect is not None:
+            return redirect
         r = submit(**req.model_dump())
         r.times["route"] = t_route
         return StreamingResponse(pcm_chunks(r), media_type="audio/pcm",
                                  headers={**hdr, "X-PTTS-Route-Time": f"{t_route:.6f}"})
 
     @app.post("/v1/audio/speech")
-    def openai_speech(req: OpenAIRequest):
+    def openai_speech(req: OpenAIRequest, request: StarletteRequest):
+        redirect = overflow(request)
+        if redirect is not None:
+            return redirect
         r = submit(text=req.input, token_ids=req.token_ids, voice=req.voice, words=req.words)
         audio = r.audio()
         if (req.response_format or "wav") == "pcm":
@@ -482,13 +570,21 @@ def create_app(service: TTSService):
     return app
 
 
+def stand_in_sample(u: int, k: int) -> float:
+    """The stand-in engine's sample value for utterance u (its first token id) at frame k: the
+    16-bit wire value (audio.rs:110-185: x 32767, truncated) is exactly (u % 128) * 256 + k % 256."""
+    return ((u % 128) * 256 + k % 256 + 0.5) / 32767.0
+
+
 class StandInEngine:
     """--stand-in-engine only (CPU; launcher and routing self-test of the multi-process server): the
     engine surface the scheduler drives, computing nothing. Row frames of utterance u (its first
-    token id) at step k hold u * 1000 + k, delivered one call late as by a pipelined engine."""
+    token id) at step k hold stand_in_sample(u, k), delivered one call late as by a pipelined
+    engine; step_s paces each step (sleep) like a GPU step."""
 
-    def __init__(self, max_slots=32, max_ctx=1024, **_):
+    def __init__(self, max_slots=32, max_ctx=1024, step_s=0.0, **_):
         self.max_slots, self.max_ctx, self.pipeline = max_slots, max_ctx, True
+        self.step_s = step_s
         self.rows, self.pending = {}, None
 
     @staticmethod
@@ -506,14 +602,16 @@ class StandInEngine:
     def open_many(self, slots, voices, ids_list, params_list):
         for s, ids, p in zip(slots, ids_list, params_list):
             self.rows[s] = [int(ids[0]) if len(ids) else 0, 0, p.max_frames]
-            if self.pending is not None:
+            if self.pending is not None and s < self.pending[1].size:  # drop the slot's undrained frame
                 self.pending[1][s] = False
 
     def step_async(self, n):
+        if self.step_s:
+            time.sleep(self.step_s)
         pcm, valid, last = np.zeros((n, FRAME), np.float32), np.zeros(n, bool), np.zeros(n, bool)
         for s, st in list(self.rows.items()):
             if s < n:
-                pcm[s], valid[s] = st[0] * 1000 + st[1], True
+                pcm[s], valid[s] = stand_in_sample(st[0], st[1]), True
                 st[1] += 1
                 last[s] = st[1] == st[2]
                 if last[s]:
@@ -539,7 +637,7 @@ class StandInEngine:
         pass
 
 
-def _listen_socket(host: str, port: int):
+def _listen_socket(host: str, port: int, reuse_port: bool = True):
     """A listening TCP socket with SO_REUSEPORT: every per-GPU worker process binds the same port
     and the kernel spreads incoming connections over them (no proxy process in the data path)."""
     import socket
@@ -550,7 +648,8 @@ def _listen_socket(host: str, port: int):
     so = socket.socket(socket.AF_INET, socket.SOCK_STREAM, socket.IPPROTO_TCP)
     so.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
     so.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-    so.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    if reuse_port:
+        so.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
     so.bind((host, port))
     so.listen(1024)
     return so
@@ -564,7 +663,10 @@ def _worker_engine(args, Engine):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    kw = dict(max_slots=args.slots, max_ctx=args.max_ctx, weights_path=args.weights, pipeline=True)
+    kw = dict(max_slots=args.slots, max_ctx=args.max_ctx, weights_path=args.weights, pipeline=True,
+              back_frames=args.back_frames)
+    if Engine is StandInEngine:
+        kw["step_s"] = args.stand_in_step_ms / 1000.0
     if "WORLD_SIZE" not in os.environ:  # a plain single-GPU server
         return Engine(device=local, **kw), 0, 1, None
     import torch
@@ -612,8 +714,14 @@ def main(argv=None):
     ap.add_argument("--max-ctx", type=int, default=1024)
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2),
+                    help="frames per Mimi decode pass (ptts_engine_config.back_frames): 2, the throughput "
+                         "configuration bench.py measures (two more calls of frame lag, ~1.2 ms at B = 32)")
     ap.add_argument("--stand-in-engine", action="store_true",
                     help="CPU self-test of the launcher and routing: a stand-in engine that computes nothing")
+    ap.add_argument("--stand-in-step-ms", type=float, default=0.0, help="--stand-in-engine: time per step")
+    ap.add_argument("--no-redirect", action="store_true",
+                    help="multi-process server: no overflow redirect to the least-loaded worker (LoadBoard)")
     args = ap.parse_args(argv)
     import sys
 
@@ -654,14 +762,28 @@ def main(argv=None):
             voices[name] = engine.voice_from_audio(audio[0], sr)
     if not voices:
         raise SystemExit("at least one --voice NAME=path is required")
-    service = TTSService(BatchScheduler(engine), voices, default_voice=next(iter(voices)),
+    scheduler = BatchScheduler(engine)
+    service = TTSService(scheduler, voices, default_voice=next(iter(voices)),
                          tokenizer=load_tokenizer(args.tokenizer) if args.tokenizer else None)
     service.worker = {"rank": rank, "world": world, "pid": os.getpid(), "weights_checksum": checksum}
+    socks = [_listen_socket(args.host, args.port)]
+    board = None
+    if world > 1 and not args.no_redirect:  # least-loaded dispatch across the workers (LoadBoard)
+        board = LoadBoard(args.port, world, rank, scheduler.max_rows)
+        board.publish(0)
+        priv = _listen_socket(args.host, 0, reuse_port=False)
+        board.set_private_port(priv.getsockname()[1])
+        socks.append(priv)
+        scheduler.on_load = board.publish
+        service.board, service.shared_port = board, args.port
     import uvicorn
 
     app = create_app(service)
-    so = _listen_socket(args.host, args.port)
-    uvicorn.Server(uvicorn.Config(app, log_level="warning")).run(sockets=[so])
+    try:
+        uvicorn.Server(uvicorn.Config(app, log_level="warning")).run(sockets=socks)
+    finally:
+        if board is not None:
+            board.close(unlink=rank == 0)
 
 
 if __name__ == "__main__":

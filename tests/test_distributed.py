@@ -74,7 +74,8 @@ def test_replicas_gloo_world2():
         assert n_seeds == 64  # utterance noise streams never collide across ranks
 
 
-def test_bench_gpus_flag_launches_replica_ranks():
+@pytest.mark.parametrize("gpus", [2, 8])
+def test_bench_gpus_flag_launches_replica_ranks(gpus):
     """`bench.py --gpus 2` outside a torch.distributed environment re-launches itself as 2 ranks
     under torch.distributed.run (a child process, never exec), each rank runs its replica, rank 0
     reports the whole job: n_gpus 2, "replicas x2", global batch 2 x 32, 125-frame utterances and
@@ -83,14 +84,15 @@ def test_bench_gpus_flag_launches_replica_ranks():
     import subprocess
     import sys
 
-    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--launcher-selftest", "--steps", "20",
-                        "--warmup", "1"], capture_output=True, text=True, timeout=240)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--launcher-selftest", "--steps",
+                        "20", "--warmup", "1"], capture_output=True, text=True, timeout=400,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1  # only rank 0 prints
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "replicas x2"
-    assert out["config"]["global_batch"] == 64 and out["config"]["utterance_frames"] == 125
+    assert out["n_gpus"] == gpus and out["config"]["parallelism"] == f"replicas x{gpus}"
+    assert out["config"]["global_batch"] == 32 * gpus and out["config"]["utterance_frames"] == 125
     assert out["steps"] == 16 * 125 and out["steps_requested"] == 20 and out["scaling"] == "weak"
     pj = out["per_job"]
     assert pj["jobs"] == 16 and pj["min"] <= pj["median"] <= pj["max"]

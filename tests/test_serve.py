@@ -235,3 +235,96 @@ def test_token_ids_need_a_word_count():
         assert r.status_code == 200 and len(r.content) == 44 + (6 + 2) * 13 * 1920 * 2
     finally:
         sch.close()
+
+
+def _start_server(tmp_path, gpus, slots, extra=()):
+    import os
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    import httpx
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    np.save(tmp_path / "v.npy", np.zeros((4, 1024), np.float32))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=os.path.join(root, "pocket-tts_amd"), OMP_NUM_THREADS="1")
+    p = subprocess.Popen([sys.executable, "-m", "pocket_tts_amd.serve", "--gpus", str(gpus), "--stand-in-engine",
+                          "--port", str(port), "--slots", str(slots), "--voice", f"v={tmp_path / 'v.npy'}", *extra],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    base = f"http://127.0.0.1:{port}"
+    deadline = time.time() + 240
+    ranks = set()
+    while len(ranks) < gpus:  # every worker up (fresh connections land on different workers)
+        try:
+            ranks.add(httpx.get(base + "/health", timeout=2).json()["worker"]["rank"])
+        except (httpx.HTTPError, KeyError):
+            time.sleep(0.5)
+        assert p.poll() is None and time.time() < deadline, p.stdout.read().decode()[-3000:]
+    return p, base
+
+
+def _stop_server(p):
+    import os
+    import signal
+    import subprocess
+
+    os.killpg(p.pid, signal.SIGTERM)
+    try:
+        p.wait(timeout=30)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+
+
+@pytest.mark.timeout(600)
+def test_configs3_256_streams_over_8_workers(tmp_path):
+    """BASELINE configs[3] readiness on the CPU: `serve --gpus 8` (8 worker processes, stand-in
+    engines paced at 1 ms per step, 32 slots each, gloo) under 256 concurrent /stream clients, two
+    bursts. Every stream completes with exactly its frames on the wire (audio.rs:110-185 rule:
+    the stand-in's samples are exact 16-bit codes), and the load spreads: the SO_REUSEPORT hash is
+    blind to load, so a worker with no free slot sends the request (307) to the least-loaded peer
+    (LoadBoard); no worker serves less than half its 32-stream share. Replaces the reference's
+    one-mutex server (pocket-tts-cli/src/server/handlers.rs:215-306, state.rs:66-69)."""
+    import asyncio
+    import collections
+
+    import httpx
+
+    from pocket_tts_amd.serve import stand_in_sample
+
+    n_frames, n_streams = 40, 256
+    p, base = _start_server(tmp_path, 8, 32, ("--stand-in-step-ms", "1"))
+    try:
+        async def one(client, u):
+            body = {"token_ids": [u, 5, 6], "max_frames": n_frames, "eos_threshold": 1e9}
+            chunks = []
+            async with client.stream("POST", base + "/stream", json=body) as r:
+                assert r.status_code == 200
+                rank = int(r.headers["x-ptts-rank"])
+                redirected = bool(r.history)
+                async for c in r.aiter_bytes():
+                    chunks.append(c)
+            pcm = np.frombuffer(b"".join(chunks), "<i2")
+            assert pcm.size == n_frames * 1920, (u, pcm.size)
+            want = np.repeat([int(round(stand_in_sample(u, k) * 32767 - 0.5)) for k in range(n_frames)], 1920)
+            assert np.array_equal(pcm, want), u
+            return rank, redirected
+
+        async def burst(first):
+            limits = httpx.Limits(max_connections=n_streams + 8, max_keepalive_connections=n_streams + 8)
+            async with httpx.AsyncClient(timeout=120, limits=limits, follow_redirects=True) as client:
+                return await asyncio.gather(*(one(client, first + i) for i in range(n_streams)))
+
+        for b in range(2):
+            res = asyncio.run(burst(1000 * b))
+            per_rank = collections.Counter(r for r, _ in res)
+            print(f"burst {b}: streams per worker {dict(sorted(per_rank.items()))}, "
+                  f"redirected {sum(x for _, x in res)}")
+            assert len(res) == n_streams and sorted(per_rank) == list(range(8)), per_rank
+            assert min(per_rank.values()) >= 16, per_rank
+    finally:
+        _stop_server(p)
