@@ -270,7 +270,8 @@ def main():
     ap.add_argument("--ops-out", default="", help="write per-op timings of the step plan (JSON)")
     ap.add_argument("--no-op-times", action="store_true", help="skip the per-op HIP-event pass (PMC runs)")
     ap.add_argument("--no-quant-variant", action="store_true",
-                    help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM) and fp8_gemm engines")
+                    help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM), fp8_gemm and "
+                         "back_bf16 engines")
     ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2),
                     help="frames per Mimi-decode pass of pipelined stepping (ptts_engine_config.back_frames; "
                          "2, the throughput configuration: 0.559 vs 0.584 ms per steady step, DESIGN.md section 1)")
@@ -389,6 +390,22 @@ def main():
             elapsed, admit_s, *job_s = max_over_ranks(dist, [elapsed, admit_s, *job_s], dev)
         return elapsed, admit_s, job_s
 
+    def pcm_sample(e, n_frames=24):
+        """Every row's PCM of n_frames frames at temp 0 (no EOS) from the bench's voice and texts:
+        [rows][frames][1920] (the bf16 variant's accuracy against this engine's f32 PCM)."""
+        voice = e.voice_from_prompt(synth_prompt())
+        e.open_many(list(range(B)), [voice] * B, [text_ids(b) for b in range(B)],
+                    [pt.GenerationParams(temp=0.0, eos_threshold=float("inf"), max_frames=n_frames, seed=b + 1)
+                     for b in range(B)])
+        out = [[] for _ in range(B)]
+        for _ in range(n_frames + sum(e.frame_lag())):
+            r = e.step(B)
+            for b in range(B):
+                if r.valid[b]:
+                    out[b].append(r.pcm[b].copy())
+        assert all(len(o) == n_frames for o in out)
+        return np.asarray(out, np.float64)
+
     elapsed, admit_s, job_s = timed_job(eng)
     steps = jobs * K
 
@@ -480,7 +497,8 @@ def main():
     # quantization of the FlowLM (quantize.rs; its step GEMMs stream int8 codes), and with the
     # large FlowLM step GEMMs as fp8 W8A8 (accuracy-gated against the f32 oracle, tests/test_fp8.py).
     # Reported beside `value`, never as it (different numerics from the f32 reference).
-    quant = fp8 = None
+    quant = fp8 = bf16 = None
+    ref_pcm = pcm_sample(eng) if not args.no_quant_variant and world == 1 and not selftest else None
     eng.close()  # one engine on the GPU at a time
     if not args.no_quant_variant and world == 1:
         eq = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
@@ -502,6 +520,24 @@ def main():
                        "activation scales), FlowLM qkv/linear1/linear2/adaLN",
                "fp8_matrices": ef.fp8_matrices}
         ef.close()
+        # the Mimi decode (back part) on bf16 MFMA: the same job, and its PCM against the f32
+        # engine's (= the f32 oracle within 1e-7, tests/test_gpu_bench_shape.py) on a 24-frame sample
+        eb = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
+                       pipeline=pipeline, back_frames=back_frames, back_bf16=True)
+        b_el, b_ad, _ = timed_job(eb)
+        bp = pcm_sample(eb)
+        eb.close()
+        err = ((bp - ref_pcm) ** 2).sum(-1)
+        snr = 10 * np.log10((ref_pcm ** 2).sum(-1) / np.maximum(err, 1e-30))
+        bf16 = {"value": round(jobs * B * K * 1920 / 24000.0 / b_el, 2), "unit": "audio-sec/wall-sec",
+                "ms_per_step": round(1000.0 * b_el / steps, 4),
+                "steady_ms_per_step": round(1000.0 * (b_el - b_ad) / steps, 4),
+                "mfma": "Mimi decoder transformer GEMMs + SEANet decoder convs on v_mfma_f32_32x32x16_bf16 "
+                        "(operands rounded to bf16, f32 accumulation); FlowLM, attention, final conv f32",
+                "pcm_snr_db_vs_f32": {"min": round(float(snr.min()), 2), "median": round(float(np.median(snr)), 2),
+                                      "frames": int(snr.size), "gate_min": 30.0},
+                "latents_eos_stop_frames": "unchanged (f32 FlowLM; the back part does not feed it): "
+                                           "tests/test_gpu_bf16.py"}
 
     # ---- CPU baseline: the oracle (C restatement of the reference algorithm) on the host cores,
     # the same 125-frame job per utterance (oracle/cpu_baseline.py, a child process)
@@ -554,6 +590,7 @@ def main():
         "p50_first_chunk_ms": None if p50 is None else round(p50, 3),
         "int8_flowlm_variant": quant,
         "fp8_flowlm_variant": fp8,
+        "bf16_back_variant": bf16,
         "roofline": roof,
         "cpu_baseline": cpu,
         "top_ops": top,

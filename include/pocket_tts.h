@@ -31,10 +31,10 @@ extern "C" {
 #define PTTS_ERR_IO 4      /* weights file missing or malformed */
 
 /* ABI version of this header. Bumped whenever a struct below changes layout (3: cfg_yaml was
- * appended to ptts_engine_config; 4: back_frames). A caller checks ptts_abi_version() ==
+ * appended to ptts_engine_config; 4: back_frames; 5: back_bf16). A caller checks ptts_abi_version() ==
  * PTTS_ABI_VERSION before passing any struct: a library built from another header reads a
  * different layout. */
-#define PTTS_ABI_VERSION 4
+#define PTTS_ABI_VERSION 5
 int ptts_abi_version(void);
 /* Build id of the loaded library: the first 16 hex digits of the sha256 over the sources it was
  * built from (pocket-tts_amd/Makefile, BUILD_ID), with "+probes" appended for a measurement build
@@ -92,6 +92,13 @@ typedef struct ptts_engine_config {
                                first). ptts_frame_lag() reports both delays. 2 is the
                                throughput setting (bench.py's default: 0.561 against 0.583 ms per
                                steady step at B = 32), 1 the low-latency one. */
+  int back_bf16;            /* 1: the Mimi decoder transformer GEMMs and the SEANet decoder convs
+                               (the back part, at >= 16 rows) multiply on
+                               v_mfma_f32_32x32x16_bf16: operands rounded to bf16, f32
+                               accumulation, f32 activations and weights in HBM. Not a reference
+                               numeric (Candle runs f32): gated on PCM accuracy vs the f32 path;
+                               the latents, EOS logits and stop frames are untouched (the back part
+                               does not feed the FlowLM). 0 = f32 (default). */
 } ptts_engine_config;
 
 #define PTTS_QUANT_NONE 0
@@ -180,6 +187,13 @@ int ptts_voice_from_audio(ptts_engine* e, const float* samples, int n_samples, i
  * rates divided by their gcd. */
 int ptts_resample_len(int n_samples, int sr_from, int sr_to);
 int ptts_resample(ptts_engine* e, const float* x, int n_samples, int sr_from, int sr_to, float* y);
+/* Test hook of the GEMM core (no reference counterpart): y = x w^T for x [m][k], w [n][k] (host
+ * buffers, k % 32 == 0) on the engine's device, with the tile of kernel layout `layout`
+ * (kernels.hip gemm_launch: the f32 tiles, and + 100 for their bf16-operand twins); splits > 1
+ * writes the [splits][m][n] split-K partial slabs to y, tail_slices > 0 takes the split-tail path
+ * (layouts 34 / 35). The tests run every shipped layout on shapes the model never runs. */
+int ptts_test_gemm(ptts_engine* e, int layout, int m, int n, int k, int splits, int tail_slices, const float* x,
+                   const float* w, float* y);
 /* Conditioning rows the voice holds (frames). */
 int ptts_voice_len(const ptts_voice* v);
 /* The [n_frames x 1024] conditioning a PCM voice was built from (host copy); for tests. */

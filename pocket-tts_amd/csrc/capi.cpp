@@ -183,6 +183,11 @@ int ptts_resample(ptts_engine* e, const float* x, int n_samples, int sr_from, in
   return guard([&] { eng(e).resample_host(x, n_samples, sr_from, sr_to, y); });
 }
 
+int ptts_test_gemm(ptts_engine* e, int layout, int m, int n, int k, int splits, int tail_slices, const float* x,
+                   const float* w, float* y) {
+  return guard([&] { eng(e).test_gemm(layout, m, n, k, splits, tail_slices, x, w, y); });
+}
+
 int ptts_voice_len(const ptts_voice* v) { return v ? v->F : 0; }
 
 int ptts_voice_conditioning(const ptts_voice* v, float* out, int max_rows) {

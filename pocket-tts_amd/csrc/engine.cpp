@@ -51,7 +51,7 @@ static void tile_override(const std::string& name, int& layout, int& ksplit) {
 // layouts served by k_gemm_glds (kernels.hip gemm_launch): the only ones that split a conv's K
 static bool lds_dma_layout(int layout) {
   return (layout >= 6 && layout <= 8) || (layout >= 11 && layout <= 16) || (layout >= 21 && layout <= 27) ||
-         (layout >= 30 && layout <= 42);
+         (layout >= 30 && layout <= 42) || (layout >= 130 && layout <= 139);
 }
 
 float* Engine::dalloc(size_t n) {
@@ -82,6 +82,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
   fp8_ = cfg.fp8_gemm;
   PTTS_REQUIRE(cfg.back_frames >= 0 && cfg.back_frames <= 2, "back_frames must be 0, 1 or 2");
   nfr_ = cfg.pipeline && cfg.back_frames == 2 ? 2 : 1;
+  PTTS_REQUIRE(cfg.back_bf16 == 0 || cfg.back_bf16 == 1, "back_bf16 must be 0 or 1");
+  back_bf16_ = cfg.back_bf16 != 0;
   nhb_ = nfr_ == 2 ? NHB : 3;
   int ndev = 0;
   PTTS_HIP(hipGetDeviceCount(&ndev));
@@ -1071,6 +1073,9 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   const bool big = B >= 16;  // B * 16 >= 256 Mimi rows: the LDS-DMA tiles fill the chip
   auto tile = [&](const std::string& op, int small_splits) {
     BackTile t = big ? back_tile(op, pipeline_) : BackTile{0, small_splits};
+    // back_bf16: the bf16-operand twin of the ILV tile (kernels.hip PTTS_GLB: layout + 100); the
+    // register-blocked and non-ILV tiles of the f32 table map to the 64 x 64 one
+    if (big && back_bf16_) t.layout = 100 + (t.layout == 35 || t.layout == 31 ? t.layout : 32);
     tile_override(op, t.layout, t.splits);  // probe builds only (tools/back_tune.py)
     return t;
   };
@@ -1257,7 +1262,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     // PTTS_RESBLOCK_STAGES (probe builds): bit mask of the stages that fuse.
     int fused_stages = 4;
     if (probe_env("PTTS_RESBLOCK_STAGES")) fused_stages = atoi(probe_env("PTTS_RESBLOCK_STAGES"));
-    if (big && (fused_stages >> i & 1)) {
+    if (big && (fused_stages >> i & 1) && !back_bf16_) {  // (f32 only: its own MFMA loop)
       const ResBlockArgs rb{ce_[i], hist_[2 + 2 * i], cb_[i], W(L_.dra_w[i]), W(L_.dra_b[i]), W(L_.drb_w[i]),
                             W(L_.drb_b[i]), ca_[i], B, T, ch};
       const double hd = ch / 2;
@@ -1515,6 +1520,61 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
       else memset(lat + (size_t)b * LDIM, 0, sizeof(float) * LDIM);
     }
   }
+}
+
+// GEMM-core test hook: one dense GEMM (mode 0) on the given tile layout, split-K slabs (splits > 1:
+// Y receives the [splits][M][N] partial slabs) or the split tail (tail_S > 0, layouts 34 / 35),
+// from host operands; the tests compare it with an fp64 product (every shipped layout, shapes the
+// model never runs).
+void Engine::test_gemm(int layout, int M, int N, int K, int splits, int tail_S, const float* X, const float* Wt,
+                       float* Y) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
+  PTTS_REQUIRE(X && Wt && Y && M >= 1 && N >= 1 && K >= 32 && K % 32 == 0, "test_gemm: bad shape");
+  PTTS_REQUIRE(splits >= 1 && splits <= 16 && (splits == 1 || tail_S == 0), "test_gemm: bad split");
+  sync();
+  const int Nw = (N + 31) / 32 * 32;
+  float *dx = nullptr, *dw = nullptr, *dy = nullptr;
+  PTTS_HIP(hipMalloc(&dx, sizeof(float) * M * K));
+  PTTS_HIP(hipMalloc(&dw, sizeof(float) * Nw * K));
+  PTTS_HIP(hipMalloc(&dy, sizeof(float) * splits * M * N));
+  try {
+    PTTS_HIP(hipMemsetAsync(dw, 0, sizeof(float) * Nw * K, stream_));
+    PTTS_HIP(hipMemcpyAsync(dx, X, sizeof(float) * M * K, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(dw, Wt, sizeof(float) * N * K, hipMemcpyHostToDevice, stream_));
+    GemmArgs a{};
+    a.mode = 0;
+    a.layout = layout;
+    a.M = M;
+    a.N = N;
+    a.K = K;
+    a.Nw = Nw;
+    a.X = dx;
+    a.ldx = K;
+    a.W = dw;
+    a.S = splits;
+    if (splits > 1) {
+      a.partial = dy;
+    } else {
+      a.Y = dy;
+      a.ldy = N;
+    }
+    if (tail_S > 0) {
+      a.tail_S = tail_S;
+      a.tail_slab = tslab_;
+      a.tail_cap = (long)TAIL_CAP;
+      a.tickets = tickets_;
+      a.tickets_cap = TICKETS;
+    }
+    gemm(a, splits, stream_);
+    PTTS_HIP(hipGetLastError());
+    PTTS_HIP(hipMemcpyAsync(Y, dy, sizeof(float) * splits * M * N, hipMemcpyDeviceToHost, stream_));
+    PTTS_HIP(hipStreamSynchronize(stream_));
+  } catch (...) {
+    (void)hipStreamSynchronize(stream_);
+    (void)hipFree(dx), (void)hipFree(dw), (void)hipFree(dy);
+    throw;
+  }
+  (void)hipFree(dx), (void)hipFree(dw), (void)hipFree(dy);
 }
 
 double Engine::time_op(int B, const std::string& name, int reps) {

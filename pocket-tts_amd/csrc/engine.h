@@ -62,6 +62,8 @@ class Engine {
   void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat, int calls_back = 0);
 
   double time_op(int B, const std::string& name, int reps);
+  // GEMM-core test hook (ptts_test_gemm): Y = X W^T on tile `layout` (host buffers)
+  void test_gemm(int layout, int M, int N, int K, int splits, int tail_S, const float* X, const float* Wt, float* Y);
   void overlap_probe(int B, int reps, double* us);
   std::vector<std::string> plan_names(int B);
   int int8_matrices() const { return (int)q8map_.size(); }
@@ -176,6 +178,7 @@ class Engine {
   static constexpr int NHB = 6;
   int nhb_ = 3;  // buffers in use: 3, or NHB = 6 with frame pairs
   int nfr_ = 1;  // frames per back-part pass (ptts_engine_config.back_frames)
+  bool back_bf16_ = false;  // ptts_engine_config.back_bf16: the back part's tiles on bf16 MFMA
   int rows_hb_[NHB] = {};  // rows of the front part that filled each hand-off buffer
   // frame-pair mode: PCM of one pair [B][2][1920] per pair parity, and its pinned host copy
   float* pcmp_[NHB / 2] = {};

@@ -598,7 +598,13 @@ __device__ __forceinline__ unsigned lds_addr(const float* p) {
 // SIMD = MINB). ILV: the DMAs of chunk c + NBUF - 1 are issued between the MFMAs of chunk c (one
 // per 16 / IPW k-steps) instead of as a burst ahead of its fragment reads: an f32 MFMA leaves 56
 // of its 64 issue cycles free, so the DMA issue (60-185 cycles each) hides behind the matrix pipe.
-template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1, int MINB = 1, bool ILV = false>
+// BF16 (engine back_bf16, a variant beside the f32 path): the same tiles, operands still f32 in
+// HBM and LDS, rounded to bf16 (v_cvt_pk_bf16_f32, RNE) as the fragments are read, and multiplied
+// on v_mfma_f32_32x32x16_bf16 with f32 accumulation: lane half h feeds elements j of MFMA q from
+// its chunk columns 16h + 8q + j for A and B alike, so each chunk's 32 k are summed once (2 MFMAs
+// per 32-k chunk instead of 16). The next chunk's DMAs are issued after the two MFMAs.
+template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1, int MINB = 1, bool ILV = false,
+          bool BF16 = false>
 __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
   if (a.front) front_prio();
   constexpr int TM = 32 * WM * TMW, TN = 32 * WN * TNW, ROWS = TM + TN;
@@ -773,7 +779,35 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
             bf[jj][4 * i + 0] = y.x; bf[jj][4 * i + 1] = y.y; bf[jj][4 * i + 2] = y.z; bf[jj][4 * i + 3] = y.w;
           }
         }
-        if (!(PTTS_PROBE(a) & 1)) {
+        if (BF16) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            bf16x8 ab[TMW], bb[TNW];
+#pragma unroll
+            for (int ii = 0; ii < TMW; ++ii) {
+              floatx8 v;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = af[ii][8 * q + j];
+              ab[ii] = __builtin_convertvector(v, bf16x8);
+            }
+#pragma unroll
+            for (int jj = 0; jj < TNW; ++jj) {
+              floatx8 v;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = bf[jj][8 * q + j];
+              bb[jj] = __builtin_convertvector(v, bf16x8);
+            }
+#pragma unroll
+            for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+              for (int jj = 0; jj < TNW; ++jj)
+                acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab[ii], bb[jj], acc[ii][jj], 0, 0, 0);
+          }
+          if (ILV && pf) {
+#pragma unroll
+            for (int ins = 0; ins < IPW; ++ins) dma(nsrc[ins], pbuf, ins);
+          }
+        } else if (!(PTTS_PROBE(a) & 1)) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
 #pragma unroll
@@ -1472,6 +1506,22 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     PTTS_GLX(39, 2, 2, 3, 1, 2, 2)  //  64 x 128, 2 per CU
 #endif
 #undef PTTS_GLX
+    // bf16 operands (GemmArgs layout + 100; engine back_bf16): the ILV tiles of the back part
+#define PTTS_GLB(L, WM_, WN_, NB_, TMW_, TNW_, MINB_)                                                 \
+  case 100 + L:                                                                                       \
+    launch_tiled((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_, MINB_, true, true>),                \
+                 dim3((a.N + 32 * WN_ * TNW_ - 1) / (32 * WN_ * TNW_),                                \
+                      (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z), 256, s, a);            \
+    return;
+    PTTS_GLB(32, 2, 2, 3, 1, 1, 2)  //  64 x  64, 2 per CU
+    PTTS_GLB(35, 2, 2, 2, 2, 1, 2)  // 128 x  64, 2 per CU
+    PTTS_GLB(31, 2, 2, 2, 2, 2, 2)  // 128 x 128, 2 per CU
+#ifdef PTTS_PROBES
+    PTTS_GLB(30, 2, 2, 3, 2, 2, 1)  // 128 x 128
+    PTTS_GLB(36, 2, 2, 3, 1, 2, 1)  //  64 x 128
+    PTTS_GLB(39, 2, 2, 3, 1, 2, 2)  //  64 x 128, 2 per CU
+#endif
+#undef PTTS_GLB
     default:
       break;
   }

@@ -18,7 +18,7 @@ LDIM = 32
 DIM = 1024
 SAMPLE_RATE = 24000
 QUANT_NONE, QUANT_FLOW_LM, QUANT_ALL = 0, 1, 2
-ABI_VERSION = 4  # PTTS_ABI_VERSION of include/pocket_tts.h that the structs below mirror
+ABI_VERSION = 5  # PTTS_ABI_VERSION of include/pocket_tts.h that the structs below mirror
 
 F32P = C.POINTER(C.c_float)
 U8P = C.POINTER(C.c_uint8)
@@ -40,6 +40,7 @@ class EngineConfig(C.Structure):
         ("fp8_gemm", C.c_int),
         ("cfg_yaml", C.c_char_p),
         ("back_frames", C.c_int),
+        ("back_bf16", C.c_int),
     ]
 
 
@@ -77,6 +78,7 @@ SIGNATURES = [
     ("ptts_voice_from_audio", C.c_int, [C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     ("ptts_resample_len", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("ptts_resample", C.c_int, [C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, F32P]),
+    ("ptts_test_gemm", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, F32P, F32P, F32P]),
     ("ptts_voice_len", C.c_int, [C.c_void_p]),
     ("ptts_voice_conditioning", C.c_int, [C.c_void_p, F32P, C.c_int]),
     ("ptts_voice_destroy", None, [C.c_void_p]),

@@ -68,7 +68,7 @@ class Engine:
     def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
                  seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
                  defer_weights: bool = False, pipeline: bool = False, weight_quant: int = 0, fp8_gemm: bool = False,
-                 cfg_yaml: str | None = None, back_frames: int = 1):
+                 cfg_yaml: str | None = None, back_frames: int = 1, back_bf16: bool = False):
         """pipeline=True: overlapped stepping, each step() returns the frame produced by the
         previous call (see ptts_engine_config.pipeline). weight_quant: QUANT_NONE / QUANT_FLOW_LM /
         QUANT_ALL, the reference's simulated int8 weight quantization (quantize.rs), with the
@@ -76,11 +76,13 @@ class Engine:
         fp8 W8A8 MFMA (accuracy-gated; see ptts_engine_config.fp8_gemm). cfg_yaml: the reference's
         model config (config/b6369a24.yaml), checked against the compiled dimensions.
         back_frames=2 (pipelined only): two frames per Mimi-decode pass; a step() returns the frame
-        computed three calls earlier (`frame_lag`)."""
+        computed three calls earlier (`frame_lag`). back_bf16=True: the Mimi decode's GEMMs and convs
+        on bf16 MFMA (f32 accumulation; a variant gated on PCM accuracy, ptts_engine_config.back_bf16)."""
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
                            weight_blob or None, int(defer_weights), int(pipeline), int(weight_quant),
-                           int(fp8_gemm), cfg_yaml.encode() if cfg_yaml else None, int(back_frames))
+                           int(fp8_gemm), cfg_yaml.encode() if cfg_yaml else None, int(back_frames),
+                           int(back_bf16))
         h = C.c_void_p()
         check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
         self.handle = h
@@ -90,6 +92,18 @@ class Engine:
         self.lsd_decode_steps = lsd_decode_steps
         self.pipeline = bool(pipeline)
         self.back_frames = int(back_frames) if pipeline else 1
+        self.back_bf16 = bool(back_bf16)
+
+    def test_gemm(self, layout: int, x: np.ndarray, w: np.ndarray, splits: int = 1, tail_slices: int = 0) -> np.ndarray:
+        """GEMM-core test hook (ptts_test_gemm): x [m][k] @ w [n][k]^T on tile `layout`; splits > 1
+        returns the [splits][m][n] partial slabs."""
+        x = np.ascontiguousarray(x, np.float32)
+        w = np.ascontiguousarray(w, np.float32)
+        m, k = x.shape
+        n = w.shape[0]
+        y = np.empty((splits, m, n) if splits > 1 else (m, n), np.float32)
+        check(lib().ptts_test_gemm(self.handle, layout, m, n, k, splits, tail_slices, fptr(x), fptr(w), fptr(y)))
+        return y
 
     def frame_lag(self) -> tuple[int, int]:
         """(lag, admit_delay): a frame arrives `lag` calls after the call that computed it; the
