@@ -467,7 +467,7 @@ def main():
         top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
         sum_ops_ms = round(sum(u for u, _, _, _ in per_op) / 1000.0, 3)
         roof["phases"] = phase_rooflines(per_op, plan, B, K, back_frames)
-        roof["step"] = step_roofline(plan, B, K, back_frames, 1000.0 * (elapsed - admit_s) / steps)
+        roof["step"] = step_roofline(plan, B, K, back_frames, 1e6 * (elapsed - admit_s) / steps)
         if args.ops_out:
             with open(args.ops_out, "w") as f:
                 json.dump({"n_rows": B, "plan": [n for n, _, _ in plan],
