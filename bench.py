@@ -213,6 +213,9 @@ class _SelftestEngine:
         for s in self.frames:
             self.frames[s] += 1
 
+    def flush_async(self, n):
+        time.sleep(1e-4)
+
     def sync(self):
         pass
 
@@ -275,6 +278,9 @@ def main():
     ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2),
                     help="frames per Mimi-decode pass of pipelined stepping (ptts_engine_config.back_frames; "
                          "2, the throughput configuration: 0.559 vs 0.584 ms per steady step, DESIGN.md section 1)")
+    ap.add_argument("--no-flush", action="store_true",
+                    help="drain each job's last frames with step calls (front parts of finished rows run and "
+                         "their frames are discarded) instead of ptts_flush_async")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sequential stepping (no FlowLM / Mimi overlap across consecutive frames)")
     ap.add_argument("--profile-frames", type=int, default=0,
@@ -360,10 +366,19 @@ def main():
             eng.open_many(list(range(B)), [voice] * B, [text_ids(b) for b in range(B)],
                           [params(round_id, b, n_frames) for b in range(B)])
 
+        def run_calls(n_frames):
+            """n_frames step calls (+ one when the admission starts a call late), then frame_lag()
+            flush calls: they decode and deliver the frames already computed without running front
+            parts for rows that have all finished (ptts_flush_async; a frame arrives lag calls late)"""
+            lag, delay = eng.frame_lag()
+            for _ in range(n_frames + delay):
+                eng.step_async(B)
+            for _ in range(lag):
+                eng.flush_async(B) if pipeline and not args.no_flush else eng.step_async(B)
+
         # warmup: a short job on the same rows (graph capture, caches), then the rows are re-admitted
         admit(0, max(1, W))
-        for _ in range(max(1, W) + sum(eng.frame_lag())):  # a frame arrives frame_lag() calls late
-            eng.step_async(B)
+        run_calls(max(1, W))
         eng.sync()
         barrier()
         eng.sync()
@@ -375,9 +390,7 @@ def main():
             admit(1 + j, K)
             eng.sync()
             admit_s += time.perf_counter() - ta0
-            calls = K + sum(eng.frame_lag())  # the K frames, then the calls that drain the last one
-            for _ in range(calls):
-                eng.step_async(B)
+            run_calls(K)  # the K frames, then the calls that drain the last one
             eng.sync()
             r = eng.fetch(B)  # the last frame of every row, from pinned host memory
             assert r.valid.all() and r.last.all(), "bench produced invalid frames"

@@ -224,6 +224,14 @@ int ptts_step(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint
               float* eos_logits, float* latents);
 /* Same step, enqueued only (outputs stay in HBM); use ptts_sync() + ptts_fetch(). */
 int ptts_step_async(ptts_engine* e, int n_rows);
+/* Pipelined engines: a call that starts no frame. The frames already computed advance through
+ * the back part and are returned as by ptts_step_async (fetch after it as usual), but no row
+ * computes a new frame: every row pauses for this call, as rows past n_rows do. A caller whose
+ * rows have all finished drains the pipeline with it (ptts_frame_lag() calls) without running
+ * front parts whose frames would be discarded. Not valid right after an admission
+ * (PTTS_ERR_INVALID: the admitted rows' first frame must fall on a step call). No reference
+ * counterpart (the reference does not pipeline). */
+int ptts_flush_async(ptts_engine* e, int n_rows);
 int ptts_sync(ptts_engine* e);
 int ptts_fetch(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
                float* eos_logits, float* latents);

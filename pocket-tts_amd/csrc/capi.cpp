@@ -248,6 +248,8 @@ int ptts_step(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint
 
 int ptts_step_async(ptts_engine* e, int n_rows) { return guard([&] { eng(e).step_async(n_rows); }); }
 
+int ptts_flush_async(ptts_engine* e, int n_rows) { return guard([&] { eng(e).flush_async(n_rows); }); }
+
 int ptts_sync(ptts_engine* e) { return guard([&] { eng(e).sync(); }); }
 
 int ptts_fetch(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last, float* eos_logits,

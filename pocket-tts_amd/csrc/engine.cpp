@@ -1400,18 +1400,43 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
 //               waits only for back(k - nhb_), the last reader of its buffer, and back(k-1) for
 //               front(k-1).
 void Engine::step_async(int B) {
-  PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
+  call_async(B, true);
+}
+
+// A flush call: frames already computed are decoded and delivered as by a step call, but no row
+// computes a new frame (every row pauses for the call, as rows past n_rows do). Pipelined engines
+// only, and not right after an admission (the admitted rows' first frame must fall on a step
+// call: with frame pairs it must be the first frame of a pair).
+void Engine::flush_async(int B) {
+  PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
+  PTTS_REQUIRE(pipeline_, "flush: pipelined engines only");
+  PTTS_REQUIRE(!admitted_since_call_ && act_slots_.empty(), "flush right after an admission: step first");
+  call_async(B, false);
+}
+
+void Engine::call_async(int B, bool run_front) {
+  PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_HIP(hipSetDevice(dev_));
   // Frame pairs: one back pass decodes a row's frames of the pair as a prefix (frame 2j, then
   // 2j+1). A row the even call did not cover must not produce the pair's second frame alone, so
   // an odd call covers at most the even call's rows; rows past that are paused for the call, as
-  // rows past n_rows are.
-  if (pipeline_ && nfr_ == 2 && (k_ & 1)) B = std::min(B, rows_hb_[(k_ - 1) % nhb_]);
+  // rows past n_rows are (an even call that was a flush covered none: the odd call is one too).
+  if (pipeline_ && nfr_ == 2 && (k_ & 1)) {
+    B = std::min(B, rows_hb_[(k_ - 1) % nhb_]);
+    if (B == 0) run_front = false;
+  }
+  if (!run_front) B = 0;
+  admitted_since_call_ = false;
   prev_hb_ = out_hb_;
   prev_rows_ = out_rows_;
   const int hb = (int)(k_ % nhb_), qp = (int)(k_ & 1);
-  hipGraphExec_t front = part_graph(0, B, hb, 0);
+  // the front part of this call, or (a flush) its hand-off buffer marked frame-less
+  hipGraphExec_t front = B > 0 ? part_graph(0, B, hb, 0) : nullptr;
+  auto run_front_part = [&]() {
+    if (front) PTTS_HIP(hipGraphLaunch(front, stream_));
+    else PTTS_HIP(hipMemsetAsync(flags_[hb], 0, sizeof(FrameFlags) * max_slots_, stream_));
+  };
   if (!pipeline_) {
     hipGraphExec_t back = part_graph(1, B, hb, qp);
     PTTS_HIP(hipGraphLaunch(front, stream_));
@@ -1433,35 +1458,40 @@ void Engine::step_async(int B) {
       act_slots_.clear();
     }
     PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
-    PTTS_HIP(hipGraphLaunch(front, stream_));
+    run_front_part();
     PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
     if ((k_ & 1) == 0 && k_ >= 2) {
       const int h0 = (int)((k_ - 2) % nhb_), h1 = (h0 + 1) % nhb_, pq = (int)(((k_ - 2) / 2) & 1);
-      hipGraphExec_t back = part_graph(1, std::max(rows_hb_[h0], rows_hb_[h1]), h0, pq);
-      PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[h1], 0));
-      if (admit_pending_) {
-        PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
-        admit_pending_ = false;
+      const int rows = std::max(rows_hb_[h0], rows_hb_[h1]);
+      if (rows > 0) {  // no pass when both calls of the pair were flushes
+        hipGraphExec_t back = part_graph(1, rows, h0, pq);
+        PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[h1], 0));
+        if (admit_pending_) {
+          PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
+          admit_pending_ = false;
+        }
+        PTTS_HIP(hipGraphLaunch(back, stream_be_));
       }
-      PTTS_HIP(hipGraphLaunch(back, stream_be_));
       PTTS_HIP(hipEventRecord(ev_back_[h0], stream_be_));
       PTTS_HIP(hipEventRecord(ev_back_[h1], stream_be_));
     }
     out_hb_ = (int)((k_ + nhb_ - 3) % nhb_);
     out_rows_ = k_ >= 3 ? rows_hb_[out_hb_] : 0;
   } else {
-    const int prev_rows = k_ > 0 ? front_rows_ : B;
+    const int prev_rows = k_ > 0 ? front_rows_ : B;  // 0: the previous call was a flush
     const int hb1 = (hb + nhb_ - 1) % nhb_, qp1 = qp ^ 1;  // frame k-1
-    hipGraphExec_t back = part_graph(1, prev_rows, hb1, qp1);
     PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
-    PTTS_HIP(hipGraphLaunch(front, stream_));
+    run_front_part();
     PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
-    PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[hb1], 0));
-    if (admit_pending_) {  // slot state rewritten since the front part this back part decodes
-      PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
-      admit_pending_ = false;
+    if (prev_rows > 0) {
+      hipGraphExec_t back = part_graph(1, prev_rows, hb1, qp1);
+      PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[hb1], 0));
+      if (admit_pending_) {  // slot state rewritten since the front part this back part decodes
+        PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
+        admit_pending_ = false;
+      }
+      PTTS_HIP(hipGraphLaunch(back, stream_be_));
     }
-    PTTS_HIP(hipGraphLaunch(back, stream_be_));
     PTTS_HIP(hipEventRecord(ev_back_[hb1], stream_be_));
     out_hb_ = hb1;
     out_rows_ = prev_rows;
@@ -2146,6 +2176,7 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     run_ops(ops);
   }
   mark_admission();
+  admitted_since_call_ = true;
 }
 
 void Engine::mark_admission() {

@@ -57,6 +57,10 @@ class Engine {
   void decode_latents(int slot, const float* lat, int n, float* pcm, float* quant, float* up, float* tr);
 
   void step_async(int B);
+  // a pipelined call that starts no frame (ptts_flush_async): only the back parts of frames
+  // already computed advance, so a caller whose rows have all finished drains the pipeline
+  // without running front parts whose frames would be discarded
+  void flush_async(int B);
   void sync();
   // the frame of the call calls_back (0 or 1) calls before the latest
   void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat, int calls_back = 0);
@@ -215,7 +219,9 @@ class Engine {
   int out_hb_ = 0;           // hand-off buffer of the frame the last call produced
   int out_rows_ = 0;         // rows that frame covers
   int prev_hb_ = 0, prev_rows_ = 0;  // the same for the call before (fetch with calls_back = 1)
-  int front_rows_ = 0;       // rows of the last front part
+  int front_rows_ = 0;       // rows of the last front part (0: the call was a flush)
+  bool admitted_since_call_ = false;  // an admission since the last step / flush call
+  void call_async(int B, bool front);
   float *temb_ = nullptr, *temb_tmp_ = nullptr;
   float* rope_ = nullptr;  // FlowLM RoPE cos/sin table [max_ctx][32][2]
 

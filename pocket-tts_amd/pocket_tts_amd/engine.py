@@ -257,6 +257,11 @@ class Engine:
     def step_async(self, n_rows: int):
         check(lib().ptts_step_async(self.handle, n_rows))
 
+    def flush_async(self, n_rows: int):
+        """A pipelined call that starts no frame (ptts_flush_async): drains the frames already
+        computed without running front parts whose frames would be discarded."""
+        check(lib().ptts_flush_async(self.handle, n_rows))
+
     def sync(self):
         check(lib().ptts_sync(self.handle))
 

@@ -396,6 +396,59 @@ def test_varying_rows_per_call_match_oracle(oracle, back_frames):
         eng.close()
 
 
+@pytest.mark.parametrize("back_frames", [1, 2])
+def test_flush_calls_drain_and_pause_rows(oracle, back_frames):
+    """ptts_flush_async: a pipelined call that starts no frame. Flushes in the middle of a job
+    pause every row for the call (their frames resume in order, equal to the oracle's), flushes at
+    the end drain the frames already computed (frame_lag() of them deliver every row's last
+    frame), and a flush right after an admission is refused."""
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    rng = np.random.default_rng(17)
+    eng = pt.Engine(device=0, max_slots=3, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
+                    back_frames=back_frames)
+    try:
+        orc, lat, got, vs, ids_l, want = {}, {}, {}, [], [], {0: 5, 1: 7, 2: 6}
+        for b in range(3):
+            F = 5 + 3 * b
+            prompt = (d["prompt"][:F] * (1.0 + 0.04 * b)).astype(np.float32)
+            ids = rng.integers(0, 4000, size=4 + b).astype(np.int32)
+            vs.append(eng.voice_from_prompt(prompt))
+            ids_l.append(ids)
+            s = oracle.new_state(256)
+            s.prefill(prompt)
+            s.prefill_tokens(ids)
+            orc[b], lat[b], got[b] = s, None, 0
+        eng.open_many([0, 1, 2], vs, ids_l, [params(max_frames=want[b]) for b in range(3)])
+        with pytest.raises(pt.PocketTTSError):
+            eng.flush_async(3)  # the admitted rows' first frame must fall on a step call
+
+        def check(r):
+            for b in range(3):
+                if not r.valid[b]:
+                    continue
+                o = orc[b].step(lat[b])
+                lat[b] = o["latent"]
+                got[b] += 1
+                assert got[b] <= want[b] and bool(r.last[b]) == (got[b] == want[b]), (b, got[b])
+                np.testing.assert_allclose(r.latents[b], o["latent"], atol=LAT_TOL)
+                assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL, (b, got[b])
+
+        # steps and flushes interleaved (two flushes in a row: with frame pairs an even-call flush
+        # makes the odd call one too), then the drain
+        for kind in "ssffsssfsss":
+            (eng.step_async if kind == "s" else eng.flush_async)(3)
+            check(eng.fetch(3))
+        lag, _ = eng.frame_lag()
+        for _ in range(lag):
+            eng.flush_async(3)
+            check(eng.fetch(3))
+        assert got == want, got
+    finally:
+        eng.close()
+
+
 def test_long_utterance_wraps_mimi_ring(gpu_engine, oracle):
     """70 frames: the Mimi decoder ring (512 positions = 32 frames) wraps twice and the 250-key
     window slides across the wrap; the FlowLM cache grows to voice + text + 70 positions. Every
