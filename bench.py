@@ -212,6 +212,7 @@ class _SelftestEngine:
         time.sleep(2e-4)
         for s in self.frames:
             self.frames[s] += 1
+        self.done = np.array([self.frames[s] >= self.max[s] for s in range(n)])  # this call's frame
 
     def flush_async(self, n):
         time.sleep(1e-4)
@@ -222,8 +223,7 @@ class _SelftestEngine:
     def fetch(self, n):
         import types
 
-        done = np.array([self.frames[s] >= self.max[s] for s in range(n)])
-        return types.SimpleNamespace(valid=done, last=done, pcm=np.zeros((n, 1920), np.float32))
+        return types.SimpleNamespace(valid=self.done, last=self.done, pcm=np.zeros((n, 1920), np.float32))
 
     def close(self):
         pass
@@ -281,6 +281,9 @@ def main():
     ap.add_argument("--no-flush", action="store_true",
                     help="drain each job's last frames with step calls (front parts of finished rows run and "
                          "their frames are discarded) instead of ptts_flush_async")
+    ap.add_argument("--no-overlap-admission", action="store_true",
+                    help="admit each job only after the previous job's last frame is fetched (no overlap of "
+                         "its text prefill with that job's last back passes)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sequential stepping (no FlowLM / Mimi overlap across consecutive frames)")
     ap.add_argument("--profile-frames", type=int, default=0,
@@ -382,20 +385,28 @@ def main():
         eng.sync()
         barrier()
         eng.sync()
-        admit_s = 0.0
         job_s = []
         t0 = time.perf_counter()
+        admit(1, K)
+        eng.sync()
+        admit_s = time.perf_counter() - t0  # one admission, alone (the later ones overlap, below)
+        tj = t0
         for j in range(jobs):
-            ta0 = time.perf_counter()
-            admit(1 + j, K)
-            eng.sync()
-            admit_s += time.perf_counter() - ta0
             run_calls(K)  # the K frames, then the calls that drain the last one
-            eng.sync()
-            r = eng.fetch(B)  # the last frame of every row, from pinned host memory
+            if j + 1 < jobs and not args.no_overlap_admission:
+                # the next job's admission is issued now: its voice-KV copy and text prefill queue
+                # behind this job's last front part and run beside its last back passes (the
+                # engine resets the back part's slot state only after those, ptts_slots_open)
+                admit(2 + j, K)
+            r = eng.fetch(B)  # the last frame of every row (waits for this job's last back pass)
             assert r.valid.all() and r.last.all(), "bench produced invalid frames"
             assert np.isfinite(r.pcm).all(), "bench produced non-finite PCM"
-            job_s.append(time.perf_counter() - ta0)
+            if j + 1 < jobs and args.no_overlap_admission:
+                eng.sync()
+                admit(2 + j, K)
+            t = time.perf_counter()
+            job_s.append(t - tj)
+            tj = t
         t1 = time.perf_counter()
         barrier()
         elapsed = t1 - t0
@@ -480,7 +491,7 @@ def main():
         top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
         sum_ops_ms = round(sum(u for u, _, _, _ in per_op) / 1000.0, 3)
         roof["phases"] = phase_rooflines(per_op, plan, B, K, back_frames)
-        roof["step"] = step_roofline(plan, B, K, back_frames, 1e6 * (elapsed - admit_s) / steps)
+        roof["step"] = step_roofline(plan, B, K, back_frames, 1e6 * (elapsed - jobs * admit_s) / steps)
         if args.ops_out:
             with open(args.ops_out, "w") as f:
                 json.dump({"n_rows": B, "plan": [n for n, _, _ in plan],
@@ -519,7 +530,7 @@ def main():
         q_el, q_ad, _ = timed_job(eq)
         quant = {"value": round(jobs * B * K * 1920 / 24000.0 / q_el, 2), "unit": "audio-sec/wall-sec",
                  "ms_per_step": round(1000.0 * q_el / steps, 4),
-                 "steady_ms_per_step": round(1000.0 * (q_el - q_ad) / steps, 4),
+                 "steady_ms_per_step": round(1000.0 * (q_el - jobs * q_ad) / steps, 4),
                  "weight_quant": "flow_lm int8 (quantize.rs QuantizeConfig::default, per-tensor symmetric)",
                  "int8_matrices": eq.int8_matrices}
         eq.close()
@@ -528,7 +539,7 @@ def main():
         f_el, f_ad, _ = timed_job(ef)
         fp8 = {"value": round(jobs * B * K * 1920 / 24000.0 / f_el, 2), "unit": "audio-sec/wall-sec",
                "ms_per_step": round(1000.0 * f_el / steps, 4),
-               "steady_ms_per_step": round(1000.0 * (f_el - f_ad) / steps, 4),
+               "steady_ms_per_step": round(1000.0 * (f_el - jobs * f_ad) / steps, 4),
                "gemm": "fp8 e4m3 W8A8 on v_mfma_f32_32x32x16_fp8_fp8 (row-scaled weights, per-slice "
                        "activation scales), FlowLM qkv/linear1/linear2/adaLN",
                "fp8_matrices": ef.fp8_matrices}
@@ -544,7 +555,7 @@ def main():
         snr = 10 * np.log10((ref_pcm ** 2).sum(-1) / np.maximum(err, 1e-30))
         bf16 = {"value": round(jobs * B * K * 1920 / 24000.0 / b_el, 2), "unit": "audio-sec/wall-sec",
                 "ms_per_step": round(1000.0 * b_el / steps, 4),
-                "steady_ms_per_step": round(1000.0 * (b_el - b_ad) / steps, 4),
+                "steady_ms_per_step": round(1000.0 * (b_el - jobs * b_ad) / steps, 4),
                 "mfma": "Mimi decoder transformer GEMMs + SEANet decoder convs on v_mfma_f32_32x32x16_bf16 "
                         "(operands rounded to bf16, f32 accumulation); FlowLM, attention, final conv f32",
                 "pcm_snr_db_vs_f32": {"min": round(float(snr.min()), 2), "median": round(float(np.median(snr)), 2),
@@ -580,8 +591,9 @@ def main():
         "steps_requested": args.steps,
         "warmup": W,
         "ms_per_step": round(1000.0 * elapsed / steps, 4),
-        "admit_ms": round(1000.0 * admit_s / jobs, 3),
-        "steady_ms_per_step": round(1000.0 * (elapsed - admit_s) / steps, 4),  # per frame, drain call included
+        "admit_ms": round(1000.0 * admit_s, 3),  # the first job's admission, alone (synchronised)
+        # per frame, drain calls included, with every job's admission counted at the first one's time
+        "steady_ms_per_step": round(1000.0 * (elapsed - jobs * admit_s) / steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

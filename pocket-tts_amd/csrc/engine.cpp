@@ -2065,12 +2065,11 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
   // Stream-ordered admission (no drain of the pipeline: a full sync() here stalled the front part
   // at every admission, a large share of the serving path's time): the host waits only until the
   // previous admission has consumed the pinned staging buffers (its event), and stream_ waits on
-  // the GPU for the back parts already queued on stream_be_, which may still decode a frame of a
-  // slot's previous utterance (they write its histories and Mimi position).
+  // the GPU for the back parts already queued on stream_be_ (which may still decode a frame of a
+  // slot's previous utterance: they write its histories and Mimi position) only before the reset
+  // of that state, after the text prefill.
   PTTS_HIP(hipEventSynchronize(ev_admit_));
   PTTS_HIP(hipEventSynchronize(ev_act_));  // pending start-of-utterance copies read h_act_
-  PTTS_HIP(hipEventRecord(ev_be_tail_, stream_be_));
-  PTTS_HIP(hipStreamWaitEvent(stream_, ev_be_tail_, 0));
   // copy-on-admit of the immutable voice prefixes
   for (int i = 0; i < n; ++i) {
     const ptts_voice* v = voices[i];
@@ -2078,6 +2077,51 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
                               sizeof(float) * v->F * 64, sizeof(float) * v->F * 64, NL * 2 * NH,
                               hipMemcpyDeviceToDevice, stream_));
   }
+  // text prefill (tts_model.rs:947-964) of every admitted utterance in shared passes
+  std::vector<int> tab, rid;
+  long off = 0;
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < n_ids[i]; ++j) {
+      tab.push_back(slots[i] << 16 | (voices[i]->F + j));
+      rid.push_back(ids[off + j]);
+    }
+    while (tab.size() % 16) {
+      tab.push_back(-1);
+      rid.push_back(0);
+    }
+    off += n_ids[i];
+  }
+  for (size_t c0 = 0; c0 < tab.size(); c0 += PREFILL) {
+    const int T = (int)std::min<size_t>(PREFILL, tab.size() - c0);  // PREFILL % 16 == 0
+    if (c0 > 0) PTTS_HIP(hipStreamSynchronize(stream_));  // ids / row table / staging reused by this pass
+    memcpy(h_ids_, rid.data() + c0, sizeof(int) * T);
+    memcpy(h_tab_, tab.data() + c0, sizeof(int) * T);
+    PTTS_HIP(hipMemcpyAsync(ids_dev_, h_ids_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(rowtab_dev_, h_tab_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    std::vector<Op> ops;
+    {
+      const int* idp = ids_dev_;
+      const float* tb = W(L_.embed);
+      float* x = x_;
+      ops.push_back({"prefill.embed", [=](hipStream_t s) { embed_gather(idp, T, tb, D, x, s); }});
+    }
+    {
+      float* x = x_;
+      float* h = h_;
+      const float* w = W(L_.fl[0].n1w);
+      const float* b = W(L_.fl[0].n1b);
+      ops.push_back({"prefill.ln1", [=](hipStream_t s) { layernorm(x, D, h, D, T, D, w, b, 1e-5f, s); }});
+    }
+    RowMap map{0, 1, 0, nullptr, rowtab_dev_};
+    flow_layers(ops, T, map, 16, false, "prefill");
+    run_ops(ops);
+  }
+  // the slot state the back part owns (Mimi ring position, conv and overlap-add histories, frame
+  // flags) is reset only after the back parts already queued, which may still decode the slot's
+  // previous utterance; the voice-KV copy and the text prefill above touch front-owned state
+  // only, so they run ahead of that wait, beside those back parts
+  PTTS_HIP(hipEventRecord(ev_be_tail_, stream_be_));
+  PTTS_HIP(hipStreamWaitEvent(stream_, ev_be_tail_, 0));
   // fresh Mimi decoder state (init_states(1, 1000) per segment, tts_model.rs:941) + slot states
   std::vector<SlotState> st(n);
   std::vector<int> fp(n);
@@ -2135,45 +2179,6 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     for (int q = 0; q < NHB; ++q) r.flags[q] = flags_[q];
     slot_reset(r, stream_);
     PTTS_HIP(hipGetLastError());
-  }
-  // text prefill (tts_model.rs:947-964) of every admitted utterance in shared passes
-  std::vector<int> tab, rid;
-  long off = 0;
-  for (int i = 0; i < n; ++i) {
-    for (int j = 0; j < n_ids[i]; ++j) {
-      tab.push_back(slots[i] << 16 | (voices[i]->F + j));
-      rid.push_back(ids[off + j]);
-    }
-    while (tab.size() % 16) {
-      tab.push_back(-1);
-      rid.push_back(0);
-    }
-    off += n_ids[i];
-  }
-  for (size_t c0 = 0; c0 < tab.size(); c0 += PREFILL) {
-    const int T = (int)std::min<size_t>(PREFILL, tab.size() - c0);  // PREFILL % 16 == 0
-    if (c0 > 0) PTTS_HIP(hipStreamSynchronize(stream_));  // ids / row table / staging reused by this pass
-    memcpy(h_ids_, rid.data() + c0, sizeof(int) * T);
-    memcpy(h_tab_, tab.data() + c0, sizeof(int) * T);
-    PTTS_HIP(hipMemcpyAsync(ids_dev_, h_ids_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
-    PTTS_HIP(hipMemcpyAsync(rowtab_dev_, h_tab_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
-    std::vector<Op> ops;
-    {
-      const int* idp = ids_dev_;
-      const float* tb = W(L_.embed);
-      float* x = x_;
-      ops.push_back({"prefill.embed", [=](hipStream_t s) { embed_gather(idp, T, tb, D, x, s); }});
-    }
-    {
-      float* x = x_;
-      float* h = h_;
-      const float* w = W(L_.fl[0].n1w);
-      const float* b = W(L_.fl[0].n1b);
-      ops.push_back({"prefill.ln1", [=](hipStream_t s) { layernorm(x, D, h, D, T, D, w, b, 1e-5f, s); }});
-    }
-    RowMap map{0, 1, 0, nullptr, rowtab_dev_};
-    flow_layers(ops, T, map, 16, false, "prefill");
-    run_ops(ops);
   }
   mark_admission();
   admitted_since_call_ = true;
