@@ -10,6 +10,7 @@ namespace ptts {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 

@@ -328,6 +328,20 @@ void Engine::derive_gemv() {
   }
   const GemvShape ada{4, 128};  // flow-head adaLN matrix: 0.6365 -> 0.6315 ms
   mats.push_back({W(L_.ada_w), NADA, FD, 16, ada});
+  // linear1 on the whole-K GEMM (gemv_fk: GELU in its epilogue, no split-K slabs, no reduce launch)
+  // wherever the register-resident linear1 is used; PTTS_NO_FK (probe builds) keeps the split-K form
+  if ((mask & 4) && !probe_env("PTTS_NO_FK") && gemv_fk_supported(1, FF, D)) {
+    void* q = nullptr;
+    PTTS_HIP(hipMalloc(&q, sizeof(float) * ((size_t)NL * FF * D + FK_A_FLOATS)));  // all written before read
+    allocs_.push_back(q);
+    float* dst = (float*)q;
+    for (int l = 0; l < NL; ++l) {
+      pack_gemv_fk(W(L_.fl[l].l1), FF, D, dst, stream_);
+      fkmap_[W(L_.fl[l].l1)] = dst;
+      dst += (size_t)FF * D;
+    }
+    hfrag_ = dst;
+  }
   size_t total = 0;
   for (const M& m : mats)
     if ((mask & m.bit) && gemv_supported(m.g, m.N, m.K)) total += (size_t)m.N * m.K;
@@ -742,8 +756,9 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, M, NH, map, kv, 0, qg, O, s); }});
     }
     auto rr = [&](const std::string& name, int S2, int N, int act, bool resid, float* Y, const float* lnw,
-                  const float* lnb, bool ln, float* Hout) {
+                  const float* lnb, bool ln, float* Hout, float* Hfrag = nullptr) {
       RowReduceArgs a{};
+      a.Hfrag = Hfrag;
       a.P = partial_;
       a.S = S2;
       a.M = M;
@@ -764,9 +779,21 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       push_rr(ops, name, a);
     };
     linear_split(ops, p + ".out_gemm", o_, D, M, W(t.out_proj), D, D, &S);
-    rr(p + ".out_reduce_ln2", S, D, ACT_NONE, true, x_, W(t.n2w), W(t.n2b), true, h_);
-    linear_split(ops, p + ".ff1_gemm", h_, D, M, W(t.l1), FF, D, &S);
-    rr(p + ".ff1_reduce_gelu", S, FF, ACT_GELU, false, u_, nullptr, nullptr, false, nullptr);
+    // step passes with the whole-K linear1 (gemv_fk): the out reduce also stores norm2's output in
+    // its A-fragment order, and linear1 applies GELU in its own epilogue (no slabs, no reduce)
+    auto fk = qg == 1 && gemv_fk_supported(M, FF, D) ? fkmap_.find(W(t.l1)) : fkmap_.end();
+    const bool use_fk = fk != fkmap_.end() && hfrag_;
+    rr(p + ".out_reduce_ln2", S, D, ACT_NONE, true, x_, W(t.n2w), W(t.n2b), true, h_, use_fk ? hfrag_ : nullptr);
+    if (use_fk) {
+      const float* Pk = fk->second;
+      const float* A = hfrag_;
+      float* U = u_;
+      ops.push_back({p + ".ff1_gemm", [=](hipStream_t s) { gemv_fk(A, M, FF, Pk, nullptr, ACT_GELU, U, FF, s); },
+                     2.0 * M * FF * D, 4.0 * ((double)FF * D + (double)M * D + (double)M * FF)});
+    } else {
+      linear_split(ops, p + ".ff1_gemm", h_, D, M, W(t.l1), FF, D, &S);
+      rr(p + ".ff1_reduce_gelu", S, FF, ACT_GELU, false, u_, nullptr, nullptr, false, nullptr);
+    }
     linear_split(ops, p + ".ff2_gemm", u_, FF, M, W(t.l2), D, FF, &S);
     if (l + 1 < NL)
       rr(p + ".ff2_reduce_ln1", S, D, ACT_NONE, true, x_, W(L_.fl[l + 1].n1w), W(L_.fl[l + 1].n1b), true, h_);

@@ -117,6 +117,10 @@ class Engine {
     int bit;  // PTTS_GEMV mask bit of the matrix
   };
   std::map<const float*, Gemv> gvmap_;
+  // whole-K copies of the FlowLM linear1 matrices for gemv_fk (weight -> packed copy), and the
+  // A-fragment-order copy of the norm2 output the step's out reduce writes for it
+  std::map<const float*, const float*> fkmap_;
+  float* hfrag_ = nullptr;
   int gemv_mask_ = 0;  // matrices that take the register-resident GEMM
   void derive_gemv();
   bool own_blob_ = true, ready_ = false;

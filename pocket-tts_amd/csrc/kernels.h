@@ -62,6 +62,8 @@ struct RowReduceArgs {
   float* x0_hx;
   int x0_B;
   int front;  // 1: a launch of the front part (issue priority, set_front_prio)
+  // (ln, N == FK_K, M <= 32) also store the LayerNorm output in gemv_fk's A-fragment order, or nullptr
+  float* Hfrag;
 };
 struct GemmArgs {
   int mode;    // 0 dense, 1 conv
@@ -141,6 +143,19 @@ struct GemvShape {
   int ks() const { return kw * (4 / wn); }
 };
 bool gemv_supported(GemvShape g, int N, int K);
+// Whole-K skinny GEMM for K = 1024, M <= 32 (the FlowLM step's linear1): Y = act(A W^T + bias),
+// one 512-thread workgroup per 16 output columns, the 8 waves splitting K in 128-k ranges, each
+// wave's weight fragment (pack_gemv_fk) AND its A fragment requested at the start: A comes in
+// fragment order (FK_A_FLOATS floats, written by the row reduce ahead of it: RowReduceArgs::Hfrag),
+// so every load instruction reads one contiguous KB. v_mfma_f32_16x16x4f32 over two 16-row tiles;
+// the waves' partial tiles are summed through LDS in wave order and the epilogue (bias, GELU)
+// writes Y: no split-K slabs and no reduce launch.
+constexpr int FK_K = 1024;
+constexpr long FK_A_FLOATS = 32L * FK_K;
+bool gemv_fk_supported(int M, int N, int K);
+void pack_gemv_fk(const float* W, int N, int K, float* packed, hipStream_t s);
+void gemv_fk(const float* Afrag, int M, int N, const float* packed, const float* bias, int act, float* Y, long ldy,
+             hipStream_t s);
 void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStream_t s);
 void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
                  hipStream_t s);

@@ -1682,6 +1682,93 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Whole-K skinny GEMM (kernels.h gemv_fk). Fragment orders, K = 1024, wave w (0..7) covering
+// k = 128 w .. 128 w + 127, lane l = 16 g + c (g = l >> 4 the lane group, c = l & 15):
+//   A: lane (g, r) of row tile t holds k = 128 w + 32 g + s, s = 0..31, for row 16 t + r, as 8 float4
+//      j = s / 4: float4 index ((w * 2 + t) * 8 + j) * 64 + l  (FK_A_FLOATS floats for 32 rows)
+//   W: lane (g, c) of column tile n0 / 16 holds k = 128 w + 32 g + s of column n0 + c:
+//      float4 index ((n0 / 16 * 8 + w) * 8 + j) * 64 + l
+// MFMA step s (16x16x4, lane group g supplies the step's k index g) sums k = 128 w + 32 g + s over
+// g for both operands alike: each wave's 128 k are covered once (a permutation of the order).
+__device__ __forceinline__ long fk_afrag_index(int row, int k) {  // float index into the A fragment
+  const int w = k >> 7, g = (k >> 5) & 3, s = k & 31, t = row >> 4, r = row & 15;
+  return ((((long)(w * 2 + t) * 8 + (s >> 2)) * 64 + (g * 16 + r)) << 2) + (s & 3);
+}
+__global__ void k_pack_gemv_fk(const float* __restrict__ W, int N, int K, float* __restrict__ P) {
+  const long i4 = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i4 >= (long)N * K / 4) return;
+  const int l = (int)(i4 & 63), j = (int)((i4 >> 6) & 7), w = (int)((i4 >> 9) & 7);
+  const int ct = (int)(i4 >> 12);
+  const int n = ct * 16 + (l & 15), k = w * 128 + (l >> 4) * 32 + 4 * j;
+  reinterpret_cast<float4*>(P)[i4] = *reinterpret_cast<const float4*>(W + (long)n * K + k);
+}
+__global__ __launch_bounds__(512) void k_gemv_fk(const float* __restrict__ A, int M, int N,
+                                                 const float* __restrict__ P, const float* __restrict__ bias,
+                                                 int act, float* __restrict__ Y, long ldy) {
+  front_prio();
+  __shared__ __attribute__((aligned(16))) float red[8 * 2 * 4 * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ct = blockIdx.x;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* wp = reinterpret_cast<const f4v*>(P) + ((long)(ct * 8 + w) * 8) * 64 + lane;
+  const f4v* ap = reinterpret_cast<const f4v*>(A) + ((long)(w * 2) * 8) * 64 + lane;
+  f4v b[8], a0[8], a1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = __builtin_nontemporal_load(wp + j * 64);  // once-read weights
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a0[j] = ap[j * 64];
+    a1[j] = ap[(8 + j) * 64];
+  }
+  // every load in flight before the first MFMA (the scheduler otherwise sinks them next to their
+  // use: a few loads in flight at a time, one round trip each)
+  __builtin_amdgcn_sched_barrier(0);
+  floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][e], b[j][e], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][e], b[j][e], c1, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    red[((w * 2 + 0) * 4 + i) * 64 + lane] = c0[i];
+    red[((w * 2 + 1) * 4 + i) * 64 + lane] = c1[i];
+  }
+  __syncthreads();
+  // thread tid: row tile t, register i, lane ll (C map: column ll & 15, row (ll >> 4) * 4 + i)
+  const int t = tid >> 8, i = (tid >> 6) & 3, ll = tid & 63;
+  float v = red[((0 * 2 + t) * 4 + i) * 64 + ll];
+#pragma unroll
+  for (int ww = 1; ww < 8; ++ww) v += red[((ww * 2 + t) * 4 + i) * 64 + ll];
+  const int row = 16 * t + (ll >> 4) * 4 + i, col = ct * 16 + (ll & 15);
+  if (row < M) {
+    if (bias) v += bias[col];
+    if (act == ACT_GELU) v = gelu_tanh(v);
+    Y[(long)row * ldy + col] = v;
+  }
+}
+
+bool gemv_fk_supported(int M, int N, int K) { return M >= 1 && M <= 32 && K == FK_K && N % 16 == 0; }
+
+void pack_gemv_fk(const float* W, int N, int K, float* packed, hipStream_t s) {
+  if (!gemv_fk_supported(1, N, K)) throw std::runtime_error("pack_gemv_fk: unsupported shape");
+  const long total4 = (long)N * K / 4;
+  hipLaunchKernelGGL(k_pack_gemv_fk, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, W, N, K, packed);
+}
+
+void gemv_fk(const float* Afrag, int M, int N, const float* packed, const float* bias, int act, float* Y, long ldy,
+             hipStream_t s) {
+  if (!gemv_fk_supported(M, N, FK_K) || (act != ACT_NONE && act != ACT_GELU))
+    throw std::runtime_error("gemv_fk: unsupported shape");
+  hipLaunchKernelGGL(k_gemv_fk, dim3((unsigned)(N / 16)), dim3(512), cap_lds(k_gemv_fk, g_wg_cap), s, Afrag, M, N,
+                     packed, bias, act, Y, ldy);
+}
+
 bool gemv_supported(GemvShape g, int N, int K) {
   const bool shape = (g.wn == 4 && g.kw == 128) || (g.wn == 1 && g.kw == 32) || (g.wn == 1 && g.kw == 64) ||
                      (g.wn == 2 && g.kw == 64);
@@ -1846,7 +1933,9 @@ __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   const float q = ok ? (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w) : 0.f;
   const float den = sqrtf(block_sum(q, sh) / (float)a.N + a.eps);
   if (!ok) return;
-  *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = rr_ln(a, m, n, d, den);
+  const float4 hv = rr_ln(a, m, n, d, den);
+  *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = hv;
+  if (a.Hfrag) *reinterpret_cast<float4*>(a.Hfrag + fk_afrag_index(m, n)) = hv;  // n % 4 == 0: one float4
 }
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s) {
