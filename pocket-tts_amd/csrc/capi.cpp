@@ -199,11 +199,7 @@ int ptts_voice_conditioning(const ptts_voice* v, float* out, int max_rows) {
   });
 }
 
-void ptts_voice_destroy(ptts_voice* v) {
-  if (!v) return;
-  if (v->kv) (void)hipFree(v->kv);
-  delete v;
-}
+void ptts_voice_destroy(ptts_voice* v) { ptts::voice_destroy(v); }
 
 int ptts_slot_open(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* ids, int n_ids,
                    const ptts_gen_params* p) {

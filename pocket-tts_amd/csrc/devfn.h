@@ -78,6 +78,32 @@ __device__ __forceinline__ void row_slot_pos(const RowMap& mp, int row, int& slo
   pos = (mp.pos_arr ? mp.pos_arr[slot] : mp.p0) + row % mp.rps;
 }
 
+// K / V of (slot, head): the slot's own rows (kb, vb; appends go there) and, under a shared voice
+// prefix, the voice's rows (pk, pv) that hold positions < F (KvStore::pre)
+struct KvHead {
+  float *kb, *vb;
+  const float *pk, *pv;
+  int F;
+};
+__device__ __forceinline__ KvHead kv_head(const KvStore& kv, int slot, int nh, int head) {
+  KvHead h;
+  h.kb = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
+  h.vb = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
+  h.pk = h.kb;
+  h.pv = h.vb;
+  h.F = 0;
+  if (kv.pre != nullptr && slot >= 0) {
+    const int F = kv.pre_len[slot];
+    if (F > 0) {
+      const float* p = kv.pre[slot] + ((long)kv.layer * 2 * nh + head) * F * 64;
+      h.pk = p;
+      h.pv = p + (long)nh * F * 64;
+      h.F = F;
+    }
+  }
+  return h;
+}
+
 // Buffer resource over a whole allocation, and 16-B loads / stores with the sc1 cache policy
 // (agent scope: a store writes through to the point of coherence of all XCDs, a load does not hit
 // a line another XCD's L2 may hold stale): the hand-off traffic of the persistent launches.

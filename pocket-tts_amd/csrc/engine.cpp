@@ -2,7 +2,9 @@
 //
 // Data layout in HBM (fp32):
 //   weight blob                packed by weights.cpp (one allocation; RCCL-broadcastable)
-//   FlowLM KV                  [slot][layer][k|v][head][max_ctx][64]   (attention.rs:211-231, preallocated)
+//   FlowLM KV                  [slot][layer][k|v][head][max_ctx][64]   (attention.rs:211-231, preallocated;
+//                              positions < F of an admitted slot are read from its voice's own
+//                              [layer][k|v][head][F][64] cache, shared by every slot of that voice)
 //   Mimi KV ring               [slot][layer][k|v][head][512][64]       (attention.rs:167-264, ctx 250)
 //   conv histories             [slot][P][C] per streaming conv          (conv.rs:71-136, time-major)
 //   activations                row-major [rows][features]; Mimi/SEANet channels-last [slot][time][ch]
@@ -14,10 +16,18 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 
 namespace ptts {
 
 namespace {
+// voice reference counts (ptts_voice::refs / dead): engines and ptts_voice_destroy may run on
+// different host threads
+std::mutex& voice_mu() {
+  static std::mutex m;
+  return m;
+}
+
 int pick_splits(int M, int N, int K) {
   const int tiles = ((N + 31) / 32) * ((M + 31) / 32);
   const int chunks = K / 32;
@@ -163,6 +173,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
   admit_slots_ = (int*)dalloc(B);
   admit_st_ = (SlotState*)dalloc((sizeof(SlotState) * B + 3) / 4);
   admit_fpos_ = (int*)dalloc(B);
+  vpre_ = (const float**)dalloc((sizeof(float*) * (B + 1) + 3) / 4);  // zero: no slot has a prefix
+  vlen_ = (int*)dalloc(B + 1);
+  slot_voice_.assign(B, nullptr);
+  share_voice_ = probe_env("PTTS_NO_SHARED_VOICE") == nullptr;
   // pipelined stepping: the back part's kernels run at most one workgroup per CU, so the
   // latency-bound front part always finds room on every CU (measured 0.735 -> 0.688 ms per step
   // for the GEMMs alone; tools/sweep_env.sh)
@@ -220,6 +234,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_HIP(hipHostMalloc((void**)&h_fp_, sizeof(int) * B, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_ids_, sizeof(int) * PREFILL, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_tab_, sizeof(int) * PREFILL, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_vpre_, sizeof(float*) * (B + 1), hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_vlen_, sizeof(int) * (B + 1), hipHostMallocDefault));
+  memset(h_vpre_, 0, sizeof(float*) * (B + 1));
+  memset(h_vlen_, 0, sizeof(int) * (B + 1));
   PTTS_HIP(hipStreamCreateWithFlags(&stream_be_, hipStreamNonBlocking));
   for (int q = 0; q < NHB; ++q) {
     PTTS_HIP(hipEventCreateWithFlags(&ev_front_[q], hipEventDisableTiming));
@@ -257,6 +275,7 @@ Engine::~Engine() {
   (void)hipSetDevice(dev_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (stream_be_) (void)hipStreamSynchronize(stream_be_);
+  for (int s = 0; s < (int)slot_voice_.size(); ++s) voice_release(s, true);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
   for (int q = 0; q < NHB; ++q) {
@@ -276,7 +295,8 @@ Engine::~Engine() {
     if (h_pcmp_[p]) (void)hipHostFree(h_pcmp_[p]);
   if (h_act_) (void)hipHostFree(h_act_);
   if (h_err_) (void)hipHostFree(h_err_);
-  for (void* hp : {(void*)h_slots_, (void*)h_st_, (void*)h_fp_, (void*)h_ids_, (void*)h_tab_})
+  for (void* hp : {(void*)h_slots_, (void*)h_st_, (void*)h_fp_, (void*)h_ids_, (void*)h_tab_, (void*)h_vpre_,
+                   (void*)h_vlen_})
     if (hp) (void)hipHostFree(hp);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -398,7 +418,8 @@ void Engine::derive_flow_lm() {
 // stretching every phase's slowest workgroup), so it runs only in probe builds on request
 // (PTTS_FLM_ON, tools/flm_ab.py, tools/flm_stamps.py).
 bool Engine::use_flow_lm(int B) const {
-  if (!flm_pack_ || !flm_ws_ || !flow_lm_fits(B) || flow_lm_grid() > flm_resident_) return false;
+  // (k_flow_lm reads every position from the slot's rows: copy-on-admit voice prefixes only)
+  if (!flm_pack_ || !flm_ws_ || !flow_lm_fits(B) || flow_lm_grid() > flm_resident_ || share_voice_) return false;
   return probe_env("PTTS_FLM_ON") != nullptr;
 }
 
@@ -449,6 +470,7 @@ void Engine::finalize() {
 }
 
 void Engine::run_ops(const std::vector<Op>& ops) {
+  xh_dirty_ = true;  // eager passes (prefills, encoder) use x_ / h_ as scratch
   for (const Op& op : ops) {
     op.fn(stream_);
     hipError_t e = hipGetLastError();
@@ -733,6 +755,11 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
     const Layout::TL& t = L_.fl[l];
     const std::string p = tag + ".l" + std::to_string(l);
     KvStore kv{kv_ + (long)l * kv_layer_, kv_slot_, max_ctx_};
+    if (share_voice_) {  // positions below a slot's voice length read the voice's own cache
+      kv.pre = vpre_;
+      kv.pre_len = vlen_;
+      kv.layer = l;
+    }
     int S = 1;
     linear_split(ops, p + ".qkv_gemm", h_, D, M, W(t.in_proj), 3 * D, D, &S);
     if (qg == 1) {  // step: slab sum + RoPE + KV append fused into the attention kernel
@@ -837,13 +864,9 @@ bool Engine::head_uniform_stride() const {
 // FRONT part of a step (FlowLM + flow head) for rows [0, B), handing its frame to buffer `hb`.
 void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
   int S = 1;
-  // ---- FlowLM step (flow_lm.rs:98-164): input_linear -> transformer -> out_norm
-  {
-    const float *lat = lat_in_, *w = inw_t_, *lw = W(L_.fl[0].n1w), *lb = W(L_.fl[0].n1b);
-    float *x = x_, *h = h_;
-    ops.push_back({"flow.input_ln1", [=](hipStream_t s) { input_ln(lat, w, lw, lb, x, h, B, s); },
-                   2.0 * B * D * LDIM, 4.0 * ((double)D * LDIM + (double)B * (LDIM + 2 * D))});
-  }
+  // ---- FlowLM step (flow_lm.rs:98-164): input_linear -> transformer -> out_norm. The input
+  // projection + norm1 of layer 0 (x_, h_) were computed by the previous step's front_commit, or
+  // by refresh_xh() after anything else wrote x_, h_ or lat_in_.
   if (use_flow_lm(B)) {
     FlowLmArgs f{};
     f.B = B;
@@ -1053,8 +1076,14 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     c.eos_out = eos_out_[hb];
     c.flags = flags_[hb];
     c.fpos = fpos_;
-    ops.push_back({"front_commit", [c](hipStream_t s) { front_commit(c, s); }, 0.0,
-                   (double)B * (sizeof(SlotState) * 2 + 4.0 * (1 + 3 * LDIM + 1 + 2 + 2))});
+    c.Wt = inw_t_;
+    c.lnw = W(L_.fl[0].n1w);
+    c.lnb = W(L_.fl[0].n1b);
+    c.x = x_;
+    c.h = h_;
+    ops.push_back({"front_commit", [c](hipStream_t s) { front_commit(c, s); }, 2.0 * B * D * LDIM,
+                   (double)B * (sizeof(SlotState) * 2 + 4.0 * (1 + 3 * LDIM + 1 + 2 + 2 + 2 * D)) +
+                       4.0 * ((double)D * LDIM + 2 * D)});
   }
 }
 
@@ -1461,12 +1490,13 @@ void Engine::call_async(int B, bool run_front) {
   // the front part of this call, or (a flush) its hand-off buffer marked frame-less
   hipGraphExec_t front = B > 0 ? part_graph(0, B, hb, 0) : nullptr;
   auto run_front_part = [&]() {
+    if (front && xh_dirty_) refresh_xh();
     if (front) PTTS_HIP(hipGraphLaunch(front, stream_));
     else PTTS_HIP(hipMemsetAsync(flags_[hb], 0, sizeof(FrameFlags) * max_slots_, stream_));
   };
   if (!pipeline_) {
     hipGraphExec_t back = part_graph(1, B, hb, qp);
-    PTTS_HIP(hipGraphLaunch(front, stream_));
+    run_front_part();
     PTTS_HIP(hipGraphLaunch(back, stream_));
     out_hb_ = hb;
     out_rows_ = B;
@@ -1585,6 +1615,7 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
 // model never runs).
 void Engine::test_gemm(int layout, int M, int N, int K, int splits, int tail_S, const float* X, const float* Wt,
                        float* Y) {
+  xh_dirty_ = true;
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(X && Wt && Y && M >= 1 && N >= 1 && K >= 32 && K % 32 == 0, "test_gemm: bad shape");
   PTTS_REQUIRE(splits >= 1 && splits <= 16 && (splits == 1 || tail_S == 0), "test_gemm: bad split");
@@ -1635,6 +1666,7 @@ void Engine::test_gemm(int layout, int M, int N, int K, int splits, int tail_S, 
 }
 
 double Engine::time_op(int B, const std::string& name, int reps) {
+  xh_dirty_ = true;  // replays write x_ / h_
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
   PTTS_REQUIRE(reps >= 1, "reps must be >= 1");
@@ -1692,6 +1724,7 @@ double Engine::time_op(int B, const std::string& name, int reps) {
 // times each alone and both launched together on two streams (no dependency, data races are
 // irrelevant for timing). us[0] = front alone, us[1] = back alone, us[2] = both concurrently.
 void Engine::overlap_probe(int B, int reps, double* us) {
+  xh_dirty_ = true;  // replays write x_ / h_
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(B >= 1 && B <= max_slots_ && reps >= 1, "bad probe arguments");
   PTTS_HIP(hipSetDevice(dev_));
@@ -2097,12 +2130,31 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
   // of that state, after the text prefill.
   PTTS_HIP(hipEventSynchronize(ev_admit_));
   PTTS_HIP(hipEventSynchronize(ev_act_));  // pending start-of-utterance copies read h_act_
-  // copy-on-admit of the immutable voice prefixes
-  for (int i = 0; i < n; ++i) {
-    const ptts_voice* v = voices[i];
-    PTTS_HIP(hipMemcpy2DAsync(kv_ + (size_t)slots[i] * kv_slot_, sizeof(float) * max_ctx_ * 64, v->kv,
-                              sizeof(float) * v->F * 64, sizeof(float) * v->F * 64, NL * 2 * NH,
-                              hipMemcpyDeviceToDevice, stream_));
+  if (share_voice_) {
+    // shared voice prefixes: each slot's positions < F read the voice's own cache (no copy; the
+    // reference copies the prompt's ModelState per utterance, tts_model.rs:940: same values)
+    {
+      std::lock_guard<std::mutex> lk(voice_mu());
+      for (int i = 0; i < n; ++i) ++voices[i]->refs;
+    }
+    for (int i = 0; i < n; ++i) voice_release(slots[i], false);
+    for (int i = 0; i < n; ++i) {
+      slot_voice_[slots[i]] = voices[i];
+      h_vpre_[slots[i]] = voices[i]->kv;
+      h_vlen_[slots[i]] = voices[i]->F;
+    }
+    // the tables are read by the text prefill below and by the steps after it (stream order); the
+    // steps queued before still read the old entries (a freed voice waited for them above)
+    PTTS_HIP(hipMemcpyAsync(vpre_, h_vpre_, sizeof(float*) * max_slots_, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(vlen_, h_vlen_, sizeof(int) * max_slots_, hipMemcpyHostToDevice, stream_));
+  } else {
+    // copy-on-admit of the immutable voice prefixes
+    for (int i = 0; i < n; ++i) {
+      const ptts_voice* v = voices[i];
+      PTTS_HIP(hipMemcpy2DAsync(kv_ + (size_t)slots[i] * kv_slot_, sizeof(float) * max_ctx_ * 64, v->kv,
+                                sizeof(float) * v->F * 64, sizeof(float) * v->F * 64, NL * 2 * NH,
+                                hipMemcpyDeviceToDevice, stream_));
+    }
   }
   // text prefill (tts_model.rs:947-964) of every admitted utterance in shared passes
   std::vector<int> tab, rid;
@@ -2214,6 +2266,16 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
 void Engine::mark_admission() {
   PTTS_HIP(hipEventRecord(ev_admit_, stream_));
   admit_pending_ = true;
+  xh_dirty_ = true;  // lat_in_ (and, with a prefill, x_ / h_) rewritten
+}
+
+// x_, h_ rows of every slot from lat_in_ (the step's input projection + layer-0 norm1), on stream_
+// ahead of the next front part: after an admission, a voice prefill or anything else that used
+// x_ / h_ as scratch or wrote lat_in_ (the step graphs keep them current themselves)
+void Engine::refresh_xh() {
+  input_ln(lat_in_, inw_t_, W(L_.fl[0].n1w), W(L_.fl[0].n1b), x_, h_, max_slots_, stream_);
+  PTTS_HIP(hipGetLastError());
+  xh_dirty_ = false;
 }
 
 // MimiModel::decode_from_latent (mimi.rs:143-157) with the denorm + quantize of tts_model.rs:
@@ -2301,8 +2363,44 @@ void Engine::slot_close(int slot) {
   PTTS_HIP(hipMemcpyAsync(st_ + slot, h_st_, sizeof s, hipMemcpyHostToDevice, stream_));
   for (int q = 0; q < NHB; ++q)  // drop a pending frame of the slot
     PTTS_HIP(hipMemsetAsync(flags_[q] + slot, 0, sizeof(FrameFlags), stream_));
+  if (share_voice_ && slot_voice_[slot]) {  // the closed row (still stepped, discarded) reads its own rows
+    h_vpre_[slot] = nullptr;
+    h_vlen_[slot] = 0;
+    PTTS_HIP(hipMemcpyAsync(vpre_ + slot, h_vpre_ + slot, sizeof(float*), hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(vlen_ + slot, h_vlen_ + slot, sizeof(int), hipMemcpyHostToDevice, stream_));
+  }
   mark_admission();
   PTTS_HIP(hipStreamSynchronize(stream_));
+  voice_release(slot, true);
+}
+
+void Engine::voice_release(int slot, bool drained) {
+  const ptts_voice* v = slot_voice_[slot];
+  if (!v) return;
+  slot_voice_[slot] = nullptr;
+  bool free_now = false;
+  {
+    std::lock_guard<std::mutex> lk(voice_mu());
+    free_now = --v->refs == 0 && v->dead;
+  }
+  if (!free_now) return;
+  if (!drained) PTTS_HIP(hipStreamSynchronize(stream_));  // queued steps may still read it
+  ptts_voice* w = const_cast<ptts_voice*>(v);
+  if (w->kv) (void)hipFree(w->kv);
+  delete w;
+}
+
+void voice_destroy(ptts_voice* v) {
+  if (!v) return;
+  {
+    std::lock_guard<std::mutex> lk(voice_mu());
+    if (v->refs > 0) {  // slots still read it: the last to let go frees it
+      v->dead = true;
+      return;
+    }
+  }
+  if (v->kv) (void)hipFree(v->kv);
+  delete v;
 }
 
 void Engine::set_latent(int slot, const float* lat) {

@@ -11,14 +11,23 @@
 
 // Immutable voice prefix (the reference's ModelState after the prompt prefill,
 // tts_model.rs:490-501 / 504-560): FlowLM KV for F conditioning positions.
+// Slots read the prefix from this copy (shared voice prefixes, KvStore::pre): `refs` counts the
+// slots that do, and ptts_voice_destroy on a referenced voice only marks it `dead`; the last
+// slot to let go of it frees it (ptts::voice_destroy, Engine::voice_release).
 struct ptts_voice {
   int F = 0;
   float* kv = nullptr;      // device [NL][2][NH][F][64]
   std::vector<float> cond;  // conditioning rows [F][1024] (kept for PCM voices)
   const void* owner = nullptr;
+  mutable int refs = 0;
+  mutable bool dead = false;
 };
 
 namespace ptts {
+
+// ptts_voice_destroy: frees the voice now, or (while slots still read its prefix) marks it for
+// the last of them to free
+void voice_destroy(ptts_voice* v);
 
 struct Op {
   std::string name;
@@ -136,6 +145,18 @@ class Engine {
   long ring_slot_ = 0, ring_layer_ = 0;
   int* fpos_ = nullptr;
   int* mpos_ = nullptr;
+  // shared voice prefixes (KvStore::pre): per slot, the voice cache its positions < F read from
+  // and F (0: the slot's own rows, as for the prefill scratch slot); pinned host mirrors; the
+  // voice each slot references. PTTS_NO_SHARED_VOICE (probe builds) copies the prefix in instead.
+  bool share_voice_ = true;
+  const float** vpre_ = nullptr;
+  int* vlen_ = nullptr;
+  const float** h_vpre_ = nullptr;
+  int* h_vlen_ = nullptr;
+  std::vector<const ptts_voice*> slot_voice_;
+  // the slot lets go of its voice (freed here if it was destroyed meanwhile: `drained` = no queued
+  // work may still read it, else stream_ is synchronized first)
+  void voice_release(int slot, bool drained);
   SlotState* st_ = nullptr;
   float *lat_in_ = nullptr, *cur_ = nullptr, *qprev_ = nullptr, *qcur_ = nullptr, *eos_ = nullptr;
   float* hist_[8] = {};
@@ -225,6 +246,9 @@ class Engine {
   int prev_hb_ = 0, prev_rows_ = 0;  // the same for the call before (fetch with calls_back = 1)
   int front_rows_ = 0;       // rows of the last front part (0: the call was a flush)
   bool admitted_since_call_ = false;  // an admission since the last step / flush call
+  // x_ / h_ / lat_in_ written outside the step graphs since the last front part (refresh_xh)
+  bool xh_dirty_ = true;
+  void refresh_xh();
   void call_async(int B, bool front);
   float *temb_ = nullptr, *temb_tmp_ = nullptr;
   float* rope_ = nullptr;  // FlowLM RoPE cos/sin table [max_ctx][32][2]

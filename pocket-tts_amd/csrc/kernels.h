@@ -186,10 +186,16 @@ struct RowMap {
   const int* pos_arr;
   const int* tab;
 };
+// Shared voice prefixes (FlowLM cache): when `pre` is set, positions < pre_len[slot] of slot
+// `slot` live in the voice's own cache pre[slot] ([NL][2][nh][F][64], F = pre_len[slot]; layer
+// `layer` of it) instead of the slot's rows, so every utterance of one voice reads one copy.
 struct KvStore {
   float* base;
   long slot_stride;
   int cap;
+  const float* const* pre = nullptr;
+  const int* pre_len = nullptr;
+  int layer = 0;
 };
 void qkv_rope_append(const float* P, int S, const float* dense, int M, int nh, RowMap map, KvStore kv,
                      float* Q, hipStream_t s);
@@ -337,6 +343,10 @@ struct FrontCommitArgs {
   float* eos_out;    // [B] frame eos logit (parity buffer)
   FrameFlags* flags; // [B] (parity buffer)
   int* fpos;         // FlowLM positions, += 1
+  // the next step's input projection + layer-0 norm1 of every row (k_input_ln's x, h), from the
+  // updated lat_in (Wt = input_linear transposed [32][1024])
+  const float *Wt, *lnw, *lnb;
+  float *x, *h;
 };
 void front_commit(const FrontCommitArgs& a, hipStream_t s);
 

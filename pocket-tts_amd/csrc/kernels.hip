@@ -2245,20 +2245,24 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
   const int kmax = qpos0 + nrows - 1;
   const int kmin = window > 0 ? max(0, qpos0 - window + 1) : 0;
   const int d = nh * 64;
-  const float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
-  const float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
+  const KvHead kh = kv_head(kv, slot, nh, head);
+  const float* kbase = kh.kb;
+  const float* vbase = kh.vb;
   const int cmask = kv.cap - 1;
   auto kidx = [&](int kp) { return RING ? (kp & cmask) : kp; };
+  // FlowLM prefill: keys below F come from the shared voice prefix (never in a wrapped ring)
+  auto kaddr = [&](int kp) { return (FUSE || kp >= kh.F ? kbase + (long)kidx(kp) * 64 : kh.pk + (long)kp * 64); };
+  auto vaddr = [&](int kp) { return (FUSE || kp >= kh.F ? vbase + (long)kidx(kp) * 64 : kh.pv + (long)kp * 64); };
   const int ntiles = (kmax - kmin + 16) / 16;
   float4 kf[4], vf[4];
   auto load = [&](int t) {
     const int kt = kmin + 16 * t;
-    const float4* kr = reinterpret_cast<const float4*>(kbase + (long)kidx(min(kt + c, kmax)) * 64 + 16 * G);
+    const float4* kr = reinterpret_cast<const float4*>(kaddr(min(kt + c, kmax)) + 16 * G);
 #pragma unroll
     for (int i = 0; i < 4; ++i) kf[i] = kr[i];
 #pragma unroll
     for (int sidx = 0; sidx < 4; ++sidx)
-      vf[sidx] = *reinterpret_cast<const float4*>(vbase + (long)kidx(min(kt + 4 * G + sidx, kmax)) * 64 + 4 * c);
+      vf[sidx] = *reinterpret_cast<const float4*>(vaddr(min(kt + 4 * G + sidx, kmax)) + 4 * c);
   };
   // a wave whose first key tile holds only keys older than this step's appended rows issues its
   // loads now, so their latency overlaps the append below (the append never evicts a key of the
@@ -2424,11 +2428,23 @@ __global__ __launch_bounds__(64 * NW) void k_attn_decode_qkv(const float* __rest
   const bool append = qp < kv.cap;
   qp = min(qp, kv.cap - 1);
   const int d = nh * 64, ld = 3 * d;
-  float* kbase = kv.base + (long)slot * kv.slot_stride + (long)head * kv.cap * 64;
-  float* vbase = kv.base + (long)slot * kv.slot_stride + (long)(nh + head) * kv.cap * 64;
+  const KvHead kh = kv_head(kv, slot, nh, head);
+  float* kbase = kh.kb;
+  float* vbase = kh.vb;
   const int last = qp - 1;
   float4 k[KQ], v[KQ];
   auto load_block = [&](int base) {
+    if (base < kh.F) {  // (part of) the block in the shared voice prefix: cached loads, since
+                        // every row of the voice reads these lines (wave-uniform branch)
+#pragma unroll
+      for (int i = 0; i < KQ; ++i) {
+        const int j = min(base + 4 * i + g, last);
+        const long off = (long)j * 64 + c4;
+        k[i] = *reinterpret_cast<const float4*>((j < kh.F ? kh.pk : kbase) + off);
+        v[i] = *reinterpret_cast<const float4*>((j < kh.F ? kh.pv : vbase) + off);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < KQ; ++i) {
       const long off = (long)min(base + 4 * i + g, last) * 64 + c4;
@@ -2570,6 +2586,8 @@ void attention16_qkv(const float* qkv, int M, int nh, RowMap map, KvStore kv, in
 }
 
 void attention(const float* Q, int M, int nh, RowMap map, KvStore kv, int window, int qg, float* O, hipStream_t s) {
+  if (kv.pre != nullptr && (qg != 16 || window > 0))
+    throw std::runtime_error("attention: shared voice prefixes need the 16-row causal kernel");
   if (qg == 1 && window <= 0) {
     hipLaunchKernelGGL(k_attn_decode, dim3(M, nh), dim3(256), cap_lds(k_attn_decode, g_wg_cap), s, Q, nh, map, kv, O);
   } else if (qg == 16) {
@@ -2780,14 +2798,54 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
   if (threadIdx.x == 0) a.mpos[b] += 16 * nv;
 }
 
-// one 64-thread block per row
-__global__ __launch_bounds__(64) void k_front_commit(FrontCommitArgs a) {
+// x[m] = lat[m] W^T (K = 32) for the 4 columns n.. of this thread, and h[m] = LN(x[m]) (eps 1e-5)
+// over the 256 threads of the workgroup (one row): flow_lm.rs:117 input_linear +
+// transformer.rs:66-90 norm1 of layer 0. The weight arrives transposed, Wt [32][1024], so the 64
+// lanes of a wave read one contiguous 1-KB run of Wt[k] per load. lat: the row's 32 inputs.
+__device__ __forceinline__ void input_ln_row(const float* lat, const float* __restrict__ Wt,
+                                             const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                             float* __restrict__ xr, float* __restrict__ hr, float* sh) {
+  const int n = 4 * threadIdx.x;  // N = 1024
+  float4 lv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lv[j] = *reinterpret_cast<const float4*>(lat + 4 * j);
+  float4 wv[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) wv[k] = *reinterpret_cast<const float4*>(Wt + (long)k * 1024 + n);
+  float acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // same summation order as the row-major form: ((k0 k1) + (k2 k3)) per float4
+      const float a0 = lv[j].x * (&wv[4 * j].x)[q], a1 = lv[j].y * (&wv[4 * j + 1].x)[q];
+      const float a2 = lv[j].z * (&wv[4 * j + 2].x)[q], a3 = lv[j].w * (&wv[4 * j + 3].x)[q];
+      t += (a0 + a1) + (a2 + a3);
+    }
+    acc[q] = t;
+  }
+  const float4 v = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(xr + n) = v;
+  const float mean = block_sum((v.x + v.y) + (v.z + v.w), sh) / 1024.f;
+  const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+  const float den = sqrtf(block_sum((d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w), sh) / 1024.f + 1e-5f);
+  const float4 w4 = *reinterpret_cast<const float4*>(lnw + n), b4 = *reinterpret_cast<const float4*>(lnb + n);
+  *reinterpret_cast<float4*>(hr + n) =
+      make_float4(d.x / den * w4.x + b4.x, d.y / den * w4.y + b4.y, d.z / den * w4.z + b4.z, d.w / den * w4.w + b4.w);
+}
+
+// one 256-thread block per row: the EOS rule and frame flags (lane 0), the frame's latent, then
+// the next step's x / h rows from the updated backbone input (the step's first launch, folded in)
+__global__ __launch_bounds__(256) void k_front_commit(FrontCommitArgs a) {
   front_prio();
+  __shared__ float s_lat[32];
+  __shared__ float sh[4];
   const int b = blockIdx.x, t = threadIdx.x;
   SlotState& ss = a.st[b];
   const int valid = ss.active;
   const float e = a.eos[b];                       // loaded with `active`: one round trip
   const float cv = t < 32 ? a.cur[b * 32 + t] : 0.f;
+  const float li = t < 32 ? a.lat_in[b * 32 + t] : 0.f;
   __syncthreads();  // every lane has read `active` before lane 0 updates the state
   if (t == 0) {
     FrameFlags f{0, 0};
@@ -2806,11 +2864,15 @@ __global__ __launch_bounds__(64) void k_front_commit(FrontCommitArgs a) {
   if (t < 32) {
     a.lat_out[b * 32 + t] = cv;
     if (valid) a.lat_in[b * 32 + t] = cv;
+    s_lat[t] = valid ? cv : li;
   }
+  if (!a.Wt) return;  // uniform
+  __syncthreads();
+  input_ln_row(s_lat, a.Wt, a.lnw, a.lnb, a.x + (long)b * 1024, a.h + (long)b * 1024, sh);
 }
 
 void front_commit(const FrontCommitArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_front_commit, dim3(a.B), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_front_commit, dim3(a.B), dim3(256), 0, s, a);
 }
 
 void step_commit(const CommitArgs& a, hipStream_t s) {
@@ -3509,41 +3571,15 @@ __global__ __launch_bounds__(64 * FH_WAVES) void k_flow_head(FlowHeadArgs a) {
 
 // FlowLM input projection + the first layer's norm1 in one launch (flow_lm.rs:117 input_linear,
 // transformer.rs:66-90 norm1): x[m] = lat[m] W^T (K = 32, no bias), h[m] = LN(x[m]) (eps 1e-5).
-// One workgroup per row, 4 output columns per thread; replaces a split-K GEMM + row reduce.
-// The weight arrives transposed, Wt [32][1024] (made at finalize), so the 64 lanes of a wave read
-// one contiguous 1-KB run of Wt[k] per load instead of 64 rows 512 B apart.
+// One workgroup per row (input_ln_row). The step graphs fold this into k_front_commit of the step
+// before; this launch refreshes every row after anything else wrote x / h or lat_in.
 __global__ __launch_bounds__(256) void k_input_ln(const float* __restrict__ lat, const float* __restrict__ Wt,
                                                   const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                   float* __restrict__ x, float* __restrict__ h) {
   front_prio();
   __shared__ float sh[4];
-  const int m = blockIdx.x, n = 4 * threadIdx.x;  // N = 1024
-  float4 lv[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) lv[j] = *reinterpret_cast<const float4*>(lat + (long)m * 32 + 4 * j);
-  float4 wv[32];
-#pragma unroll
-  for (int k = 0; k < 32; ++k) wv[k] = *reinterpret_cast<const float4*>(Wt + (long)k * 1024 + n);
-  float acc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float t = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {  // same summation order as the row-major form: ((k0 k1) + (k2 k3)) per float4
-      const float a0 = lv[j].x * (&wv[4 * j].x)[q], a1 = lv[j].y * (&wv[4 * j + 1].x)[q];
-      const float a2 = lv[j].z * (&wv[4 * j + 2].x)[q], a3 = lv[j].w * (&wv[4 * j + 3].x)[q];
-      t += (a0 + a1) + (a2 + a3);
-    }
-    acc[q] = t;
-  }
-  const float4 v = make_float4(acc[0], acc[1], acc[2], acc[3]);
-  *reinterpret_cast<float4*>(x + (long)m * 1024 + n) = v;
-  const float mean = block_sum((v.x + v.y) + (v.z + v.w), sh) / 1024.f;
-  const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
-  const float den = sqrtf(block_sum((d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w), sh) / 1024.f + 1e-5f);
-  const float4 w4 = *reinterpret_cast<const float4*>(lnw + n), b4 = *reinterpret_cast<const float4*>(lnb + n);
-  *reinterpret_cast<float4*>(h + (long)m * 1024 + n) =
-      make_float4(d.x / den * w4.x + b4.x, d.y / den * w4.y + b4.y, d.z / den * w4.z + b4.z, d.w / den * w4.w + b4.w);
+  const int m = blockIdx.x;
+  input_ln_row(lat + (long)m * 32, Wt, lnw, lnb, x + (long)m * 1024, h + (long)m * 1024, sh);
 }
 
 void input_ln(const float* lat, const float* Wt, const float* lnw, const float* lnb, float* x, float* h, int M,

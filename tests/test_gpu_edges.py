@@ -240,3 +240,52 @@ def test_nan_latent_propagates_without_stalling_the_head_chain(gpu_engine, oracl
     ref = s.step(lat)
     np.testing.assert_allclose(r.latents[0], ref["latent"], atol=LAT_TOL)
     assert pcm_err(r.pcm[0] - ref["pcm"]) <= PCM_TOL
+
+
+def test_shared_voice_prefix_outlives_destroyed_voice(oracle):
+    """Slots read a voice's prefix from the voice's own cache (one copy per voice):
+    two slots share voice A, a third row holds voice B of another length. Destroying A while both
+    of its utterances run defers the free to the last slot that lets go of it (re-admission with
+    B, then slot_close); every frame matches the oracle, including the re-admitted row's."""
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    eng = pt.Engine(device=0, max_slots=3, max_ctx=128, seed=0x5EED, pipeline=True)
+    try:
+        pa, pb = d["prompt"][:7], (d["prompt"][:11] * 0.9).astype(np.float32)
+        ia, ia2, ib = d["text_ids"][:4], d["text_ids"][3:9], d["text_ids"][1:6]
+        va, vb = eng.voice_from_prompt(pa), eng.voice_from_prompt(pb)
+        eng.open_many([0, 1, 2], [va, va, vb], [ia, ia2, ib], [_params(max_frames=10)] * 3)
+        va.close()  # both of A's utterances still read its prefix
+        refs = [_oracle_frames(oracle, pa, ia, 10), _oracle_frames(oracle, pa, ia2, 10),
+                _oracle_frames(oracle, pb, ib, 10)]
+        got = [[], [], []]
+        for _ in range(eng.frame_lag()[0] + 4):
+            r = eng.step(3)
+            for b in range(3):
+                if r.valid[b]:
+                    got[b].append((r.latents[b].copy(), r.pcm[b].copy()))
+        eng.open(0, vb, ib, _params(max_frames=3))  # row 0 lets go of A; row 1 still holds it
+        ref0 = _oracle_frames(oracle, pb, ib, 3)
+        got0 = []
+        for _ in range(eng.frame_lag()[0] + 8):
+            r = eng.step(3)
+            if r.valid[0]:
+                got0.append((r.latents[0].copy(), r.pcm[0].copy()))
+            for b in (1, 2):
+                if r.valid[b]:
+                    got[b].append((r.latents[b].copy(), r.pcm[b].copy()))
+        eng.close_slot(1)  # the last reference: A is freed here
+        for b in range(3):
+            assert len(got[b]) >= 4
+            for i, (lat, pcm) in enumerate(got[b]):
+                np.testing.assert_allclose(lat, refs[b][i]["latent"], atol=LAT_TOL)
+                assert pcm_err(pcm - refs[b][i]["pcm"]) <= PCM_TOL
+        assert len(got0) == 3
+        for i, (lat, pcm) in enumerate(got0):
+            np.testing.assert_allclose(lat, ref0[i]["latent"], atol=LAT_TOL)
+            assert pcm_err(pcm - ref0[i]["pcm"]) <= PCM_TOL
+        r = eng.step(3)  # the engine keeps stepping with the freed voice's rows closed
+        assert not r.valid[1]
+    finally:
+        eng.close()
