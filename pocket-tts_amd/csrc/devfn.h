@@ -28,8 +28,22 @@ __device__ __forceinline__ void front_prio() {
   else if (p == 2) __builtin_amdgcn_s_setprio(2);
   else if (p == 1) __builtin_amdgcn_s_setprio(1);
 }
+// the same for back-part (Mimi decode) tiles: PTTS_BACK_PRIO, set_back_prio (probe builds)
+extern __device__ int g_back_prio;
+__device__ __forceinline__ void back_prio() {
+  const int p = __builtin_amdgcn_readfirstlane(g_back_prio);
+  if (p >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+}
+// front-part skip probe (PTTS_FRONT_SKIP, results wrong): bit 0 the skinny GEMMs' weight loads,
+// bit 1 their MFMAs, bit 2 the step attention's cached K / V loads
+extern __device__ int g_front_skip;
+__device__ __forceinline__ int front_skip() { return __builtin_amdgcn_readfirstlane(g_front_skip); }
 #else
 __device__ __forceinline__ void front_prio() {}
+__device__ __forceinline__ void back_prio() {}
+__device__ __forceinline__ constexpr int front_skip() { return 0; }
 #endif
 
 __device__ __forceinline__ float gelu_tanh(float x) {

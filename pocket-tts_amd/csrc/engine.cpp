@@ -177,6 +177,12 @@ Engine::Engine(const ptts_engine_config& cfg) {
   vlen_ = (int*)dalloc(B + 1);
   slot_voice_.assign(B, nullptr);
   share_voice_ = probe_env("PTTS_NO_SHARED_VOICE") == nullptr;
+#ifdef PTTS_PROBES
+  if (probe_env("PTTS_STAMPS")) {
+    stamp_ring_ = (unsigned long long*)dalloc((size_t)STAMP_CAP * 4);
+    stamp_ctr_ = (unsigned*)dalloc(1);
+  }
+#endif
   // pipelined stepping: the back part's kernels run at most one workgroup per CU, so the
   // latency-bound front part always finds room on every CU (measured 0.735 -> 0.688 ms per step
   // for the GEMMs alone; tools/sweep_env.sh)
@@ -186,6 +192,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
   // buffers measured 0.5% slower).
   if (probe_env("PTTS_BACK_WG_CAP")) back_cap_ = atoi(probe_env("PTTS_BACK_WG_CAP"));
   if (probe_env("PTTS_FRONT_PRIO")) set_front_prio(atoi(probe_env("PTTS_FRONT_PRIO")));
+  if (probe_env("PTTS_BACK_PRIO")) set_back_prio(atoi(probe_env("PTTS_BACK_PRIO")));
+  if (probe_env("PTTS_FRONT_SKIP")) set_front_skip(atoi(probe_env("PTTS_FRONT_SKIP")));
   ysilu_ = dalloc((size_t)lsd_ * B * FD);
   mods_ = dalloc((size_t)lsd_ * B * NADA);
   xf_ = dalloc((size_t)B * FD);
@@ -275,6 +283,20 @@ Engine::~Engine() {
   (void)hipSetDevice(dev_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (stream_be_) (void)hipStreamSynchronize(stream_be_);
+#ifdef PTTS_PROBES
+  if (stamp_ring_) {  // tag (part << 8 | buffer << 1 | end), then the 100-MHz realtime count
+    unsigned n = 0;
+    std::vector<unsigned long long> r((size_t)STAMP_CAP * 2);
+    if (hipMemcpy(&n, stamp_ctr_, 4, hipMemcpyDeviceToHost) == hipSuccess &&
+        hipMemcpy(r.data(), stamp_ring_, r.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
+      if (FILE* f = fopen(probe_env("PTTS_STAMPS"), "w")) {
+        for (int p = 0; p < 2; ++p)
+          for (size_t i = 0; i < stamp_names_[p].size(); ++i) fprintf(f, "# %d %zu %s\n", p, i, stamp_names_[p][i].c_str());
+        for (unsigned i = 0; i < std::min(n, STAMP_CAP); ++i) fprintf(f, "%llu %llu\n", r[2 * i], r[2 * i + 1]);
+        fclose(f);
+      }
+  }
+#endif
   for (int s = 0; s < (int)slot_voice_.size(); ++s) voice_release(s, true);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
@@ -1409,7 +1431,24 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
   // per-op cap override for back-part launches: PTTS_OP_CAP="name=cap,..." (tuning)
   const char* opcap = part == 1 && pipeline_ ? probe_env("PTTS_OP_CAP") : nullptr;
   try {
+#ifdef PTTS_PROBES
+    if (stamp_ring_) stamp(stamp_ring_, stamp_ctr_, (unsigned)(part << 8 | hb << 1), cs);
+#endif
+#ifdef PTTS_PROBES
+    // PTTS_STAMP_OPS: a stamp ahead of every op as well (two back to back first: the stamp cost)
+    const bool op_stamps = stamp_ring_ && probe_env("PTTS_STAMP_OPS");
+    if (op_stamps) {
+      stamp(stamp_ring_, stamp_ctr_, 0x10000u | part << 12 | 0xFFEu, cs);
+      stamp(stamp_ring_, stamp_ctr_, 0x10000u | part << 12 | 0xFFFu, cs);
+      stamp_names_[part].clear();
+      for (const Op& op : ops) stamp_names_[part].push_back(op.name);
+    }
+    unsigned op_i = 0;
+#endif
     for (const Op& op : ops) {
+#ifdef PTTS_PROBES
+      if (op_stamps) stamp(stamp_ring_, stamp_ctr_, 0x10000u | part << 12 | op_i++, cs);
+#endif
       if (opcap) {
         int cap = back_cap_;
         const std::string e(opcap), key = op.name + "=";
@@ -1434,6 +1473,9 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
       PTTS_HIP(hipMemcpyAsync(h_meta_[hb], meta_[hb], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
                               cs));
     }
+#ifdef PTTS_PROBES
+    if (stamp_ring_) stamp(stamp_ring_, stamp_ctr_, (unsigned)(part << 8 | hb << 1 | 1), cs);
+#endif
   } catch (...) {
     set_wg_cap(0);
     (void)hipStreamEndCapture(cs, &g);

@@ -278,9 +278,16 @@ struct FlowHeadArgs {
 // Launches issued while a cap > 0 is set reserve dynamic LDS so that at most `cap` workgroups of
 // each kernel share a CU (0 = no cap). Per host thread; the engine sets it around graph capture.
 void set_wg_cap(int cap);
+#ifdef PTTS_PROBES
+// one {tag, s_memrealtime} record appended to a device ring (tools/stamps.py)
+constexpr unsigned STAMP_CAP = 1u << 16;
+void stamp(unsigned long long* ring, unsigned* ctr, unsigned tag, hipStream_t s);
+#endif
 // Issue priority of the front part's waves (s_setprio 0..3) when they share a SIMD with back-part
 // waves: probe builds only (PTTS_FRONT_PRIO), for A/B runs; a no-op in product builds.
 void set_front_prio(int prio);
+void set_back_prio(int prio);  // probe builds only
+void set_front_skip(int v);    // probe builds only
 bool flow_head_fits(int B);
 // x0 = cur W_in^T + b_in into hand-off region 0 as its own launch (the adaLN reduce's side job,
 // for replaying k_flow_head alone)

@@ -36,8 +36,20 @@ void set_front_prio(int prio) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_front_prio), &prio, sizeof prio) != hipSuccess)
     throw std::runtime_error("set_front_prio failed");
 }
+__device__ int g_back_prio = 0;
+__device__ int g_front_skip = 0;
+void set_front_skip(int v) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_front_skip), &v, sizeof v) != hipSuccess)
+    throw std::runtime_error("set_front_skip failed");
+}
+void set_back_prio(int prio) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_back_prio), &prio, sizeof prio) != hipSuccess)
+    throw std::runtime_error("set_back_prio failed");
+}
 #else
 void set_front_prio(int) {}  // product builds: no front priority
+void set_back_prio(int) {}
+void set_front_skip(int) {}
 #endif
 template <typename K>
 static size_t cap_lds(K kernel, int cap) {
@@ -607,6 +619,7 @@ template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1, 
           bool BF16 = false>
 __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
   if (a.front) front_prio();
+  else back_prio();
   constexpr int TM = 32 * WM * TMW, TN = 32 * WN * TNW, ROWS = TM + TN;
   constexpr int CPR = BK / 4;        // 16-byte columns per LDS row
   constexpr int RPI = 64 / CPR;      // rows per 1-KiB wave instruction
@@ -931,6 +944,7 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
 // ---------------------------------------------------------------------------------------------
 template <int MODE, int TM, int TN>
 __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
+  back_prio();
   __shared__ float red[4 * 16 * 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1636,7 +1650,8 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   const f4v* wp = reinterpret_cast<const f4v*>(P) + (((long)t * S + z) * 4 + wave) * NV * 64 + lane;
   f4v w[NV];
 #pragma unroll
-  for (int j = 0; j < NV; ++j) w[j] = __builtin_nontemporal_load(wp + j * 64);  // once-read weights
+  for (int j = 0; j < NV; ++j)
+    w[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);  // once-read
 #pragma unroll
   for (int i = 0; i < AV; ++i) {
     const int e = tid + 256 * i, row = e / (KS / 4), c4 = e % (KS / 4);
@@ -1650,6 +1665,7 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   for (int g = 0; g < 16; ++g) acc[g] = 0.f;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
+    if (front_skip() & 2) break;
     const float4 a = *reinterpret_cast<const float4*>(ar + 4 * j);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, w[j].x, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, w[j].y, acc, 0, 0, 0);
@@ -1716,7 +1732,8 @@ __global__ __launch_bounds__(512) void k_gemv_fk(const float* __restrict__ A, in
   const f4v* ap = reinterpret_cast<const f4v*>(A) + ((long)(w * 2) * 8) * 64 + lane;
   f4v b[8], a0[8], a1[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) b[j] = __builtin_nontemporal_load(wp + j * 64);  // once-read weights
+  for (int j = 0; j < 8; ++j)
+    b[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);  // once-read
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     a0[j] = ap[j * 64];
@@ -1728,6 +1745,7 @@ __global__ __launch_bounds__(512) void k_gemv_fk(const float* __restrict__ A, in
   floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
+    if (front_skip() & 2) break;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][e], b[j][e], c0, 0, 0, 0);
@@ -2434,6 +2452,11 @@ __global__ __launch_bounds__(64 * NW) void k_attn_decode_qkv(const float* __rest
   const int last = qp - 1;
   float4 k[KQ], v[KQ];
   auto load_block = [&](int base) {
+    if (front_skip() & 4) {
+#pragma unroll
+      for (int i = 0; i < KQ; ++i) k[i] = v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      return;
+    }
     if (base < kh.F) {  // (part of) the block in the shared voice prefix: cached loads, since
                         // every row of the voice reads these lines (wave-uniform branch)
 #pragma unroll
@@ -2992,6 +3015,7 @@ void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols
 // =============================================================================================
 template <int C, int H, int TT>
 __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
+  back_prio();
   constexpr int LDE = C + 4, LDV = H + 4;
   __shared__ __attribute__((aligned(16))) float sm[(TT + 2) * LDE + TT * LDV];
   float* sE = sm;
@@ -3635,5 +3659,19 @@ void flow_head(const FlowHeadArgs& a, hipStream_t s) {
   if (!flow_head_fits(a.B)) throw std::runtime_error("flow_head: B out of range");
   hipLaunchKernelGGL(k_flow_head, dim3(flow_head_grid(a.B)), dim3(64 * FH_WAVES), 0, s, a);
 }
+
+#ifdef PTTS_PROBES
+__global__ void k_stamp(unsigned long long* ring, unsigned* ctr, unsigned tag) {
+  const unsigned i = atomicAdd(ctr, 1u);
+  if (i < STAMP_CAP) {
+    ring[2 * i] = tag;
+    ring[2 * i + 1] = wall_clock64();
+  }
+}
+
+void stamp(unsigned long long* ring, unsigned* ctr, unsigned tag, hipStream_t s) {
+  hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, s, ring, ctr, tag);
+}
+#endif
 
 }  // namespace ptts
