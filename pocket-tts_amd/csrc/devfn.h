@@ -28,7 +28,8 @@ __device__ __forceinline__ void front_prio() {
   else if (p == 2) __builtin_amdgcn_s_setprio(2);
   else if (p == 1) __builtin_amdgcn_s_setprio(1);
 }
-// the same for back-part (Mimi decode) tiles: PTTS_BACK_PRIO, set_back_prio (probe builds)
+// the back part's GEMM / conv tile waves: product builds issue at priority 3 (back_prio below);
+// probe builds take the level from PTTS_BACK_PRIO (set_back_prio, default 3, 0 = off)
 extern __device__ int g_back_prio;
 __device__ __forceinline__ void back_prio() {
   const int p = __builtin_amdgcn_readfirstlane(g_back_prio);
@@ -42,7 +43,12 @@ extern __device__ int g_front_skip;
 __device__ __forceinline__ int front_skip() { return __builtin_amdgcn_readfirstlane(g_front_skip); }
 #else
 __device__ __forceinline__ void front_prio() {}
-__device__ __forceinline__ void back_prio() {}
+// Issue priority 3 for the back part's GEMM / conv tile waves (k_gemm_glds launches outside the
+// front part, k_gemm_rb, k_resblock): where a back wave and a front wave are both ready on a SIMD,
+// the back wave issues first. In the frame-pair step the back stream runs end to end (graph stamps,
+// tools/stamps.py); steady step 0.5569 -> 0.5513 and 0.5674 -> 0.5631 ms on two boxes
+// (tools/gpu_r04o.sh, tools/gpu_r04s.sh, interleaved repeats).
+__device__ __forceinline__ void back_prio() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ constexpr int front_skip() { return 0; }
 #endif
 

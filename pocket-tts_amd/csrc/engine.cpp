@@ -383,6 +383,21 @@ void Engine::derive_gemv() {
       dst += (size_t)FF * D;
     }
     hfrag_ = dst;
+    // linear1 + linear2 as ONE launch (ffn_fused) wherever the whole-K linear1 is used;
+    // PTTS_NO_FFN (probe builds) keeps the two launches
+    if (!probe_env("PTTS_NO_FFN") && ffn_fused_supported(1, D, FF)) {
+      void* f = nullptr;
+      PTTS_HIP(hipMalloc(&f, sizeof(float) * ((size_t)NL * D * FF + 2 * FFN_HAND_FLOATS)));
+      allocs_.push_back(f);
+      float* fd = (float*)f;
+      for (int l = 0; l < NL; ++l) {
+        pack_ffn2(W(L_.fl[l].l2), fd, stream_);
+        ffnmap_[W(L_.fl[l].l2)] = fd;
+        fd += (size_t)D * FF;
+      }
+      ffn_hand_ = fd;  // both sets empty (0xFFFFFFFF) before the first launch
+      PTTS_HIP(hipMemsetD32Async(ffn_hand_, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, stream_));
+    }
   }
   size_t total = 0;
   for (const M& m : mats)
@@ -833,17 +848,35 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
     auto fk = qg == 1 && gemv_fk_supported(M, FF, D) ? fkmap_.find(W(t.l1)) : fkmap_.end();
     const bool use_fk = fk != fkmap_.end() && hfrag_;
     rr(p + ".out_reduce_ln2", S, D, ACT_NONE, true, x_, W(t.n2w), W(t.n2b), true, h_, use_fk ? hfrag_ : nullptr);
-    if (use_fk) {
-      const float* Pk = fk->second;
-      const float* A = hfrag_;
-      float* U = u_;
-      ops.push_back({p + ".ff1_gemm", [=](hipStream_t s) { gemv_fk(A, M, FF, Pk, nullptr, ACT_GELU, U, FF, s); },
-                     2.0 * M * FF * D, 4.0 * ((double)FF * D + (double)M * D + (double)M * FF)});
+    auto ffn = use_fk && ffn_hand_ ? ffnmap_.find(W(t.l2)) : ffnmap_.end();
+    if (ffn != ffnmap_.end()) {
+      // linear1 + GELU + linear2 in one launch (16 K slices of linear2 into the slabs): layer l uses
+      // hand-off set l % 2 and empties the other for layer l + 1 (the last layer's launch empties
+      // set 0 for the next step's first, NL even)
+      static_assert(NL % 2 == 0, "the fused FFN's hand-off sets alternate by layer");
+      const float *A = hfrag_, *P1 = fk->second, *P2 = ffn->second;
+      float *hand = ffn_hand_, *Pp = partial_;
+      int* err = herr_;
+      const int set = l & 1;
+      Op op{p + ".ffn", [=](hipStream_t s) { ffn_fused(A, M, P1, P2, hand, set, Pp, err, s); },
+            2.0 * M * FF * D * 2, 4.0 * (2.0 * FF * D + (double)M * D + 16.0 * M * D)};
+      // an isolated replay (time_op, overlap_probe) finds its set empty again
+      op.prep = [hand](hipStream_t s) { PTTS_HIP(hipMemsetD32Async(hand, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, s)); };
+      ops.push_back(op);
+      S = 16;
     } else {
-      linear_split(ops, p + ".ff1_gemm", h_, D, M, W(t.l1), FF, D, &S);
-      rr(p + ".ff1_reduce_gelu", S, FF, ACT_GELU, false, u_, nullptr, nullptr, false, nullptr);
+      if (use_fk) {
+        const float* Pk = fk->second;
+        const float* A = hfrag_;
+        float* U = u_;
+        ops.push_back({p + ".ff1_gemm", [=](hipStream_t s) { gemv_fk(A, M, FF, Pk, nullptr, ACT_GELU, U, FF, s); },
+                       2.0 * M * FF * D, 4.0 * ((double)FF * D + (double)M * D + (double)M * FF)});
+      } else {
+        linear_split(ops, p + ".ff1_gemm", h_, D, M, W(t.l1), FF, D, &S);
+        rr(p + ".ff1_reduce_gelu", S, FF, ACT_GELU, false, u_, nullptr, nullptr, false, nullptr);
+      }
+      linear_split(ops, p + ".ff2_gemm", u_, FF, M, W(t.l2), D, FF, &S);
     }
-    linear_split(ops, p + ".ff2_gemm", u_, FF, M, W(t.l2), D, FF, &S);
     if (l + 1 < NL)
       rr(p + ".ff2_reduce_ln1", S, D, ACT_NONE, true, x_, W(L_.fl[l + 1].n1w), W(L_.fl[l + 1].n1b), true, h_);
     else
@@ -1625,6 +1658,7 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
     PTTS_HIP(hipMemsetAsync(herr_, 0, sizeof(int), stream_));
     // a timed-out launch leaves its hand-off regions part-filled: empty every set again
     if (flm_ws_) PTTS_HIP(hipMemsetD32Async(flm_ws_, 0xFFFFFFFFu, NHB * flow_lm_set_floats(), stream_));
+    if (ffn_hand_) PTTS_HIP(hipMemsetD32Async(ffn_hand_, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, stream_));
     PTTS_HIP(hipStreamSynchronize(stream_));
     throw Error(PTTS_ERR_HIP, "persistent launch (FlowLM layers / flow head): an in-launch hand-off wait timed out");
   }

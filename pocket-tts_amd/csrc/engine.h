@@ -130,6 +130,9 @@ class Engine {
   // A-fragment-order copy of the norm2 output the step's out reduce writes for it
   std::map<const float*, const float*> fkmap_;
   float* hfrag_ = nullptr;
+  // fused feed-forward of step passes (ffn_fused): linear2 fragment copies, the hand-off sets
+  std::map<const float*, const float*> ffnmap_;
+  float* ffn_hand_ = nullptr;
   int gemv_mask_ = 0;  // matrices that take the register-resident GEMM
   void derive_gemv();
   bool own_blob_ = true, ready_ = false;

@@ -36,7 +36,7 @@ void set_front_prio(int prio) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_front_prio), &prio, sizeof prio) != hipSuccess)
     throw std::runtime_error("set_front_prio failed");
 }
-__device__ int g_back_prio = 0;
+__device__ int g_back_prio = 3;  // the product level (devfn.h back_prio)
 __device__ int g_front_skip = 0;
 void set_front_skip(int v) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_front_skip), &v, sizeof v) != hipSuccess)
@@ -1785,6 +1785,165 @@ void gemv_fk(const float* Afrag, int M, int N, const float* packed, const float*
     throw std::runtime_error("gemv_fk: unsupported shape");
   hipLaunchKernelGGL(k_gemv_fk, dim3((unsigned)(N / 16)), dim3(512), cap_lds(k_gemv_fk, g_wg_cap), s, Afrag, M, N,
                      packed, bias, act, Y, ldy);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused FlowLM feed-forward of a step pass (kernels.h ffn_fused). Workgroup L (512 threads) is
+// member i of group z, with all 16 members of a group on one XCD when workgroups are dealt to the
+// XCDs round-robin (speed only: the hand-off is coherent across XCDs). Linear2 fragments (packed
+// by pack_ffn2), float4 index (((z * 16 + i) * 8 + w) * 8 + j) * 64 + l: lane l of wave w holds
+// W2[n][k .. k + 3], n = 64 i + 32 (w & 1) + (l & 31), k = 256 z + 64 (w >> 1) + 32 (l >> 5) + 4 j:
+// the B operand of v_mfma_f32_32x32x2f32 for the wave's 32 steps (k-half l >> 5 as in k_gemv).
+// The hand-off region of group z holds linear1's 32 x 256 outputs in the matching A order: float4
+// (q * 8 + j) * 64 + l = U[row l & 31][64 q + 32 (l >> 5) + 4 j .. + 3].
+// ---------------------------------------------------------------------------------------------
+__global__ void k_pack_ffn2(const float* __restrict__ W, float* __restrict__ P) {
+  const long f = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index into P
+  if (f >= 1024L * 4096 / 4) return;
+  const int l = (int)(f & 63), j = (int)((f >> 6) & 7), w = (int)((f >> 9) & 7), i = (int)((f >> 12) & 15);
+  const int z = (int)(f >> 16);
+  const int n = 64 * i + 32 * (w & 1) + (l & 31), k = 256 * z + 64 * (w >> 1) + 32 * (l >> 5) + 4 * j;
+  reinterpret_cast<float4*>(P)[f] = *reinterpret_cast<const float4*>(W + (long)n * 4096 + k);
+}
+
+__global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, int M, const float* __restrict__ P1,
+                                                   const float* __restrict__ P2, float* __restrict__ hand, int set,
+                                                   float* __restrict__ P, int* err) {
+  front_prio();
+  __shared__ __attribute__((aligned(16))) float red[8 * 16 * 64];  // phase 1: 8 x 2 x 4 x 64; phase 2: all
+  __shared__ __attribute__((aligned(16))) float sU[32 * 16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int L = blockIdx.x, x = L & 7, jj = L >> 3;
+  const int z = 2 * x + (jj >> 4), i = jj & 15;  // group (linear2 slice), member
+  const int ct = 16 * z + i;                     // linear1 column tile: columns 16 ct .. 16 ct + 15
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  // every operand that does not depend on the hand-off, requested up front: linear1's weight and
+  // A fragments (as k_gemv_fk), then linear2's weight fragment (used after the hand-off)
+  const f4v* wp = reinterpret_cast<const f4v*>(P1) + ((long)(ct * 8 + w) * 8) * 64 + lane;
+  const f4v* ap = reinterpret_cast<const f4v*>(A) + ((long)(w * 2) * 8) * 64 + lane;
+  const f4v* w2p = reinterpret_cast<const f4v*>(P2) + ((long)((z * 16 + i) * 8 + w) * 8) * 64 + lane;
+  f4v b[8], a0[8], a1[8], b2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    b[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a0[j] = ap[j * 64];
+    a1[j] = ap[(8 + j) * 64];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    b2[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(w2p + j * 64);
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- linear1 + GELU (k_gemv_fk): two 16-row tiles, the 8 waves' partial tiles summed in LDS
+  floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (front_skip() & 2) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][e], b[j][e], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][e], b[j][e], c1, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[((w * 2 + 0) * 4 + r) * 64 + lane] = c0[r];
+    red[((w * 2 + 1) * 4 + r) * 64 + lane] = c1[r];
+  }
+  __syncthreads();
+  {  // thread tid: row tile t, register r, lane ll (C map: column ll & 15, row (ll >> 4) * 4 + r)
+    const int t = tid >> 8, r = (tid >> 6) & 3, ll = tid & 63;
+    float v = red[((0 * 2 + t) * 4 + r) * 64 + ll];
+#pragma unroll
+    for (int ww = 1; ww < 8; ++ww) v += red[((ww * 2 + t) * 4 + r) * 64 + ll];
+    const int row = 16 * t + (ll >> 4) * 4 + r;
+    sU[row * 16 + (ll & 15)] = row < M ? gelu_tanh(v) : 0.f;  // rows past M: handed off as 0
+  }
+  __syncthreads();
+  const auto hr = sc1_rsrc(hand + (long)set * FFN_HAND_FLOATS + (long)z * 32 * 256);
+  if (tid < 128) {  // publish: row m, columns 4 c4 .. 4 c4 + 3 of this tile = k_local 16 i + 4 c4
+    const int m = tid & 31, c4 = tid >> 5;
+    const int q = i >> 2, h = (i >> 1) & 1, j = 4 * (i & 1) + c4;
+    const float4 v = *reinterpret_cast<const float4*>(&sU[m * 16 + 4 * c4]);
+    fh_put(hr, (((q * 8 + j) * 64) + h * 32 + m) * 16, v);
+  }
+  // ---- linear2, slice z: wave w = (column tile w & 1, k quarter q = w >> 1); its A fragment is
+  // linear1's output of the group's members 4 q .. 4 q + 3, swept until none is empty
+  const int q = w >> 1;
+  float4 av[8];
+  bool dead = false;
+  {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) av[j] = fh_ld(hr, ((q * 8 + j) * 64 + lane) * 16);
+    unsigned spins = 0;
+    while (true) {
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ok &= !fh_empty(av[j]);
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (fh_empty(av[j])) av[j] = fh_ld(hr, ((q * 8 + j) * 64 + lane) * 16);
+      if (++spins > (1u << 20)) {
+        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dead = true;
+        break;
+      }
+    }
+  }
+  (void)dead;
+  floatx16 acc;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (front_skip() & 2) break;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, b2[j].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, b2[j].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, b2[j].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, b2[j].w, acc, 0, 0, 0);
+  }
+  // the 4 k quarters of each column tile summed in k order; slab z of P
+#pragma unroll
+  for (int g = 0; g < 16; ++g) red[(w * 16 + g) * 64 + lane] = acc[g];
+  __syncthreads();
+  {
+    float* out = P + (long)z * M * 1024;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int f = tid + 512 * rr;  // (column tile c, register g, lane ll)
+      const int c = f >> 10, g = (f >> 6) & 15, ll = f & 63;
+      float v = red[((0 * 2 + c) * 16 + g) * 64 + ll];
+#pragma unroll
+      for (int qq = 1; qq < 4; ++qq) v += red[((qq * 2 + c) * 16 + g) * 64 + ll];
+      const int row = (g & 3) + 8 * (g >> 2) + 4 * (ll >> 5);
+      if (row < M) out[(long)row * 1024 + 64 * i + 32 * c + (ll & 31)] = v;
+    }
+  }
+  // empty this workgroup's float4s of the other set for the next launch
+  if (tid < 128) {
+    const int m = tid & 31, c4 = tid >> 5;
+    const int qh = i >> 2, h = (i >> 1) & 1, j = 4 * (i & 1) + c4;
+    const auto er = sc1_rsrc(hand + (long)(set ^ 1) * FFN_HAND_FLOATS + (long)z * 32 * 256);
+    fh_st(er, (((qh * 8 + j) * 64) + h * 32 + m) * 16,
+          make_float4(__uint_as_float(~0u), __uint_as_float(~0u), __uint_as_float(~0u), __uint_as_float(~0u)));
+  }
+}
+
+bool ffn_fused_supported(int M, int D, int FF) { return M >= 1 && M <= 32 && D == 1024 && FF == 4096; }
+
+void pack_ffn2(const float* W2, float* packed, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_ffn2, dim3(1024 * 4096 / 4 / 256), dim3(256), 0, s, W2, packed);
+}
+
+void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, float* hand, int set, float* P, int* err,
+               hipStream_t s) {
+  if (!ffn_fused_supported(M, 1024, 4096) || (set != 0 && set != 1)) throw std::runtime_error("ffn_fused: bad shape");
+  hipLaunchKernelGGL(k_ffn_fused, dim3(256), dim3(512), cap_lds(k_ffn_fused, g_wg_cap), s, Afrag, M, P1, P2, hand,
+                     set, P, err);
 }
 
 bool gemv_supported(GemvShape g, int N, int K) {
