@@ -228,7 +228,7 @@ def test_generate_convenience(gpu_engine):
 def test_plan_and_kernel_timer(gpu_engine):
     names = gpu_engine.plan_ops(8)
     assert "flow.l0.qkv_gemm" in names and "seanet.conv0" in names and names[-1] == "commit"
-    assert gpu_engine.time_kernel(8, "flow.l0.out_gemm", reps=5) > 0
+    assert gpu_engine.time_kernel(8, "flow.l0.qkv_gemm", reps=5) > 0
 
 
 def test_pipelined_stepping_matches_oracle(oracle):
