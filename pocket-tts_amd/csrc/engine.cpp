@@ -128,18 +128,23 @@ Engine::Engine(const ptts_engine_config& cfg) {
   eos_ = dalloc(B);
   static_assert(sizeof(FrameFlags) == 2 * sizeof(float), "FrameFlags packs into two floats");
   meta_floats_ = (size_t)B * (LDIM + 1 + 2);
+  // frame pairs: pair p's PCM [B][2][1920] and the meta blocks of its buffers 2p, 2p + 1 in ONE
+  // device block and ONE pinned host block, so the pass delivers both frames with one copy node
+  // (a 128-B multiple per meta block keeps FrameFlags 8-B aligned)
+  const size_t mstride = (meta_floats_ + 31) / 32 * 32;
+  if (nfr_ == 2)
+    for (int p = 0; p < NHB / 2; ++p) {
+      const size_t n = (size_t)B * 2 * FRAME + 2 * mstride;
+      pcmp_[p] = dalloc(n);
+      PTTS_HIP(hipHostMalloc((void**)&h_pcmp_[p], sizeof(float) * n, hipHostMallocDefault));
+    }
   for (int q = 0; q < NHB; ++q) {  // front -> back hand-off buffers
-    meta_[q] = dalloc(meta_floats_);
+    meta_[q] = nfr_ == 2 ? pcmp_[q / 2] + (size_t)B * 2 * FRAME + (q & 1) * mstride : dalloc(meta_floats_);
     lat_out_[q] = meta_[q];                                  // 128-B aligned,
     flags_[q] = (FrameFlags*)(meta_[q] + (size_t)B * LDIM);  // so FrameFlags stay 8-B aligned
     eos_out_[q] = meta_[q] + (size_t)B * (LDIM + 2);
     pcm_[q] = dalloc((size_t)B * FRAME);
   }
-  if (nfr_ == 2)
-    for (int p = 0; p < NHB / 2; ++p) {
-      pcmp_[p] = dalloc((size_t)B * 2 * FRAME);
-      PTTS_HIP(hipHostMalloc((void**)&h_pcmp_[p], sizeof(float) * B * 2 * FRAME, hipHostMallocDefault));
-    }
   PTTS_HIP(hipHostMalloc((void**)&h_act_, sizeof(SlotState) * B, hipHostMallocDefault));
   // back part's own split-K slabs: up to 8 slices of the Mimi / conv0 rows (B * 16 x 512), 4 of the
   // stage-0 transposed conv (B * 16 x 6 * 256), per frame of a pass
@@ -232,7 +237,10 @@ Engine::Engine(const ptts_engine_config& cfg) {
 
   for (int q = 0; q < NHB; ++q) {
     PTTS_HIP(hipHostMalloc((void**)&h_pcm_[q], sizeof(float) * B * FRAME, hipHostMallocDefault));
-    PTTS_HIP(hipHostMalloc((void**)&h_meta_[q], sizeof(float) * meta_floats_, hipHostMallocDefault));
+    if (nfr_ == 2)  // inside the pair's pinned block (above)
+      h_meta_[q] = h_pcmp_[q / 2] + (size_t)B * 2 * FRAME + (q & 1) * ((meta_floats_ + 31) / 32 * 32);
+    else
+      PTTS_HIP(hipHostMalloc((void**)&h_meta_[q], sizeof(float) * meta_floats_, hipHostMallocDefault));
     memset(h_meta_[q], 0, sizeof(float) * meta_floats_);
   }
   PTTS_HIP(hipHostMalloc((void**)&h_err_, sizeof(int), hipHostMallocDefault));
@@ -311,7 +319,7 @@ Engine::~Engine() {
   for (void* p : allocs_) (void)hipFree(p);
   for (int q = 0; q < NHB; ++q) {
     if (h_pcm_[q]) (void)hipHostFree(h_pcm_[q]);
-    if (h_meta_[q]) (void)hipHostFree(h_meta_[q]);
+    if (h_meta_[q] && nfr_ != 2) (void)hipHostFree(h_meta_[q]);
   }
   for (int p = 0; p < NHB / 2; ++p)
     if (h_pcmp_[p]) (void)hipHostFree(h_pcmp_[p]);
@@ -1497,10 +1505,9 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
       // past B carry no frame
       if (nfr_ == 2 && B < max_slots_)
         PTTS_HIP(hipMemsetAsync(flags_[hb] + B, 0, sizeof(FrameFlags) * (max_slots_ - B), cs));
-    } else if (nfr_ == 2) {  // both frames of the pair leave HBM inside the pass
-      PTTS_HIP(hipMemcpyAsync(h_pcmp_[hb / 2], pcmp_[hb / 2], sizeof(float) * B * 2 * FRAME, hipMemcpyDeviceToHost, cs));
-      for (int q : {hb, (hb + 1) % nhb_})
-        PTTS_HIP(hipMemcpyAsync(h_meta_[q], meta_[q], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost, cs));
+    } else if (nfr_ == 2) {  // both frames of the pair (PCM and meta) leave HBM in one copy
+      const size_t n = (size_t)max_slots_ * 2 * FRAME + 2 * ((meta_floats_ + 31) / 32 * 32);
+      PTTS_HIP(hipMemcpyAsync(h_pcmp_[hb / 2], pcmp_[hb / 2], sizeof(float) * n, hipMemcpyDeviceToHost, cs));
     } else {  // the frame of this buffer leaves HBM inside the step (fetch() reads host memory)
       PTTS_HIP(hipMemcpyAsync(h_pcm_[hb], pcm_[hb], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, cs));
       PTTS_HIP(hipMemcpyAsync(h_meta_[hb], meta_[hb], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
@@ -1589,7 +1596,12 @@ void Engine::call_async(int B, bool run_front) {
       PTTS_HIP(hipEventRecord(ev_act_, stream_));
       act_slots_.clear();
     }
-    PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
+    // front(k) overwrites hand-off buffer k % 6, last read by the pass over frames k - 6, k - 5; an
+    // even call waits for that pass, which also read the buffer of the odd call after it, so odd
+    // calls need no wait of their own (stream order). A stream wait costs the front stream ≈ 5 us
+    // at the graph boundary even on a completed event (graph stamps, tools/gpu_r04x.sh);
+    // PTTS_ALWAYS_WAIT (probe builds) restores the per-call wait for A/B runs.
+    if ((k_ & 1) == 0 || probe_env("PTTS_ALWAYS_WAIT")) PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
     run_front_part();
     PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
     if ((k_ & 1) == 0 && k_ >= 2) {
