@@ -1378,6 +1378,10 @@ static int choose_xcd_pn(const GemmArgs& a, int gx, int gy) {
   return best;
 }
 #ifdef PTTS_PROBES
+static bool rr4_off() {  // PTTS_NO_RR4: the back part's 512-wide reduces one row per workgroup (A/B)
+  static const bool v = getenv("PTTS_NO_RR4") != nullptr;
+  return v;
+}
 static int back_probe() {
   static const int p = getenv("PTTS_BACK_PROBE") ? atoi(getenv("PTTS_BACK_PROBE")) : 0;
   return p;
@@ -1386,6 +1390,8 @@ static int front_probe() {  // the same probe on every uncapped launch (front pa
   static const int p = getenv("PTTS_FRONT_PROBE") ? atoi(getenv("PTTS_FRONT_PROBE")) : 0;
   return p;
 }
+#else
+static constexpr bool rr4_off() { return false; }
 #endif
 template <typename K>
 static void launch_tiled(K kernel, dim3 grid, int threads, hipStream_t s, const GemmArgs& a) {
@@ -2115,7 +2121,45 @@ __global__ __launch_bounds__(256) void k_row_reduce(RowReduceArgs a) {
   if (a.Hfrag) *reinterpret_cast<float4*>(a.Hfrag + fk_afrag_index(m, n)) = hv;  // n % 4 == 0: one float4
 }
 
+// The same for the back part's 512-wide rows (Mimi d_model, SEANet conv0): FOUR rows per 512-thread
+// workgroup, 128 threads per row, so a pass's 16 B rows fill the chip's one capped workgroup per
+// CU in a single round instead of four (the one-row form left half of its 256 threads idle). A
+// row's sums are its two waves' DPP sums, combined in LDS: the values, their order and every
+// rounding are those of k_row_reduce (whose other two waves add zeros).
+template <int SMAX>
+__global__ __launch_bounds__(512) void k_row_reduce4(RowReduceArgs a) {
+  if (a.front) front_prio();
+  __shared__ float sh[2][8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid >> 7;
+  const int m = blockIdx.x * 4 + r, n = 4 * (tid & 127);
+  const bool ok = m < a.M;
+  const float4 v = rr_value<SMAX>(a, ok ? m : a.M - 1, n);
+  if (ok) rr_store(a, m, n, v);
+  if (!a.ln) return;  // workgroup-uniform
+  const float s = wave_sum(ok ? (v.x + v.y) + (v.z + v.w) : 0.f);
+  if (lane == 0) sh[0][wave] = s;
+  __syncthreads();
+  const float mean = (sh[0][2 * r] + sh[0][2 * r + 1]) / 512.f;
+  const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+  const float q = wave_sum(ok ? (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w) : 0.f);
+  if (lane == 0) sh[1][wave] = q;
+  __syncthreads();
+  const float den = sqrtf((sh[1][2 * r] + sh[1][2 * r + 1]) / 512.f + a.eps);
+  if (!ok) return;
+  const float4 hv = rr_ln(a, m, n, d, den);
+  *reinterpret_cast<float4*>(a.Hout + (long)m * a.ldh + n) = hv;
+}
+
 void row_reduce(const RowReduceArgs& a, hipStream_t s) {
+  if (!a.front && a.N == 512 && !a.fill && !a.x0_hx && !a.fhm && !a.Hfrag && !rr4_off()) {
+    const dim3 g4((a.M + 3) / 4);
+    if (a.S <= 1) hipLaunchKernelGGL(k_row_reduce4<1>, g4, dim3(512), cap_lds(k_row_reduce4<1>, g_wg_cap), s, a);
+    else if (a.S <= 2) hipLaunchKernelGGL(k_row_reduce4<2>, g4, dim3(512), cap_lds(k_row_reduce4<2>, g_wg_cap), s, a);
+    else if (a.S <= 4) hipLaunchKernelGGL(k_row_reduce4<4>, g4, dim3(512), cap_lds(k_row_reduce4<4>, g_wg_cap), s, a);
+    else if (a.S <= 8) hipLaunchKernelGGL(k_row_reduce4<8>, g4, dim3(512), cap_lds(k_row_reduce4<8>, g_wg_cap), s, a);
+    else hipLaunchKernelGGL(k_row_reduce4<16>, g4, dim3(512), cap_lds(k_row_reduce4<16>, g_wg_cap), s, a);
+    return;
+  }
   dim3 grid(a.M, (a.N + 1023) / 1024);
   if (a.S <= 1) hipLaunchKernelGGL(k_row_reduce<1>, grid, dim3(256), cap_lds(k_row_reduce<1>, g_wg_cap), s, a);
   else if (a.S <= 2) hipLaunchKernelGGL(k_row_reduce<2>, grid, dim3(256), cap_lds(k_row_reduce<2>, g_wg_cap), s, a);
