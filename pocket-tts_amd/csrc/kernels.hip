@@ -2131,11 +2131,18 @@ __global__ __launch_bounds__(512) void k_row_reduce4(RowReduceArgs a) {
   if (a.front) front_prio();
   __shared__ float sh[2][8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = tid >> 7;
+  if (!a.ln) {  // no row statistics: elementwise over the 4 rows
+    const int q = a.N >> 2;  // float4 per row
+    for (int e = tid; e < 4 * q; e += 512) {
+      const int mm = blockIdx.x * 4 + e / q, nn = 4 * (e % q);
+      if (mm < a.M) rr_store(a, mm, nn, rr_value<SMAX>(a, mm, nn));
+    }
+    return;
+  }
   const int m = blockIdx.x * 4 + r, n = 4 * (tid & 127);
   const bool ok = m < a.M;
   const float4 v = rr_value<SMAX>(a, ok ? m : a.M - 1, n);
   if (ok) rr_store(a, m, n, v);
-  if (!a.ln) return;  // workgroup-uniform
   const float s = wave_sum(ok ? (v.x + v.y) + (v.z + v.w) : 0.f);
   if (lane == 0) sh[0][wave] = s;
   __syncthreads();
@@ -2151,6 +2158,8 @@ __global__ __launch_bounds__(512) void k_row_reduce4(RowReduceArgs a) {
 }
 
 void row_reduce(const RowReduceArgs& a, hipStream_t s) {
+  // (N = 512 only: the 2,048-wide reduce as 4 rows per workgroup, 4 float4 per thread, measured
+  // slower than its one-row form, profiles/r04/row_reduce4_ab.txt)
   if (!a.front && a.N == 512 && !a.fill && !a.x0_hx && !a.fhm && !a.Hfrag && !rr4_off()) {
     const dim3 g4((a.M + 3) / 4);
     if (a.S <= 1) hipLaunchKernelGGL(k_row_reduce4<1>, g4, dim3(512), cap_lds(k_row_reduce4<1>, g_wg_cap), s, a);
@@ -3006,21 +3015,25 @@ void quant_upsample(const float* const latent[2], const FrameFlags* const fl[2],
 // =============================================================================================
 // Step commit: conv histories (last P input rows per slot), counters, next backbone input.
 // =============================================================================================
+// One workgroup per row: every history of the row (P x C floats each, C % 4 == 0) and its
+// quantizer output, as float4 copies (the launch is one capped round: 32 workgroups, where a
+// workgroup per (history, row) took two rounds of scalar copies).
 __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
-  const int b = blockIdx.y;
+  const int b = blockIdx.x;
   const int nv = !a.flags[b].valid ? 0 : (a.nfr > 1 && a.flags1[b].valid ? 2 : 1);  // valid frames: a prefix
   if (nv == 0) return;
-  if ((int)blockIdx.x < a.nh) {
-    const HistDesc& hd = a.h[blockIdx.x];
-    const long n = (long)hd.P * hd.C;
+  for (int i = 0; i < a.nh; ++i) {
+    const HistDesc& hd = a.h[i];
+    const long n4 = (long)hd.P * hd.C / 4;
     const int tv = hd.T / a.nfr * nv;  // rows through the last valid frame
-    const float* src = hd.src + ((long)b * hd.T + (tv - hd.P)) * hd.C;
-    float* dst = hd.dst + (long)b * n;
-    for (long e = threadIdx.x; e < n; e += 256) dst[e] = src[e];
-    return;
+    const float4* src = reinterpret_cast<const float4*>(hd.src + ((long)b * hd.T + (tv - hd.P)) * hd.C);
+    float4* dst = reinterpret_cast<float4*>(hd.dst + (long)b * hd.P * hd.C);
+    for (long e = threadIdx.x; e < n4; e += 256) dst[e] = src[e];
   }
   // the overlap-add history of the next pass: the last valid frame's quantizer output
-  for (int c = threadIdx.x; c < 512; c += 256) a.qprev[(long)b * 512 + c] = a.qcur[((long)b * 2 + nv - 1) * 512 + c];
+  if (threadIdx.x < 128)
+    reinterpret_cast<float4*>(a.qprev + (long)b * 512)[threadIdx.x] =
+        reinterpret_cast<const float4*>(a.qcur + ((long)b * 2 + nv - 1) * 512)[threadIdx.x];
   if (threadIdx.x == 0) a.mpos[b] += 16 * nv;
 }
 
@@ -3102,7 +3115,9 @@ void front_commit(const FrontCommitArgs& a, hipStream_t s) {
 }
 
 void step_commit(const CommitArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_commit, dim3(a.nh + 1, a.B), dim3(256), cap_lds(k_commit, g_wg_cap), s, a);
+  for (int i = 0; i < a.nh; ++i)
+    if (a.h[i].C % 4) throw std::runtime_error("step_commit: history channels must be a multiple of 4");
+  hipLaunchKernelGGL(k_commit, dim3(a.B), dim3(256), cap_lds(k_commit, g_wg_cap), s, a);
 }
 
 __global__ __launch_bounds__(256) void k_slot_reset(ResetArgs a) {

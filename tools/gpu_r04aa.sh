@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: the back part's 512-wide row reduces four rows per 512-thread workgroup (one capped
+# Round 4: the back part's row reduces four rows per 512-thread workgroup (one capped round; now also
 # round instead of four) - parity tests, then A/B on the probe build (PTTS_NO_RR4=1: one row per
 # workgroup), interleaved.
 set -u
