@@ -1603,7 +1603,8 @@ void Engine::call_async(int B, bool run_front) {
     // PTTS_ALWAYS_WAIT (probe builds) restores the per-call wait for A/B runs.
     if ((k_ & 1) == 0 || probe_env("PTTS_ALWAYS_WAIT")) PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
     run_front_part();
-    PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
+    // only the odd call's front part is waited for (by the pair's back pass, below)
+    if (k_ & 1) PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
     if ((k_ & 1) == 0 && k_ >= 2) {
       const int h0 = (int)((k_ - 2) % nhb_), h1 = (h0 + 1) % nhb_, pq = (int)(((k_ - 2) / 2) & 1);
       const int rows = std::max(rows_hb_[h0], rows_hb_[h1]);
@@ -1616,8 +1617,7 @@ void Engine::call_async(int B, bool run_front) {
         }
         PTTS_HIP(hipGraphLaunch(back, stream_be_));
       }
-      PTTS_HIP(hipEventRecord(ev_back_[h0], stream_be_));
-      PTTS_HIP(hipEventRecord(ev_back_[h1], stream_be_));
+      PTTS_HIP(hipEventRecord(ev_back_[h0], stream_be_));  // the pass of buffers h0 and h1 (fetch, waits)
     }
     out_hb_ = (int)((k_ + nhb_ - 3) % nhb_);
     out_rows_ = k_ >= 3 ? rows_hb_[out_hb_] : 0;
@@ -1661,7 +1661,8 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
   // Pipelined: wait only for the back part that produced this call's frame. The front part of
   // the next frame keeps running, so the front stream never idles across calls (the next call's
   // front graph is queued behind it while this one still runs).
-  if (pipeline_) PTTS_HIP(hipEventSynchronize(ev_back_[q]));
+  // (frame pairs: the pass of buffers 2p, 2p + 1 records only the event of 2p)
+  if (pipeline_) PTTS_HIP(hipEventSynchronize(ev_back_[nfr_ == 2 ? (q & ~1) : q]));
   else sync();
   const int n = std::min(B, rows);
   if (*h_err_) {  // k_flow_head's bounded hand-off waits: a timeout poisons the frame, fail loudly
