@@ -394,12 +394,13 @@ void Engine::derive_gemv() {
     // linear1 + linear2 as ONE launch (ffn_fused) wherever the whole-K linear1 is used;
     // PTTS_NO_FFN (probe builds) keeps the two launches
     if (!probe_env("PTTS_NO_FFN") && ffn_fused_supported(1, D, FF)) {
+      ffn_groups_ = probe_env("PTTS_FFN16") ? 16 : 8;  // probe builds: the 16-group form, for A/B runs
       void* f = nullptr;
       PTTS_HIP(hipMalloc(&f, sizeof(float) * ((size_t)NL * D * FF + 2 * FFN_HAND_FLOATS)));
       allocs_.push_back(f);
       float* fd = (float*)f;
       for (int l = 0; l < NL; ++l) {
-        pack_ffn2(W(L_.fl[l].l2), fd, stream_);
+        pack_ffn2(W(L_.fl[l].l2), ffn_groups_, fd, stream_);
         ffnmap_[W(L_.fl[l].l2)] = fd;
         fd += (size_t)D * FF;
       }
@@ -866,12 +867,13 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       float *hand = ffn_hand_, *Pp = partial_;
       int* err = herr_;
       const int set = l & 1;
-      Op op{p + ".ffn", [=](hipStream_t s) { ffn_fused(A, M, P1, P2, hand, set, Pp, err, s); },
-            2.0 * M * FF * D * 2, 4.0 * (2.0 * FF * D + (double)M * D + 16.0 * M * D)};
+      const int groups = ffn_groups_;
+      Op op{p + ".ffn", [=](hipStream_t s) { ffn_fused(A, M, P1, P2, groups, hand, set, Pp, err, s); },
+            2.0 * M * FF * D * 2, 4.0 * (2.0 * FF * D + (double)M * D + (double)groups * M * D)};
       // an isolated replay (time_op, overlap_probe) finds its set empty again
       op.prep = [hand](hipStream_t s) { PTTS_HIP(hipMemsetD32Async(hand, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, s)); };
       ops.push_back(op);
-      S = 16;
+      S = groups;
     } else {
       if (use_fk) {
         const float* Pk = fk->second;

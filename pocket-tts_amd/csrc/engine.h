@@ -133,6 +133,7 @@ class Engine {
   // fused feed-forward of step passes (ffn_fused): linear2 fragment copies, the hand-off sets
   std::map<const float*, const float*> ffnmap_;
   float* ffn_hand_ = nullptr;
+  int ffn_groups_ = 8;  // linear2 K slices (slabs) of the fused feed-forward
   int gemv_mask_ = 0;  // matrices that take the register-resident GEMM
   void derive_gemv();
   bool own_blob_ = true, ready_ = false;

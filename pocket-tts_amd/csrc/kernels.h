@@ -157,19 +157,21 @@ void pack_gemv_fk(const float* W, int N, int K, float* packed, hipStream_t s);
 void gemv_fk(const float* Afrag, int M, int N, const float* packed, const float* bias, int act, float* Y, long ldy,
              hipStream_t s);
 // FlowLM feed-forward of a step pass in ONE launch (M <= 32; D = 1024, FF = 4096): linear1 + GELU as
-// gemv_fk, then linear2 split over 16 K slices of 256 into the partial slabs P [16][M][D] (the
-// following row reduce sums them). The 256 workgroups form 16 groups, one per linear2 slice: the
-// 16 workgroups of group z produce linear1's columns 256 z .. 256 z + 255 (16 each) and hand them
-// to each other through `hand` (data-as-flag, sc1 stores / loads, 32 KB per group in the MFMA
-// A-fragment order of linear2), then each computes 64 linear2 columns of slice z, its linear2
+// gemv_fk, then linear2 split over `groups` K slices into the partial slabs P [groups][M][D] (the
+// following row reduce sums them). The 256 workgroups form the groups, one per linear2 slice (8
+// groups of 32: the product; 16 of 16: probe builds): the members of group z produce linear1's
+// columns of slice z (16 each) and hand them to each other through `hand` (data-as-flag, sc1
+// stores / loads, in the MFMA A-fragment order of linear2), then each computes its linear2
+// columns of slice z, its linear2
 // weight fragment requested at the start beside linear1's. `hand` holds two sets of
 // FFN_HAND_FLOATS floats: the launch uses set `set` (emptied, 0xFFFFFFFF, by the launch before)
 // and empties the other one for the launch after. A hand-off wait that times out sets *err.
 constexpr long FFN_HAND_FLOATS = 16L * 32 * 256;
 bool ffn_fused_supported(int M, int D, int FF);
-void pack_ffn2(const float* W2, float* packed, hipStream_t s);  // linear2 [1024][4096] -> fragment order
-void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, float* hand, int set, float* P, int* err,
-               hipStream_t s);
+// groups: 16 (linear2 K slices of 256, 16 slabs) or 8 (slices of 512 with 32 members, 8 slabs)
+void pack_ffn2(const float* W2, int groups, float* packed, hipStream_t s);  // linear2 [1024][4096] -> fragment order
+void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, int groups, float* hand, int set, float* P,
+               int* err, hipStream_t s);
 void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStream_t s);
 void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
                  hipStream_t s);

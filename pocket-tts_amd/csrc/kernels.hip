@@ -1803,32 +1803,47 @@ void gemv_fk(const float* Afrag, int M, int N, const float* packed, const float*
 // The hand-off region of group z holds linear1's 32 x 256 outputs in the matching A order: float4
 // (q * 8 + j) * 64 + l = U[row l & 31][64 q + 32 (l >> 5) + 4 j .. + 3].
 // ---------------------------------------------------------------------------------------------
+template <int NG>
 __global__ void k_pack_ffn2(const float* __restrict__ W, float* __restrict__ P) {
+  constexpr int MB = 256 / NG, CT = 1024 / MB / 32;  // members per group, 32-column tiles per member
   const long f = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index into P
   if (f >= 1024L * 4096 / 4) return;
-  const int l = (int)(f & 63), j = (int)((f >> 6) & 7), w = (int)((f >> 9) & 7), i = (int)((f >> 12) & 15);
-  const int z = (int)(f >> 16);
-  const int n = 64 * i + 32 * (w & 1) + (l & 31), k = 256 * z + 64 * (w >> 1) + 32 * (l >> 5) + 4 * j;
+  const int l = (int)(f & 63), j = (int)((f >> 6) & 7), w = (int)((f >> 9) & 7);
+  const long r = f >> 12;
+  const int i = (int)(r % MB), z = (int)(r / MB);
+  const int n = (1024 / MB) * i + 32 * (w % CT) + (l & 31), k = (4096 / NG) * z + 64 * (w / CT) + 32 * (l >> 5) + 4 * j;
   reinterpret_cast<float4*>(P)[f] = *reinterpret_cast<const float4*>(W + (long)n * 4096 + k);
 }
 
+template <int NG>
 __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, int M, const float* __restrict__ P1,
                                                    const float* __restrict__ P2, float* __restrict__ hand, int set,
                                                    float* __restrict__ P, int* err) {
+  constexpr int MB = 256 / NG;        // members per group
+  constexpr int CT = 1024 / MB / 32;  // linear2 32-column tiles per member
+  constexpr int KG = 4096 / NG;       // linear2 K slice of a group = linear1 columns of the group
   front_prio();
   __shared__ __attribute__((aligned(16))) float red[8 * 16 * 64];  // phase 1: 8 x 2 x 4 x 64; phase 2: all
   __shared__ __attribute__((aligned(16))) float sU[32 * 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int L = blockIdx.x, x = L & 7, jj = L >> 3;
-  const int z = 2 * x + (jj >> 4), i = jj & 15;  // group (linear2 slice), member
-  const int ct = 16 * z + i;                     // linear1 column tile: columns 16 ct .. 16 ct + 15
+  const int L = blockIdx.x;
+  int z, i;  // group (linear2 slice), member
+  if (NG == 16) {  // a group's 16 members on one XCD (workgroups dealt round-robin; speed only)
+    const int x = L & 7, jj = L >> 3;
+    z = 2 * x + (jj >> 4);
+    i = jj & 15;
+  } else {  // contiguous members: progress needs only one group co-resident
+    z = L / MB;
+    i = L % MB;
+  }
+  const int ct = MB * z + i;  // linear1 column tile: columns 16 ct .. 16 ct + 15
   typedef float f4v __attribute__((ext_vector_type(4)));
   // every operand that does not depend on the hand-off, requested up front: linear1's weight and
   // A fragments (as k_gemv_fk), then linear2's weight fragment (used after the hand-off)
   const f4v* wp = reinterpret_cast<const f4v*>(P1) + ((long)(ct * 8 + w) * 8) * 64 + lane;
   const f4v* ap = reinterpret_cast<const f4v*>(A) + ((long)(w * 2) * 8) * 64 + lane;
-  const f4v* w2p = reinterpret_cast<const f4v*>(P2) + ((long)((z * 16 + i) * 8 + w) * 8) * 64 + lane;
+  const f4v* w2p = reinterpret_cast<const f4v*>(P2) + ((long)((z * MB + i) * 8 + w) * 8) * 64 + lane;
   f4v b[8], a0[8], a1[8], b2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j)
@@ -1868,16 +1883,16 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
     sU[row * 16 + (ll & 15)] = row < M ? gelu_tanh(v) : 0.f;  // rows past M: handed off as 0
   }
   __syncthreads();
-  const auto hr = sc1_rsrc(hand + (long)set * FFN_HAND_FLOATS + (long)z * 32 * 256);
+  const auto hr = sc1_rsrc(hand + (long)set * FFN_HAND_FLOATS + (long)z * 32 * KG);
   if (tid < 128) {  // publish: row m, columns 4 c4 .. 4 c4 + 3 of this tile = k_local 16 i + 4 c4
     const int m = tid & 31, c4 = tid >> 5;
     const int q = i >> 2, h = (i >> 1) & 1, j = 4 * (i & 1) + c4;
     const float4 v = *reinterpret_cast<const float4*>(&sU[m * 16 + 4 * c4]);
     fh_put(hr, (((q * 8 + j) * 64) + h * 32 + m) * 16, v);
   }
-  // ---- linear2, slice z: wave w = (column tile w & 1, k quarter q = w >> 1); its A fragment is
+  // ---- linear2, slice z: wave w = (column tile w % CT, 64-k part q = w / CT); its A fragment is
   // linear1's output of the group's members 4 q .. 4 q + 3, swept until none is empty
-  const int q = w >> 1;
+  const int q = w / CT;
   float4 av[8];
   bool dead = false;
   {
@@ -1912,28 +1927,28 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, b2[j].z, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, b2[j].w, acc, 0, 0, 0);
   }
-  // the 4 k quarters of each column tile summed in k order; slab z of P
+  // the 8 / CT k parts of each column tile summed in k order; slab z of P
 #pragma unroll
   for (int g = 0; g < 16; ++g) red[(w * 16 + g) * 64 + lane] = acc[g];
   __syncthreads();
   {
     float* out = P + (long)z * M * 1024;
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
+    for (int rr = 0; rr < 2 * CT; ++rr) {
       const int f = tid + 512 * rr;  // (column tile c, register g, lane ll)
       const int c = f >> 10, g = (f >> 6) & 15, ll = f & 63;
-      float v = red[((0 * 2 + c) * 16 + g) * 64 + ll];
+      float v = red[((0 * CT + c) * 16 + g) * 64 + ll];
 #pragma unroll
-      for (int qq = 1; qq < 4; ++qq) v += red[((qq * 2 + c) * 16 + g) * 64 + ll];
+      for (int qq = 1; qq < 8 / CT; ++qq) v += red[((qq * CT + c) * 16 + g) * 64 + ll];
       const int row = (g & 3) + 8 * (g >> 2) + 4 * (ll >> 5);
-      if (row < M) out[(long)row * 1024 + 64 * i + 32 * c + (ll & 31)] = v;
+      if (row < M) out[(long)row * 1024 + (1024 / MB) * i + 32 * c + (ll & 31)] = v;
     }
   }
   // empty this workgroup's float4s of the other set for the next launch
   if (tid < 128) {
     const int m = tid & 31, c4 = tid >> 5;
     const int qh = i >> 2, h = (i >> 1) & 1, j = 4 * (i & 1) + c4;
-    const auto er = sc1_rsrc(hand + (long)(set ^ 1) * FFN_HAND_FLOATS + (long)z * 32 * 256);
+    const auto er = sc1_rsrc(hand + (long)(set ^ 1) * FFN_HAND_FLOATS + (long)z * 32 * KG);
     fh_st(er, (((qh * 8 + j) * 64) + h * 32 + m) * 16,
           make_float4(__uint_as_float(~0u), __uint_as_float(~0u), __uint_as_float(~0u), __uint_as_float(~0u)));
   }
@@ -1941,15 +1956,22 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
 
 bool ffn_fused_supported(int M, int D, int FF) { return M >= 1 && M <= 32 && D == 1024 && FF == 4096; }
 
-void pack_ffn2(const float* W2, float* packed, hipStream_t s) {
-  hipLaunchKernelGGL(k_pack_ffn2, dim3(1024 * 4096 / 4 / 256), dim3(256), 0, s, W2, packed);
+void pack_ffn2(const float* W2, int groups, float* packed, hipStream_t s) {
+  if (groups == 16) hipLaunchKernelGGL(k_pack_ffn2<16>, dim3(1024 * 4096 / 4 / 256), dim3(256), 0, s, W2, packed);
+  else if (groups == 8) hipLaunchKernelGGL(k_pack_ffn2<8>, dim3(1024 * 4096 / 4 / 256), dim3(256), 0, s, W2, packed);
+  else throw std::runtime_error("pack_ffn2: 8 or 16 groups");
 }
 
-void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, float* hand, int set, float* P, int* err,
-               hipStream_t s) {
-  if (!ffn_fused_supported(M, 1024, 4096) || (set != 0 && set != 1)) throw std::runtime_error("ffn_fused: bad shape");
-  hipLaunchKernelGGL(k_ffn_fused, dim3(256), dim3(512), cap_lds(k_ffn_fused, g_wg_cap), s, Afrag, M, P1, P2, hand,
-                     set, P, err);
+void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, int groups, float* hand, int set, float* P,
+               int* err, hipStream_t s) {
+  if (!ffn_fused_supported(M, 1024, 4096) || (set != 0 && set != 1) || (groups != 8 && groups != 16))
+    throw std::runtime_error("ffn_fused: bad shape");
+  if (groups == 16)
+    hipLaunchKernelGGL(k_ffn_fused<16>, dim3(256), dim3(512), cap_lds(k_ffn_fused<16>, g_wg_cap), s, Afrag, M, P1, P2,
+                       hand, set, P, err);
+  else
+    hipLaunchKernelGGL(k_ffn_fused<8>, dim3(256), dim3(512), cap_lds(k_ffn_fused<8>, g_wg_cap), s, Afrag, M, P1, P2,
+                       hand, set, P, err);
 }
 
 bool gemv_supported(GemvShape g, int N, int K) {
