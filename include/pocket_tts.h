@@ -13,6 +13,10 @@
  *
  * Threading: calls on one engine are externally serialized, as in the
  * reference (tts_model.py:315-316; server state.rs:69). One engine per GPU.
+ *
+ * Measurement and test hooks with no reference counterpart (per-kernel timing, the step plan,
+ * the overlap probe, the GEMM-core test entry) are declared in pocket_tts_probe.h, not here:
+ * this header is only the drop-in boundary a reference maintainer binds.
  */
 #ifndef POCKET_TTS_H
 #define POCKET_TTS_H
@@ -187,13 +191,6 @@ int ptts_voice_from_audio(ptts_engine* e, const float* samples, int n_samples, i
  * rates divided by their gcd. */
 int ptts_resample_len(int n_samples, int sr_from, int sr_to);
 int ptts_resample(ptts_engine* e, const float* x, int n_samples, int sr_from, int sr_to, float* y);
-/* Test hook of the GEMM core (no reference counterpart): y = x w^T for x [m][k], w [n][k] (host
- * buffers, k % 32 == 0) on the engine's device, with the tile of kernel layout `layout`
- * (kernels.hip gemm_launch: the f32 tiles, and + 100 for their bf16-operand twins); splits > 1
- * writes the [splits][m][n] split-K partial slabs to y, tail_slices > 0 takes the split-tail path
- * (layouts 34 / 35). The tests run every shipped layout on shapes the model never runs. */
-int ptts_test_gemm(ptts_engine* e, int layout, int m, int n, int k, int splits, int tail_slices, const float* x,
-                   const float* w, float* y);
 /* Conditioning rows the voice holds (frames). */
 int ptts_voice_len(const ptts_voice* v);
 /* The [n_frames x 1024] conditioning a PCM voice was built from (host copy); for tests. */
@@ -260,19 +257,6 @@ int ptts_decode_latents(ptts_engine* e, int slot, const float* latents, int n_fr
  * until the row's last frame. pcm_out receives up to max_samples samples. */
 int ptts_generate(ptts_engine* e, int slot, const ptts_voice* v, const int32_t* ids, int n_ids,
                   const ptts_gen_params* p, float* pcm_out, int max_samples, int* n_samples);
-
-/* Measurement: replay one named kernel of the step plan `reps` times between HIP events on
- * the engine stream; returns the average duration in microseconds. */
-int ptts_time_kernel(ptts_engine* e, int n_rows, const char* name, int reps, double* avg_us);
-/* The step plan for n_rows: one line per op, "name<TAB>flops<TAB>bytes" (algorithmic cost of one
- * launch; 0 where not modelled). */
-int ptts_plan_ops(ptts_engine* e, int n_rows, char* buf, int buflen);
-
-/* Measurement: the step plan split at the FlowLM/flow-head -> Mimi boundary, timed as two
- * graphs alone and launched together on two streams; us8 = {front, back, both, both with the
- * front on a high-priority stream, 0, 0, 0, 0} microseconds per step. Clobbers engine state
- * (timing only). */
-int ptts_probe_overlap(ptts_engine* e, int n_rows, int reps, double* us8);
 
 const char* ptts_last_error(void);
 

@@ -38,6 +38,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 PROMPT_FRAMES, TEXT_TOKENS = 125, 40
+WEIGHT_BYTES_PER_FRAME = 379e6  # f32 weights read per generated frame
 
 
 def _job_inputs(u):
@@ -91,8 +92,72 @@ def worker(core, u0, n_utt, frames, lib_name):
     print(json.dumps({"t0": t0, "t1": time.monotonic()}), flush=True)
 
 
+def physical_cpus(n):
+    """Up to n CPUs of this process's affinity set on DISTINCT physical cores: one CPU per SMT
+    sibling group (/sys/devices/system/cpu/cpuN/topology/thread_siblings_list), so that no two
+    pinned workers share a core's pipelines and caches."""
+    seen, out = set(), []
+    for c in sorted(os.sched_getaffinity(0)):
+        try:
+            sib = Path(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read_text().strip()
+        except OSError:
+            sib = str(c)
+        if sib not in seen:
+            seen.add(sib)
+            out.append(c)
+        if len(out) == n:
+            break
+    return out
+
+
+def cgroup_cpus():
+    """The CPU time the container may use (cgroup v2 cpu.max quota / period), None if unlimited or
+    unreadable: the share a worker pool really runs on, whatever the affinity mask shows."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def _bw_worker(core, mb, reps):
+    import numpy as np
+
+    if core >= 0:
+        os.sched_setaffinity(0, {core})
+    a = np.ones(mb * (1 << 20) // 4, np.float32)
+    a.dot(a)  # one read of a per call (SIMD dot: memory-bound, unlike numpy's pairwise sum)
+    print("ready", flush=True)
+    sys.stdin.readline()
+    t0 = time.monotonic()
+    for _ in range(reps):
+        a.dot(a)
+    print(json.dumps({"t0": t0, "t1": time.monotonic(), "bytes": reps * a.nbytes}), flush=True)
+
+
+def mem_bandwidth(procs, mb=256, reps=8):
+    """Aggregate DRAM read rate of `procs` pinned single-thread processes streaming 256-MB arrays
+    (a float32 dot of the array with itself, far larger than any cache), started together: GB/s."""
+    cores = physical_cpus(procs)
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, __file__, "--bw-worker", str(c), str(mb), str(reps)], env=env,
+                           stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True) for c in cores]
+    try:
+        for p in ps:
+            assert p.stdout.readline().strip() == "ready"
+        for p in ps:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        res = [json.loads(p.stdout.readline()) for p in ps]
+    finally:
+        for p in ps:
+            p.wait(timeout=300)
+    wall = max(r["t1"] for r in res) - min(r["t0"] for r in res)
+    return round(sum(r["bytes"] for r in res) / wall / 1e9, 1)
+
+
 def per_core(procs, frames, utts_per_proc=1, lib_name="libptts_oracle.so"):
-    cores = sorted(os.sched_getaffinity(0))[:procs]
+    cores = physical_cpus(procs)
     env = dict(os.environ, OMP_NUM_THREADS="1")
     ps = [subprocess.Popen([sys.executable, __file__, "--worker", str(c), str(i * utts_per_proc), str(utts_per_proc),
                             str(frames), lib_name], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
@@ -136,6 +201,51 @@ def physical_cores():
     return {"sockets": len(phys) or None, "physical_cores_per_socket": cores}
 
 
+def voice_chunk_frames(F):
+    """adaptive_voice_prompt_chunk_frames (tts_model.rs:562-577), as the engine applies it."""
+    return max(F, 1) if F <= 120 else (120 if F <= 600 else (180 if F <= 1800 else 240))
+
+
+def voice(threads):
+    """The CPU port's voice state (get_voice_state_from_tensor, tts_model.rs:504-577): N(0, 1) PCM
+    of 3, 15 and 60 s at 24 kHz, and ref.wav (48 kHz, resampled by the oracle's resample_poly
+    rule) -> chunked Mimi encode -> speaker projection -> prompt prefill, one utterance with the
+    OpenMP intra-op threads of the share (the reference's Candle runs a single voice multi-
+    threaded), blocked build, one timed call each after a warm one on 3 s."""
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _oracle import resample
+
+    o = _oracle("libptts_cpu_fast.so")
+    from safetensors.numpy import load_file
+
+    g = load_file(str(ROOT / "tests" / "golden" / "ref_voice.safetensors"))
+    cases = [(f"{s}s_randn", np.random.default_rng(s).standard_normal(24000 * s).astype(np.float32), 24000)
+             for s in (3, 15, 60)]
+    cases.append(("ref_wav", g["refwav_i16"].astype(np.float32) / np.float32(32768.0), 48000))
+
+    def run(x, sr):
+        t0 = time.monotonic()
+        if sr != 24000:
+            x = resample(x, sr, 24000)
+        F = -(-x.size // 1920)
+        x = np.pad(x, (0, F * 1920 - x.size))
+        cond = o.encode(x, voice_chunk_frames(F))[0]
+        st = o.new_state(F + 8)
+        st.prefill(cond)
+        return time.monotonic() - t0, F
+
+    run(cases[0][1], 24000)
+    out = {}
+    for name, x, sr in cases:
+        t, F = run(x, sr)
+        out[name] = {"ms": round(1000 * t, 1), "audio_s": round(x.size / sr, 3), "frames": F}
+    return {"kind": "port", "build": "blocked (libptts_cpu_fast.so)", "threads": threads, "cores": threads,
+            "cases": out, "sample": "one call per case (3 / 15 / 60 s randn, ref.wav), after one warm 3-s call"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=16, help="per-core layout: worker processes (<= CPU share)")
@@ -146,14 +256,23 @@ def main():
     ap.add_argument("--scaling-procs", default="1,4",
                     help="per-core layout at these process counts too (1 utterance each): the per-core rate's "
                          "scaling over the share, which the 32-process and whole-host figures extrapolate")
+    ap.add_argument("--voice", action="store_true", help="time the voice state instead (configs[4] leg)")
+    ap.add_argument("--no-bandwidth", action="store_true", help="skip the DRAM bandwidth probe")
     ap.add_argument("--worker", nargs=5, help=argparse.SUPPRESS)
+    ap.add_argument("--bw-worker", nargs=3, help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.worker:
         c, u0, n, f, lib_name = a.worker
         worker(int(c), int(u0), int(n), int(f), lib_name)
         return
+    if a.bw_worker:
+        _bw_worker(*[int(v) for v in a.bw_worker])
+        return
     share = len(os.sched_getaffinity(0))
     procs = max(1, min(a.procs, share))
+    if a.voice:
+        print(json.dumps(voice(procs)))
+        return
     fast, plain = "libptts_cpu_fast.so", "libptts_oracle.so"
     n, wall = per_core(procs, a.frames, a.utts_per_proc, fast)
     utts = n * a.utts_per_proc
@@ -186,6 +305,22 @@ def main():
     out["per_core_scaling"] = {"realtime_per_core_by_procs": scal,
                                "note": "one utterance per pinned single-thread process (the share's own "
                                        "layout: 2 utterances each)"}
+    # why the per-core rate falls with the process count: each utterance streams the model's
+    # per-frame weights (WEIGHT_BYTES_PER_FRAME: B = 1 has no reuse across frames, and 379 MB do not
+    # fit any CPU cache), so P processes need P x rate / 0.08 s x 379 MB of DRAM reads per second;
+    # the probe measures what P pinned streaming processes get
+    out["cpu_cores"] = {"pinned": physical_cpus(procs), "distinct_physical_cores": True,
+                        "cgroup_cpu_quota": cgroup_cpus()}
+    if not a.no_bandwidth:
+        bw = {}
+        for p_ in sorted({1, procs}):
+            bw[str(p_)] = mem_bandwidth(p_)
+        need = {k: round(int(k) * scal[k] / 0.08 * WEIGHT_BYTES_PER_FRAME / 1e9, 1) for k in scal}
+        out["per_core_scaling"]["dram"] = {
+            "weight_stream_GBps_by_procs": need, "measured_read_GBps_by_procs": bw,
+            "note": "weight stream = procs x frames/s x 379 MB per frame (B = 1: every frame re-reads the "
+                    "f32 FlowLM + flow head + Mimi decoder weights); measured = float32 dots of 256-MB "
+                    "arrays on the same number of pinned cores"}
     rate = min(scal.values())
     out["extrapolated"] = {
         "per_core_32": {"value": round(32 * rate, 3), "cores": 32,

@@ -4,6 +4,7 @@
 
 #include "engine.h"
 #include "pocket_tts.h"
+#include "pocket_tts_probe.h"
 
 struct ptts_engine {
   ptts::Engine* impl = nullptr;

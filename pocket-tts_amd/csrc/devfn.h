@@ -1,4 +1,4 @@
-// Device helpers shared by the kernel files (kernels.hip, flow_lm.hip): activations, wave
+// Device helpers of the kernel file (kernels.hip): activations, wave
 // reductions, float4 arithmetic, the row -> (slot, position) map and the sc1 (agent-coherent)
 // buffer loads / stores of the in-launch hand-offs.
 #pragma once
@@ -19,7 +19,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // takes an immediate). Measured: with frame pairs, priority 3 took the steady
 // step from 0.602 to 0.580 ms, but with one frame per pass (the back part bounds the step) it
 // cost 5 % (0.583 -> 0.613 ms), and pairs + priority beat the product's one-frame passes by
-// 0.5 % only (same-box A/B, tools/bf_ab.sh): not adopted.
+// 0.5 % only (same-box A/B, alternating rounds): not adopted.
 #ifdef PTTS_PROBES
 extern __device__ int g_front_prio;
 __device__ __forceinline__ void front_prio() {
@@ -47,7 +47,7 @@ __device__ __forceinline__ void front_prio() {}
 // front part, k_gemm_rb, k_resblock): where a back wave and a front wave are both ready on a SIMD,
 // the back wave issues first. In the frame-pair step the back stream runs end to end (graph stamps,
 // tools/stamps.py); steady step 0.5569 -> 0.5513 and 0.5674 -> 0.5631 ms on two boxes
-// (tools/gpu_r04o.sh, tools/gpu_r04s.sh, interleaved repeats).
+// (profiles/r04/interference_probes.txt, interleaved repeats).
 __device__ __forceinline__ void back_prio() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ constexpr int front_skip() { return 0; }
 #endif

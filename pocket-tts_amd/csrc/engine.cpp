@@ -268,14 +268,6 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_HIP(hipEventRecord(ev_admit_, stream_));
   pipeline_ = cfg.pipeline != 0;
   head_resident_ = flow_head_max_resident(dev_);
-  flm_resident_ = flow_lm_max_resident(dev_);
-  // k_flow_lm hand-off regions: one set per front hand-off buffer, all empty (0xFFFFFFFF); the
-  // launch of step k reads set k % nhb_ and empties set (k + 1) % nhb_
-  if (probe_env("PTTS_FLM_ON")) {  // probe builds only (use_flow_lm)
-    flm_ws_ = dalloc((size_t)NHB * flow_lm_set_floats());
-    PTTS_HIP(hipMemset(flm_ws_, 0xFF, sizeof(float) * NHB * flow_lm_set_floats()));
-    PTTS_HIP(hipDeviceSynchronize());  // null-stream memset: see dalloc
-  }
 
   if (!cfg.defer_weights) {
     std::unique_ptr<TensorSource> src = cfg.weights_path && cfg.weights_path[0]
@@ -355,9 +347,8 @@ void Engine::derive_gemv() {
   // sequential stepping (the B = 1 first-chunk path, no concurrent back part) and frame-pair
   // pipelined stepping (the front part bounds the step): every matrix. Single-frame pipelined
   // stepping (the back part bounds it): qkv and linear1 stay on the LDS-DMA tile, whose smaller
-  // register footprint crowds the concurrent back part less (same-box product bench,
-  // tools/gpu_gemv_ab.sh: pairs 4,093 -> 4,395x with every matrix register-resident, single
-  // frames 4,228 -> 4,170x)
+  // register footprint crowds the concurrent back part less (same-box product bench, DESIGN.md §1:
+  // pairs 4,093 -> 4,395x with every matrix register-resident, single frames 4,228 -> 4,170x)
   int mask = pipeline_ && nfr_ == 1 ? 2 | 8 | 16 : 31;
   if (probe_env("PTTS_GEMV_MASK")) mask = atoi(probe_env("PTTS_GEMV_MASK"));  // probe builds: A/B runs
   gemv_mask_ = mask;
@@ -426,55 +417,11 @@ void Engine::derive_gemv() {
   PTTS_HIP(hipStreamSynchronize(stream_));
 }
 
-// The FlowLM step matrices in the fragment order of the persistent transformer launch (k_flow_lm):
-// in_proj and out_proj {1, 32} (8 K slices of 128), linear1 and linear2 {1, 64} (slices of 256).
-void Engine::derive_flow_lm() {
-  const size_t per_layer = (size_t)4 * D * D + (size_t)2 * D * FF;
-  void* p = nullptr;
-  PTTS_HIP(hipMalloc(&p, sizeof(float) * per_layer * NL));  // every element is written by the packing
-  allocs_.push_back(p);
-  flm_pack_ = (float*)p;
-  for (int l = 0; l < NL; ++l) {
-    const Layout::TL& t = L_.fl[l];
-    float* dst = flm_pack_ + per_layer * l;
-    pack_gemv(W(t.in_proj), 3 * D, D, GemvShape{1, 32}, dst, stream_);
-    pack_gemv(W(t.out_proj), D, D, GemvShape{1, 32}, dst + (size_t)3 * D * D, stream_);
-    pack_gemv(W(t.l1), FF, D, GemvShape{1, 64}, dst + (size_t)4 * D * D, stream_);
-    pack_gemv(W(t.l2), D, FF, GemvShape{1, 64}, dst + (size_t)4 * D * D + (size_t)D * FF, stream_);
-  }
-  // the launch's per-layer operand table (FlowLmArgs::lw)
-  std::vector<const float*> tab((size_t)NL * FL_LW);
-  for (int l = 0; l < NL; ++l) {
-    const Layout::TL& t = L_.fl[l];
-    const float* pl = flm_pack_ + per_layer * l;
-    const float* e[FL_LW] = {pl, pl + (size_t)3 * D * D, pl + (size_t)4 * D * D, pl + (size_t)4 * D * D + (size_t)D * FF,
-                             W(t.n1w), W(t.n1b), W(t.n2w), W(t.n2b)};
-    for (int i = 0; i < FL_LW; ++i) tab[(size_t)FL_LW * l + i] = e[i];
-  }
-  if (!flm_tab_) flm_tab_ = (const float**)dalloc(tab.size() * sizeof(void*) / sizeof(float));
-  PTTS_HIP(hipMemcpy(flm_tab_, tab.data(), tab.size() * sizeof(void*), hipMemcpyHostToDevice));
-  PTTS_HIP(hipGetLastError());
-  PTTS_HIP(hipStreamSynchronize(stream_));
-}
-
-// The six FlowLM layers of a step as one persistent launch (B <= 32 rows, f32 weights, the
-// launch's 256 workgroups co-resident: each waits for data the others store). Measured slower
-// than the 48 launches it replaces in every mode (sequential B = 32 step 0.829 vs
-// 0.809 ms, B = 1 0.561 vs 0.520 ms; pipelined 0.640 vs 0.584 ms, the concurrent back part
-// stretching every phase's slowest workgroup), so it runs only in probe builds on request
-// (PTTS_FLM_ON, tools/flm_ab.py, tools/flm_stamps.py).
-bool Engine::use_flow_lm(int B) const {
-  // (k_flow_lm reads every position from the slot's rows: copy-on-admit voice prefixes only)
-  if (!flm_pack_ || !flm_ws_ || !flow_lm_fits(B) || flow_lm_grid() > flm_resident_ || share_voice_) return false;
-  return probe_env("PTTS_FLM_ON") != nullptr;
-}
-
 void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   if (fp8_ && f8map_.empty()) derive_fp8();
   if (wq_ == QUANT_NONE && !fp8_ && gvmap_.empty()) derive_gemv();
-  if (wq_ == QUANT_NONE && !fp8_ && !flm_pack_ && probe_env("PTTS_FLM_ON")) derive_flow_lm();
   if (!inw_t_) {  // every element is written by the transpose below: no (null-stream) memset
     void* p = nullptr;
     PTTS_HIP(hipMalloc(&p, sizeof(float) * LDIM * D));
@@ -812,12 +759,15 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       const float* P = partial_;
       float* O = o_;
       const float* rope = rope_;
-      // per row: K and V of every head over its L cached positions (8,192 B per position), the QKV
-      // slabs, the appended K/V and the output row; QK^T + PV = 4,096 flops per position
+      // K and V of every head over the cached positions the launch reads (8,192 B per position):
+      // each row's own positions, plus ONE copy of every distinct shared voice prefix (the rows of
+      // a voice read its cache, KvStore::pre: plan_kvu_), the QKV slabs, the appended K/V and the
+      // output row; QK^T + PV = 4,096 flops per position and row
       const double L = plan_ctx_ > 0 ? plan_ctx_ : max_ctx_ / 2.0;
+      const double kvu = plan_kvu_ > 0 ? plan_kvu_ : M * L;
       ops.push_back({p + ".attention", [=](hipStream_t s) { attention_step_qkv(P, S, M, NH, map, kv, rope, O, s); },
                      (double)M * 4096.0 * L,
-                     (double)M * (8192.0 * L + 4.0 * (S * 3.0 * D + 2.0 * D + D) + 64.0 * 4 * 2)});
+                     8192.0 * kvu + (double)M * (4.0 * (S * 3.0 * D + 2.0 * D + D) + 64.0 * 4 * 2)});
     } else {
       {
         const float* P = partial_;
@@ -932,39 +882,7 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
   // ---- FlowLM step (flow_lm.rs:98-164): input_linear -> transformer -> out_norm. The input
   // projection + norm1 of layer 0 (x_, h_) were computed by the previous step's front_commit, or
   // by refresh_xh() after anything else wrote x_, h_ or lat_in_.
-  if (use_flow_lm(B)) {
-    FlowLmArgs f{};
-    f.B = B;
-    f.x = x_;
-    f.h = h_;
-    const size_t per_layer = (size_t)4 * D * D + (size_t)2 * D * FF;
-    f.lw = flm_tab_;
-    f.onw = W(L_.out_norm_w);
-    f.onb = W(L_.out_norm_b);
-    f.kv = kv_;
-    f.kv_layer = kv_layer_;
-    f.kv_slot = kv_slot_;
-    f.cap = max_ctx_;
-    f.map = RowMap{0, 1, 0, fpos_, nullptr};
-    f.rope = rope_;
-    const size_t set = flow_lm_set_floats();
-    f.ws = flm_ws_ + set * hb;
-    f.ws_next = flm_ws_ + set * ((hb + 1) % nhb_);
-    f.err = herr_;
-    f.dbg = probe_env("PTTS_FLM_DBG") ? (unsigned long long*)strtoull(probe_env("PTTS_FLM_DBG"), nullptr, 0) : nullptr;
-    // per row and layer: 2 (4 D^2 + 2 D FF) GEMM flops + 4,096 L attention flops; bytes: the
-    // step's f32 matrices once, K and V of L cached positions (8,192 B each) per row and layer
-    const double L = plan_ctx_ > 0 ? plan_ctx_ : max_ctx_ / 2.0;
-    const double fl = (double)B * NL * (2.0 * per_layer + 4096.0 * L);
-    const double by = 4.0 * per_layer * NL + (double)B * NL * (8192.0 * L + 4.0 * 8 * D);
-    Op op{"flow.layers", [f](hipStream_t s) { flow_lm(f, s); }, fl, by};
-    // an isolated replay reads its own set again: empty it first (time_op, overlap_probe)
-    float* wsc = f.ws;
-    op.prep = [wsc, set](hipStream_t s) { PTTS_HIP(hipMemsetD32Async(wsc, 0xFFFFFFFFu, set, s)); };
-    ops.push_back(op);
-  } else {
-    flow_layers(ops, B, RowMap{0, 1, 0, fpos_}, 1, true, "flow");
-  }
+  flow_layers(ops, B, RowMap{0, 1, 0, fpos_}, 1, true, "flow");
   // ---- flow head (mlp.rs:215-383): cond_embed | out_eos, EOS bookkeeping, noise
   linear_split(ops, "head.cond_eos_gemm", h_, D, B, W(L_.cond_eos_w), NCOND, D, &S);
   PTTS_REQUIRE(S <= FLOW_COND_MAX_SLABS, "head.flow_cond sums at most 16 split-K slabs");
@@ -1441,13 +1359,21 @@ std::vector<std::string> Engine::plan_names(int B) {
   std::vector<int> fp(B), mp(B);
   PTTS_HIP(hipMemcpy(fp.data(), fpos_, sizeof(int) * B, hipMemcpyDeviceToHost));
   PTTS_HIP(hipMemcpy(mp.data(), mpos_, sizeof(int) * B, hipMemcpyDeviceToHost));
-  double L = 0, Wn = 0;
+  double L = 0, Wn = 0, kvu = 0;
+  std::vector<const float*> seen;  // distinct shared voice prefixes: read once per launch
   for (int b = 0; b < B; ++b) {
     L += fp[b] + 1;
     Wn += std::min(mp[b] + UP, MCTX + UP - 1);
+    const int F = share_voice_ && h_vpre_[b] ? h_vlen_[b] : 0;
+    kvu += fp[b] + 1 - F;
+    if (F > 0 && std::find(seen.begin(), seen.end(), h_vpre_[b]) == seen.end()) {
+      seen.push_back(h_vpre_[b]);
+      kvu += F;
+    }
   }
   plan_ctx_ = L / B;
   plan_win_ = Wn / B;
+  plan_kvu_ = kvu;
   std::vector<std::string> v;
   char buf[64];
   for (auto& op : build_step(B)) {
@@ -1601,9 +1527,8 @@ void Engine::call_async(int B, bool run_front) {
     // front(k) overwrites hand-off buffer k % 6, last read by the pass over frames k - 6, k - 5; an
     // even call waits for that pass, which also read the buffer of the odd call after it, so odd
     // calls need no wait of their own (stream order). A stream wait costs the front stream ≈ 5 us
-    // at the graph boundary even on a completed event (graph stamps, tools/gpu_r04x.sh);
-    // PTTS_ALWAYS_WAIT (probe builds) restores the per-call wait for A/B runs.
-    if ((k_ & 1) == 0 || probe_env("PTTS_ALWAYS_WAIT")) PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
+    // at the graph boundary even on a completed event (graph stamps, profiles/r04/graph_boundary_ab.txt).
+    if ((k_ & 1) == 0) PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
     run_front_part();
     // only the odd call's front part is waited for (by the pair's back pass, below)
     if (k_ & 1) PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
@@ -1672,7 +1597,6 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
     *h_err_ = 0;
     PTTS_HIP(hipMemsetAsync(herr_, 0, sizeof(int), stream_));
     // a timed-out launch leaves its hand-off regions part-filled: empty every set again
-    if (flm_ws_) PTTS_HIP(hipMemsetD32Async(flm_ws_, 0xFFFFFFFFu, NHB * flow_lm_set_floats(), stream_));
     if (ffn_hand_) PTTS_HIP(hipMemsetD32Async(ffn_hand_, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, stream_));
     PTTS_HIP(hipStreamSynchronize(stream_));
     throw Error(PTTS_ERR_HIP, "persistent launch (FlowLM layers / flow head): an in-launch hand-off wait timed out");

@@ -191,13 +191,6 @@ class Engine {
   size_t hx_floats(int B) const { return (size_t)lsd_ * 13 * ((B + 15) / 16 * 16) * FD; }
   float* inw_t_ = nullptr;  // input_linear weight transposed, [32][1024] (k_input_ln)
   int *hctr_ = nullptr, *herr_ = nullptr;
-  // persistent FlowLM transformer (k_flow_lm, B <= 32): the 24 step matrices fragment-packed,
-  // its hand-off workspace (NHB sets); flm_resident_: co-resident workgroups on this device
-  float *flm_pack_ = nullptr, *flm_ws_ = nullptr;
-  const float** flm_tab_ = nullptr;  // FlowLmArgs::lw
-  int flm_resident_ = 0;
-  void derive_flow_lm();
-  bool use_flow_lm(int B) const;
   float *mx_ = nullptr, *mh_ = nullptr, *mq_ = nullptr, *mo_ = nullptr, *mqkv_ = nullptr, *mu_ = nullptr;
   float* a0_ = nullptr;
   float *cb_[3] = {}, *cv_[3] = {}, *ca_[3] = {}, *ce_[3] = {};
@@ -221,8 +214,10 @@ class Engine {
   SlotState* h_act_ = nullptr;
   std::vector<int> act_slots_;
   int admit_delay_ = 0;
-  // positions the attention ops' algorithmic costs are stated for (plan_names; 0 = a default)
-  double plan_ctx_ = 0, plan_win_ = 0;
+  // positions the attention ops' algorithmic costs are stated for (plan_names; 0 = a default):
+  // the mean FlowLM context and Mimi window of the rows, and the FlowLM cached positions one step
+  // attention launch reads (every row's own positions + each distinct shared voice prefix once)
+  double plan_ctx_ = 0, plan_win_ = 0, plan_kvu_ = 0;
   float* lat_out_[NHB] = {};
   float* eos_out_[NHB] = {};
   FrameFlags* flags_[NHB] = {};

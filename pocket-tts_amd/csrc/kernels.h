@@ -320,40 +320,6 @@ void input_ln(const float* lat, const float* Wt, const float* lnw, const float* 
 void transpose(const float* src, int rows, int cols, float* dst, hipStream_t s);
 void flow_head(const FlowHeadArgs& a, hipStream_t s);
 
-// The FlowLM step's six transformer layers (transformer.rs:66-90, attention.rs:104-283 with the
-// single-query mask skip of sdpa.rs:3-18, rope.rs:18-60) in ONE persistent launch for B <= 32
-// rows (flow_lm.hip): per layer seven phases with in-launch hand-offs instead of 48 launches.
-// Matrices arrive fragment-packed (pack_gemv layouts, WN = 1): in_proj {1, 32}, out_proj {1, 32},
-// linear1 {1, 64}, linear2 {1, 64}; lw: FL_LW pointers per layer. x [B][1024] is the residual
-// stream (in / out); h [B][1024] holds norm1(x) of layer 0 at entry and out_norm(x) at exit.
-// ws: a workspace set of flow_lm_set_floats() floats, all 0xFFFFFFFF at launch (its hand-off
-// regions; the data is its own flag); ws_next: the set of the next launch, which this launch
-// empties. err is set to 1 if a hand-off wait timed out.
-constexpr int FL_NL = 6, FL_LW = 8;
-struct FlowLmArgs {
-  int B;
-  float *x, *h;
-  // per-layer operands in device memory (a kernel-argument array indexed by the layer would be
-  // copied to scratch): lw[8 l + i], i = 0 wq, 1 wo, 2 w1, 3 w2, 4 n1w, 5 n1b, 6 n2w, 7 n2b
-  const float* const* lw;
-  const float *onw, *onb;
-  float* kv;  // layer l, slot s: kv + l * kv_layer + s * kv_slot ([2][16][cap][64])
-  long kv_layer, kv_slot;
-  int cap;
-  RowMap map;
-  const float* rope;
-  float *ws, *ws_next;
-  int* err;
-  // -DPTTS_PROBES builds: s_memrealtime stamps of workgroups 0, 37, 255 at the phase boundaries
-  // ([3][128]; tools/flm_stamps.py), or nullptr
-  unsigned long long* dbg;
-};
-bool flow_lm_fits(int B);
-size_t flow_lm_set_floats();
-int flow_lm_grid();
-int flow_lm_max_resident(int dev);  // co-resident k_flow_lm workgroups (occupancy x CUs)
-void flow_lm(const FlowLmArgs& a, hipStream_t s);
-
 // End of the front part: EOS state machine (tts_model.rs:1055-1063), frame flags, the frame's
 // latent / eos logit into the parity buffers, next backbone input, step / FlowLM position.
 struct FrontCommitArgs {

@@ -55,7 +55,8 @@ class GenParams(C.Structure):
     ]
 
 
-# (name, restype, argtypes) for every symbol include/pocket_tts.h declares
+# (name, restype, argtypes) for every symbol include/pocket_tts.h (the boundary) and
+# include/pocket_tts_probe.h (measurement / test hooks) declare
 SIGNATURES = [
     ("ptts_abi_version", C.c_int, []),
     ("ptts_build_id", C.c_char_p, []),
@@ -138,10 +139,12 @@ def build_id() -> str:
 
 def source_build_id() -> str:
     """The build id the checked-out sources produce (the Makefile's BUILD_ID rule: sha256 over the
-    sorted csrc/*.{hip,cpp,h}, include/pocket_tts.h and the Makefile, first 16 hex digits)."""
+    sorted csrc/*.{hip,cpp,h}, include/pocket_tts.h, include/pocket_tts_probe.h and the Makefile,
+    first 16 hex digits)."""
     csrc = PKG_ROOT / "csrc"
     files = sorted(p for ext in ("*.hip", "*.cpp", "*.h") for p in csrc.glob(ext))
-    files += [PKG_ROOT.parent / "include" / "pocket_tts.h", PKG_ROOT / "Makefile"]
+    files += [PKG_ROOT.parent / "include" / "pocket_tts.h", PKG_ROOT.parent / "include" / "pocket_tts_probe.h",
+              PKG_ROOT / "Makefile"]
     h = hashlib.sha256()
     for f in files:
         h.update(f.read_bytes())

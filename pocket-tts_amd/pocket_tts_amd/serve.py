@@ -313,14 +313,18 @@ class LoadBoard:
     /dev/shm that every worker of the server maps, and a worker with no free slot answers a request
     on the shared port with 307 (method and body kept) to the private port of the least-loaded peer
     that has one. Requests on a private port are always served (a request is redirected at most
-    once). One int64 pair per rank: (load, private port)."""
+    once). One int64 triple per rank: (load, private port, pid). Each worker resets its own entry
+    when it maps the board, and a peer is a target only while its pid is alive, so an entry left by
+    a crashed worker, or by an earlier server on the same port, is never redirected to."""
+
+    FIELDS = 3
 
     def __init__(self, port: int, world: int, rank: int, max_rows: int, path: str | None = None):
         import mmap
 
         self.world, self.rank, self.max_rows = world, rank, max_rows
         self.path = path or f"/dev/shm/ptts-serve-{port}-{world}.load"
-        size = 16 * world
+        size = 8 * self.FIELDS * world
         fd = os.open(self.path, os.O_RDWR | os.O_CREAT, 0o600)
         try:
             if os.fstat(fd).st_size != size:
@@ -328,7 +332,8 @@ class LoadBoard:
             self._mm = mmap.mmap(fd, size)
         finally:
             os.close(fd)
-        self.v = np.frombuffer(self._mm, np.int64).reshape(world, 2)
+        self.v = np.frombuffer(self._mm, np.int64).reshape(world, self.FIELDS)
+        self.v[rank] = (0, 0, os.getpid())  # this worker's entry, whatever an earlier run left
         self.private_port = 0
 
     def publish(self, load: int):
@@ -338,14 +343,27 @@ class LoadBoard:
         self.private_port = port
         self.v[self.rank, 1] = port
 
+    @staticmethod
+    def _alive(pid: int) -> bool:
+        if pid <= 0:
+            return False
+        try:
+            os.kill(int(pid), 0)
+        except ProcessLookupError:
+            return False
+        except PermissionError:  # exists, owned by another user: not one of this server's workers
+            return False
+        return True
+
     def redirect_target(self, own_load: int) -> int | None:
-        """The private port of the least-loaded peer with a free slot, if this worker has none."""
+        """The private port of the least-loaded live peer with a free slot, if this worker has none."""
         if own_load < self.max_rows:
             return None
-        loads, ports = self.v[:, 0].copy(), self.v[:, 1].copy()
+        loads, ports, pids = self.v[:, 0].copy(), self.v[:, 1].copy(), self.v[:, 2].copy()
         best = None
         for r in range(self.world):
-            if r != self.rank and ports[r] > 0 and loads[r] < self.max_rows and (best is None or loads[r] < loads[best]):
+            if (r != self.rank and ports[r] > 0 and loads[r] < self.max_rows and (best is None or loads[r] < loads[best])
+                    and self._alive(pids[r])):
                 best = r
         if best is None:
             return None
@@ -353,6 +371,8 @@ class LoadBoard:
         return int(ports[best])
 
     def close(self, unlink: bool = False):
+        if self.v is not None:
+            self.v[self.rank] = (0, 0, 0)  # a closed worker is no target
         self.v = None
         self._mm.close()
         if unlink:

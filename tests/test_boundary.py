@@ -10,9 +10,19 @@ import pytest
 from conftest import ROOT
 
 
-def declared_symbols():
-    text = (ROOT / "include" / "pocket_tts.h").read_text()
+def declared_symbols(header="pocket_tts.h"):
+    text = (ROOT / "include" / header).read_text()
     return sorted(set(re.findall(r"\b(ptts_[a-z0-9_]+)\s*\(", text)))
+
+
+PROBE_HOOKS = {"ptts_test_gemm", "ptts_time_kernel", "ptts_plan_ops", "ptts_probe_overlap"}
+
+
+def test_boundary_header_holds_no_measurement_hooks():
+    """pocket_tts.h is the drop-in boundary only; the measurement / test hooks live
+    in pocket_tts_probe.h."""
+    assert not PROBE_HOOKS & set(declared_symbols())
+    assert set(declared_symbols("pocket_tts_probe.h")) == PROBE_HOOKS
 
 
 def test_header_declares_the_boundary():
@@ -26,9 +36,10 @@ def test_library_exports_every_declared_symbol():
     from pocket_tts_amd import _lib
 
     L = _lib.lib()
-    for s in declared_symbols():
+    declared = set(declared_symbols()) | set(declared_symbols("pocket_tts_probe.h"))
+    for s in declared:
         assert hasattr(L, s), s
-    assert {n for n, _, _ in _lib.SIGNATURES} == set(declared_symbols())
+    assert {n for n, _, _ in _lib.SIGNATURES} == declared
 
 
 def test_blob_size_is_the_packed_model():

@@ -103,3 +103,73 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
             if i < d["latent"].shape[0]:
                 cmp("golden", frames[i][0], (d["eos_logit"][i], d["latent"][i], d["pcm"][i]), (bf, i, 0))
         print(f"back_frames={bf}: worst |d| eos/latent/pcm: vs golden {worst['golden']}, vs oracle {worst['oracle']}")
+
+
+def _oracle_run_noisy(oracle, prompt, ids, n, seed, temp):
+    from _oracle import lib as oracle_lib
+    from test_gpu_parity import _noise
+
+    oracle_lib().omp_set_num_threads(1)
+    s = oracle.new_state(320)
+    s.prefill(prompt)
+    s.prefill_tokens(ids)
+    lat, out = None, []
+    for i in range(n):
+        o = s.step(lat, noise=_noise(seed, i, temp, None))
+        lat = o["latent"]
+        out.append((o["eos_logit"], o["latent"], o["pcm"]))
+    return out
+
+
+def test_bench_exact_input_shared_voice_matches_oracle(oracle):
+    """bench.py's own job, input for input: ONE voice (bench.synth_prompt, 125 frames) admitted
+    into all 32 rows in one batched admission, so every row reads the voice's shared KV prefix
+    (KvStore::pre) rather than a copy; bench.text_ids(b); temperature 0.7 with bench.slot_seed's
+    noise streams; EOS off; 125 frames; pipelined frame pairs drained by flush calls, exactly as
+    bench.run_calls issues them. Every row and frame against its own oracle run (the same noise,
+    replayed on the host by test_gpu_parity._noise), at the f32 gates."""
+    import bench
+    import pocket_tts_amd as pt
+
+    n, temp = bench.UTT_FRAMES, 0.7
+    prompt = bench.synth_prompt()
+    ids = [bench.text_ids(b) for b in range(B)]
+    seeds = [bench.slot_seed(1, 0, b) for b in range(B)]
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    with ThreadPoolExecutor(workers) as ex:
+        futs = [ex.submit(_oracle_run_noisy, oracle, prompt, ids[b], n, seeds[b], temp) for b in range(B)]
+        eng = pt.Engine(device=0, max_slots=B, max_ctx=bench.PROMPT_FRAMES + bench.TEXT_TOKENS + n + 8,
+                        lsd_decode_steps=1, seed=0x5EED, pipeline=True, back_frames=2)
+        try:
+            voice = eng.voice_from_prompt(prompt)
+            eng.open_many(list(range(B)), [voice] * B, ids,
+                          [pt.GenerationParams(temp=temp, eos_threshold=float("inf"), frames_after_eos=3,
+                                               max_frames=n, seed=seeds[b]) for b in range(B)])
+            lag, delay = eng.frame_lag()
+            got = [[] for _ in range(B)]
+
+            def collect():
+                eng.sync()
+                r = eng.fetch(B)
+                for b in range(B):
+                    if r.valid[b]:
+                        got[b].append((float(r.eos_logits[b]), r.latents[b].copy(), r.pcm[b].copy()))
+
+            for _ in range(n + delay):
+                eng.step_async(B)
+                collect()
+            for _ in range(lag):
+                eng.flush_async(B)
+                collect()
+        finally:
+            eng.close()
+        ref = [f.result() for f in futs]
+    worst = [0.0, 0.0, 0.0]
+    for b in range(B):
+        assert len(got[b]) == n, (b, len(got[b]))
+        for i in range(n):
+            g, e = got[b][i], ref[b][i]
+            err = [abs(g[0] - e[0]), float(np.abs(g[1] - e[1]).max()), float(np.abs(g[2] - e[2]).max())]
+            worst = [max(x, y) for x, y in zip(worst, err)]
+            assert err[0] <= LAT_TOL and err[1] <= LAT_TOL and err[2] <= PCM_TOL, (b, i, err)
+    print(f"bench input (shared voice, temp {temp}): worst |d| eos/latent/pcm vs oracle {worst}")

@@ -328,3 +328,32 @@ def test_configs3_256_streams_over_8_workers(tmp_path):
             assert min(per_rank.values()) >= 16, per_rank
     finally:
         _stop_server(p)
+
+
+def test_load_board_never_redirects_to_a_dead_or_stale_worker(tmp_path):
+    """a board entry left by a crashed worker (or an earlier server on the same port)
+    must not draw 307s. Entries carry the worker's pid; a worker resets its own entry when it maps
+    the board and clears it on close."""
+    import subprocess
+    import sys
+
+    from pocket_tts_amd.serve import LoadBoard
+
+    path = str(tmp_path / "board.load")
+    b0 = LoadBoard(port=1, world=3, rank=0, max_rows=4, path=path)
+    b0.publish(4)  # rank 0 is full
+    # rank 1: an entry of a process that has exited (free slots, a port)
+    p = subprocess.Popen([sys.executable, "-c", "pass"])
+    p.wait()
+    b0.v[1] = (0, 5001, p.pid)
+    # rank 2: a stale entry with no pid at all (an earlier board layout / run)
+    b0.v[2] = (0, 5002, 0)
+    assert b0.redirect_target(4) is None
+    # a live peer with a free slot is a target; re-mapping as rank 1 resets the stale entry first
+    b1 = LoadBoard(port=1, world=3, rank=1, max_rows=4, path=path)
+    assert tuple(b0.v[1]) == (0, 0, b1.v[1, 2])
+    b1.set_private_port(6001)
+    assert b0.redirect_target(4) == 6001
+    b1.close()
+    assert b0.redirect_target(4) is None
+    b0.close(unlink=True)
