@@ -562,9 +562,42 @@ def main():
             dist.destroy_process_group()
         return
 
+    # ---- p50 first-chunk latency (config 2): text prefill + 1 step, voice precomputed
+    p50 = None
+    if not args.no_latency:
+        e1 = pt.Engine(device=local_rank, max_slots=1, max_ctx=PROMPT_FRAMES + TEXT_TOKENS + 16, seed=0x5EED)
+        v1 = e1.voice_from_prompt(synth_prompt())
+        lat = []
+        for i in range(55):
+            t = time.perf_counter()
+            e1.open(0, v1, text_ids(0), pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), max_frames=4,
+                                                             seed=i + 1))
+            rr = e1.step(1)
+            lat.append(time.perf_counter() - t)
+            assert rr.valid[0]
+        p50 = float(np.median(lat[5:]) * 1000.0)
+        e1.close()
+
+    # ---- configs[4] variants: the same job on an engine with the reference's int8 weight
+    # quantization of the FlowLM (quantize.rs; its step GEMMs stream int8 codes), and with the
+    # large FlowLM step GEMMs as fp8 W8A8 (accuracy-gated against the f32 oracle, tests/test_fp8.py).
+    # Reported beside `value`, never as it (different numerics from the f32 reference).
+    quant = fp8 = bf16 = None
+    ref_pcm = pcm_sample(eng) if not args.no_quant_variant and world == 1 and not selftest else None
+    # the same job with B distinct voices: every row reads its own 125-frame prefix (6 MB of KV)
+    # instead of the bench's one shared voice; the headline's shared-prefix benefit, made visible
+    distinct = None
+    if not args.no_distinct_voices and world == 1:
+        d_el, d_ad, _ = timed_job(eng, distinct_voices=True)
+        distinct = {"value": round(jobs * B * K * 1920 / 24000.0 / d_el, 2), "unit": "audio-sec/wall-sec",
+                    "ms_per_step": round(1000.0 * d_el / steps, 4),
+                    "steady_ms_per_step": round(1000.0 * (d_el - d_ad) / steps, 4),
+                    "voices": f"{B} distinct {PROMPT_FRAMES}-frame prompts (one per row)",
+                    "front_bytes_per_step": round(front_bytes(B, K, distinct_voices=B))}
     # ---- dominant kernel: time every op of the step plan on the engine stream (HIP events), with
     # the rows at the job's midpoint (context prompt + text + K/2, the job's mean: what the step's
-    # attention ops read on average), on the bench's own shared voice
+    # attention ops read on average), on the bench's own shared voice. Last use of this engine:
+    # the isolated replays rewrite slot state of the rows in flight
     roof, top, sum_ops_ms = None, None, None
     if not args.no_op_times:
         v_mid = eng.voice_from_prompt(synth_prompt())
@@ -627,38 +660,6 @@ def main():
         with open(args.ops_out, "w") as f:
             json.dump({"n_rows": B, "plan": [n for n, _, _ in eng.plan(B)], "ops": []}, f, indent=1)
 
-    # ---- p50 first-chunk latency (config 2): text prefill + 1 step, voice precomputed
-    p50 = None
-    if not args.no_latency:
-        e1 = pt.Engine(device=local_rank, max_slots=1, max_ctx=PROMPT_FRAMES + TEXT_TOKENS + 16, seed=0x5EED)
-        v1 = e1.voice_from_prompt(synth_prompt())
-        lat = []
-        for i in range(55):
-            t = time.perf_counter()
-            e1.open(0, v1, text_ids(0), pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), max_frames=4,
-                                                             seed=i + 1))
-            rr = e1.step(1)
-            lat.append(time.perf_counter() - t)
-            assert rr.valid[0]
-        p50 = float(np.median(lat[5:]) * 1000.0)
-        e1.close()
-
-    # ---- configs[4] variants: the same job on an engine with the reference's int8 weight
-    # quantization of the FlowLM (quantize.rs; its step GEMMs stream int8 codes), and with the
-    # large FlowLM step GEMMs as fp8 W8A8 (accuracy-gated against the f32 oracle, tests/test_fp8.py).
-    # Reported beside `value`, never as it (different numerics from the f32 reference).
-    quant = fp8 = bf16 = None
-    ref_pcm = pcm_sample(eng) if not args.no_quant_variant and world == 1 and not selftest else None
-    # the same job with B distinct voices: every row reads its own 125-frame prefix (6 MB of KV)
-    # instead of the bench's one shared voice; the headline's shared-prefix benefit, made visible
-    distinct = None
-    if not args.no_distinct_voices and world == 1:
-        d_el, d_ad, _ = timed_job(eng, distinct_voices=True)
-        distinct = {"value": round(jobs * B * K * 1920 / 24000.0 / d_el, 2), "unit": "audio-sec/wall-sec",
-                    "ms_per_step": round(1000.0 * d_el / steps, 4),
-                    "steady_ms_per_step": round(1000.0 * (d_el - d_ad) / steps, 4),
-                    "voices": f"{B} distinct {PROMPT_FRAMES}-frame prompts (one per row)",
-                    "front_bytes_per_step": round(front_bytes(B, K, distinct_voices=B))}
     eng.close()  # one engine on the GPU at a time
     if not args.no_quant_variant and world == 1:
         eq = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
