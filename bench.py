@@ -384,6 +384,9 @@ def main():
     ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2),
                     help="frames per Mimi-decode pass of pipelined stepping (ptts_engine_config.back_frames; "
                          "2, the throughput configuration: 0.559 vs 0.584 ms per steady step, DESIGN.md section 1)")
+    ap.add_argument("--back-mfma", choices=("f32", "f32x6"), default="f32",
+                    help="the back part's f32 GEMMs: f32 MFMA, or f32 products from exact three-piece bf16 "
+                         "splits (ptts_engine_config.back_mfma PTTS_BACK_F32X6, f32 accuracy)")
     ap.add_argument("--no-flush", action="store_true",
                     help="drain each job's last frames with step calls (front parts of finished rows run and "
                          "their frames are discarded) instead of ptts_flush_async")
@@ -438,6 +441,7 @@ def main():
     jobs = max(MIN_JOBS, -(-args.steps // K)) if args.profile_frames <= 0 else 1
     pipeline = not args.no_pipeline
     back_frames = args.back_frames if pipeline else 1
+    back_mfma = {"f32": 0, "f32x6": 2}[args.back_mfma]
     max_ctx = PROMPT_FRAMES + TEXT_TOKENS + K + 8
 
     def params(round_id, b, n_frames):
@@ -447,14 +451,14 @@ def main():
     # ---- engine (+ one RCCL broadcast of the packed weights at load time)
     if dist is None:
         eng = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
-                        pipeline=pipeline, back_frames=back_frames)
+                        pipeline=pipeline, back_frames=back_frames, back_mfma=back_mfma)
     else:
         import torch
 
         blob = torch.empty(pt.Engine.weight_blob_bytes() // 4, dtype=torch.float32, device=dev)
         eng = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                         weight_blob=blob.data_ptr(), defer_weights=(rank != 0), pipeline=pipeline,
-                        back_frames=back_frames)
+                        back_frames=back_frames, back_mfma=back_mfma)
         if not selftest:
             torch.cuda.synchronize()
         broadcast_weights(dist, blob)

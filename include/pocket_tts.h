@@ -35,10 +35,11 @@ extern "C" {
 #define PTTS_ERR_IO 4      /* weights file missing or malformed */
 
 /* ABI version of this header. Bumped whenever a struct below changes layout (3: cfg_yaml was
- * appended to ptts_engine_config; 4: back_frames; 5: back_bf16). A caller checks ptts_abi_version() ==
+ * appended to ptts_engine_config; 4: back_frames; 5: back_bf16; 6: that field became back_mfma, with
+ * the bf16x6 f32 mode). A caller checks ptts_abi_version() ==
  * PTTS_ABI_VERSION before passing any struct: a library built from another header reads a
  * different layout. */
-#define PTTS_ABI_VERSION 5
+#define PTTS_ABI_VERSION 6
 int ptts_abi_version(void);
 /* Build id of the loaded library: the first 16 hex digits of the sha256 over the sources it was
  * built from (pocket-tts_amd/Makefile, BUILD_ID), with "+probes" appended for a measurement build
@@ -96,14 +97,23 @@ typedef struct ptts_engine_config {
                                first). ptts_frame_lag() reports both delays. 2 is the
                                throughput setting (bench.py's default: 0.561 against 0.583 ms per
                                steady step at B = 32), 1 the low-latency one. */
-  int back_bf16;            /* 1: the Mimi decoder transformer GEMMs and the SEANet decoder convs
-                               (the back part, at >= 16 rows) multiply on
-                               v_mfma_f32_32x32x16_bf16: operands rounded to bf16, f32
-                               accumulation, f32 activations and weights in HBM. Not a reference
-                               numeric (Candle runs f32): gated on PCM accuracy vs the f32 path;
-                               the latents, EOS logits and stop frames are untouched (the back part
-                               does not feed the FlowLM). 0 = f32 (default). */
+  int back_mfma;            /* PTTS_BACK_*: how the Mimi decoder transformer GEMMs and the SEANet
+                               decoder convs (the back part, at >= 16 rows) use the matrix cores.
+                               PTTS_BACK_F32 (0): v_mfma_f32_32x32x2_f32, an exact f32 FMA chain.
+                               PTTS_BACK_F32X6 (2): f32 products on the bf16 matrix pipe: each f32
+                               operand as the exact sum of three bf16 pieces, the six piece products
+                               of order <= 2 summed in f32 (dropped terms < 2^-24 |a b|): f32
+                               accuracy (the GEMM-core tests hold it to the f32 tile's error against
+                               fp64), 6 bf16 MFMAs per 16 k instead of 8 f32 ones.
+                               PTTS_BACK_BF16 (1): operands rounded to bf16, f32 accumulation: NOT a
+                               reference numeric (Candle runs f32), gated on PCM accuracy.
+                               The latents, EOS logits and stop frames never depend on it (the back
+                               part does not feed the FlowLM). */
 } ptts_engine_config;
+
+#define PTTS_BACK_F32 0
+#define PTTS_BACK_BF16 1
+#define PTTS_BACK_F32X6 2
 
 #define PTTS_QUANT_NONE 0
 #define PTTS_QUANT_FLOW_LM 1 /* quantize_weights() over the flow_lm.* tensors */

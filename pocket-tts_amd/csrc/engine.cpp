@@ -92,8 +92,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
   fp8_ = cfg.fp8_gemm;
   PTTS_REQUIRE(cfg.back_frames >= 0 && cfg.back_frames <= 2, "back_frames must be 0, 1 or 2");
   nfr_ = cfg.pipeline && cfg.back_frames == 2 ? 2 : 1;
-  PTTS_REQUIRE(cfg.back_bf16 == 0 || cfg.back_bf16 == 1, "back_bf16 must be 0 or 1");
-  back_bf16_ = cfg.back_bf16 != 0;
+  PTTS_REQUIRE(cfg.back_mfma >= PTTS_BACK_F32 && cfg.back_mfma <= PTTS_BACK_F32X6, "unknown back_mfma mode");
+  back_mfma_ = cfg.back_mfma;
   nhb_ = nfr_ == 2 ? NHB : 3;
   int ndev = 0;
   PTTS_HIP(hipGetDeviceCount(&ndev));
@@ -417,11 +417,57 @@ void Engine::derive_gemv() {
   PTTS_HIP(hipStreamSynchronize(stream_));
 }
 
+// bf16x6 back part (back_mfma = PTTS_BACK_F32X6): every back-part GEMM / conv weight matrix split
+// into its exact three bf16 pieces (split3: hi | mid in W's f32 layout, lo as bf16), padded with
+// zero rows to a multiple of 32 (the tiles read rows < Nw). Shapes as build_back multiplies them.
+void Engine::derive_split() {
+  auto add = [&](size_t off, int N, int K) {
+    const int Nw = (N + 31) / 32 * 32;
+    void *hm = nullptr, *lo = nullptr;
+    PTTS_HIP(hipMalloc(&hm, sizeof(unsigned) * (size_t)Nw * K));
+    allocs_.push_back(hm);
+    PTTS_HIP(hipMalloc(&lo, sizeof(unsigned short) * (size_t)Nw * K));
+    allocs_.push_back(lo);
+    if (Nw > N) {
+      PTTS_HIP(hipMemsetAsync((unsigned*)hm + (size_t)N * K, 0, sizeof(unsigned) * (size_t)(Nw - N) * K, stream_));
+      PTTS_HIP(hipMemsetAsync((unsigned short*)lo + (size_t)N * K, 0, sizeof(unsigned short) * (size_t)(Nw - N) * K,
+                              stream_));
+    }
+    split3(W(off), (long)N * K, (unsigned*)hm, (unsigned short*)lo, stream_);
+    split_[W(off)] = {(const unsigned*)hm, (const unsigned short*)lo};
+  };
+  for (int l = 0; l < MNL; ++l) {
+    const Layout::TL& t = L_.mdec[l];
+    add(t.in_proj, 3 * MD, MD);
+    add(t.out_proj, MD, MD);
+    add(t.l1, MFF, MD);
+    add(t.l2, MD, MFF);
+  }
+  add(L_.dc0_w, 512, 7 * 512);
+  for (int i = 0, ch = 512; i < 3; ++i, ch /= 2) {
+    add(L_.dtr_w[i], RATIOS[i] * (ch / 2), 2 * ch);
+    add(L_.dra_w[i], ch / 4, 3 * (ch / 2));
+    add(L_.drb_w[i], ch / 2, ch / 4);
+  }
+  PTTS_HIP(hipGetLastError());
+  PTTS_HIP(hipStreamSynchronize(stream_));
+}
+
+// A bf16x6 tile (layout >= 200) reads the split copy of its weight matrix (derive_split)
+void Engine::attach_split(GemmArgs& a) const {
+  if (a.layout < 200) return;
+  auto it = split_.find(a.W);
+  PTTS_REQUIRE(it != split_.end(), "bf16x6 tile without a split weight copy");
+  a.Whm = it->second.first;
+  a.Wlo = it->second.second;
+}
+
 void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   if (fp8_ && f8map_.empty()) derive_fp8();
   if (wq_ == QUANT_NONE && !fp8_ && gvmap_.empty()) derive_gemv();
+  if (back_mfma_ == PTTS_BACK_F32X6 && split_.empty()) derive_split();
   if (!inw_t_) {  // every element is written by the transpose below: no (null-stream) memset
     void* p = nullptr;
     PTTS_HIP(hipMalloc(&p, sizeof(float) * LDIM * D));
@@ -687,6 +733,7 @@ void Engine::dense_op(std::vector<Op>& ops, const std::string& name, const float
   a.ldr = N;
   a.Y = Y;
   a.ldy = N;
+  attach_split(a);
   ops.push_back({name, [a](hipStream_t s) { gemm(a, 1, s); }, 2.0 * M * N * K,
                  4.0 * ((double)N * K + (double)M * K + (double)M * N * (R ? 2 : 1))});
 }
@@ -730,6 +777,7 @@ void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float*
   a.elu_out = elu_out;
   a.Y2 = Y2;
   const int nph = phases;
+  attach_split(a);
   if (ksplit > 1) {
     PTTS_REQUIRE((size_t)ksplit * a.M * a.N <= mpcap_, "back split-K slab buffer too small");
     a.S = ksplit;
@@ -1112,9 +1160,11 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   const bool big = B >= 16;  // B * 16 >= 256 Mimi rows: the LDS-DMA tiles fill the chip
   auto tile = [&](const std::string& op, int small_splits) {
     BackTile t = big ? back_tile(op, pipeline_) : BackTile{0, small_splits};
-    // back_bf16: the bf16-operand twin of the ILV tile (kernels.hip PTTS_GLB: layout + 100); the
-    // register-blocked and non-ILV tiles of the f32 table map to the 64 x 64 one
-    if (big && back_bf16_) t.layout = 100 + (t.layout == 35 || t.layout == 31 ? t.layout : 32);
+    // back_mfma bf16 / bf16x6: the bf16-operand / split-f32 twin of the ILV tile (kernels.hip
+    // PTTS_GLB: layout + 100, PTTS_GLX6: + 200); the register-blocked and non-ILV tiles of the f32
+    // table map to the 64 x 64 one
+    if (big && back_mfma_ == PTTS_BACK_BF16) t.layout = 100 + (t.layout == 35 || t.layout == 31 ? t.layout : 32);
+    if (big && back_mfma_ == PTTS_BACK_F32X6) t.layout = 200 + (t.layout == 35 ? t.layout : 32);
     tile_override(op, t.layout, t.splits);  // probe builds only (tools/back_tune.py)
     return t;
   };
@@ -1156,6 +1206,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     a.W = Wt;
     a.S = t.splits;
     a.partial = mpartial_;
+    attach_split(a);
     const int S = t.splits;
     ops.push_back({name, [a, S](hipStream_t s) { gemm(a, S, s); }, 2.0 * M * N * K,
                    4.0 * ((double)N * K + (double)M * K + (double)S * M * N)});
@@ -1301,7 +1352,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     // PTTS_RESBLOCK_STAGES (probe builds): bit mask of the stages that fuse.
     int fused_stages = 4;
     if (probe_env("PTTS_RESBLOCK_STAGES")) fused_stages = atoi(probe_env("PTTS_RESBLOCK_STAGES"));
-    if (big && (fused_stages >> i & 1) && !back_bf16_) {  // (f32 only: its own MFMA loop)
+    if (big && (fused_stages >> i & 1) && back_mfma_ == PTTS_BACK_F32) {  // (f32 only: its own MFMA loop)
       const ResBlockArgs rb{ce_[i], hist_[2 + 2 * i], cb_[i], W(L_.dra_w[i]), W(L_.dra_b[i]), W(L_.drb_w[i]),
                             W(L_.drb_b[i]), ca_[i], B, T, ch};
       const double hd = ch / 2;
@@ -1637,13 +1688,25 @@ void Engine::test_gemm(int layout, int M, int N, int K, int splits, int tail_S, 
   sync();
   const int Nw = (N + 31) / 32 * 32;
   float *dx = nullptr, *dw = nullptr, *dy = nullptr;
+  unsigned* dhm = nullptr;  // bf16x6 layouts (>= 200): the split copy of W (split3)
+  unsigned short* dlo = nullptr;
   PTTS_HIP(hipMalloc(&dx, sizeof(float) * M * K));
   PTTS_HIP(hipMalloc(&dw, sizeof(float) * Nw * K));
   PTTS_HIP(hipMalloc(&dy, sizeof(float) * splits * M * N));
+  if (layout >= 200) {
+    PTTS_HIP(hipMalloc(&dhm, sizeof(unsigned) * Nw * K));
+    PTTS_HIP(hipMalloc(&dlo, sizeof(unsigned short) * Nw * K));
+  }
+  auto release = [&]() {
+    (void)hipFree(dx), (void)hipFree(dw), (void)hipFree(dy);
+    if (dhm) (void)hipFree(dhm);
+    if (dlo) (void)hipFree(dlo);
+  };
   try {
     PTTS_HIP(hipMemsetAsync(dw, 0, sizeof(float) * Nw * K, stream_));
     PTTS_HIP(hipMemcpyAsync(dx, X, sizeof(float) * M * K, hipMemcpyHostToDevice, stream_));
     PTTS_HIP(hipMemcpyAsync(dw, Wt, sizeof(float) * N * K, hipMemcpyHostToDevice, stream_));
+    if (dhm) split3(dw, (long)Nw * K, dhm, dlo, stream_);
     GemmArgs a{};
     a.mode = 0;
     a.layout = layout;
@@ -1654,6 +1717,8 @@ void Engine::test_gemm(int layout, int M, int N, int K, int splits, int tail_S, 
     a.X = dx;
     a.ldx = K;
     a.W = dw;
+    a.Whm = dhm;
+    a.Wlo = dlo;
     a.S = splits;
     if (splits > 1) {
       a.partial = dy;
@@ -1674,10 +1739,10 @@ void Engine::test_gemm(int layout, int M, int N, int K, int splits, int tail_S, 
     PTTS_HIP(hipStreamSynchronize(stream_));
   } catch (...) {
     (void)hipStreamSynchronize(stream_);
-    (void)hipFree(dx), (void)hipFree(dw), (void)hipFree(dy);
+    release();
     throw;
   }
-  (void)hipFree(dx), (void)hipFree(dw), (void)hipFree(dy);
+  release();
 }
 
 double Engine::time_op(int B, const std::string& name, int reps) {

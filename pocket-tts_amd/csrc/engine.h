@@ -204,7 +204,11 @@ class Engine {
   static constexpr int NHB = 6;
   int nhb_ = 3;  // buffers in use: 3, or NHB = 6 with frame pairs
   int nfr_ = 1;  // frames per back-part pass (ptts_engine_config.back_frames)
-  bool back_bf16_ = false;  // ptts_engine_config.back_bf16: the back part's tiles on bf16 MFMA
+  int back_mfma_ = PTTS_BACK_F32;  // ptts_engine_config.back_mfma: the back part's tiles' arithmetic
+  // bf16x6 back part: weight matrix -> its split3 copy (hi | mid, lo), derive_split at finalize
+  std::map<const float*, std::pair<const unsigned*, const unsigned short*>> split_;
+  void derive_split();
+  void attach_split(GemmArgs& a) const;
   int rows_hb_[NHB] = {};  // rows of the front part that filled each hand-off buffer
   // frame-pair mode: PCM of one pair [B][2][1920] per pair parity, and its pinned host copy
   float* pcmp_[NHB / 2] = {};

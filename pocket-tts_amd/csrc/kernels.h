@@ -78,6 +78,11 @@ struct GemmArgs {
   // B operand
   const float* W;
   long w_phase_stride;  // floats between polyphase weight blocks (mode 1)
+  // bf16x6 tiles (layout >= 200, ptts_engine_config.back_mfma = PTTS_BACK_F32X6): W split exactly
+  // into three bf16 pieces, W = hi + mid + lo (split3): Whm[n][k] = hi << 16 | mid (the f32 layout
+  // of W, 4 B per element), Wlo[n][k] = lo (2 B per element); same indexing as W
+  const unsigned* Whm;
+  const unsigned short* Wlo;
   // int8 B operand (weight_quant; mode 0, split-K slabs only): W[n][k] = float(Wq[n][k]) *
   // wscale[n], formed per element before the MFMA. Replaces W when non-null.
   const int8_t* Wq;
@@ -130,6 +135,10 @@ struct GemmArgs {
   float* Y2;
 };
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s);
+// Exact three-piece bf16 split of n f32 values (the B operand of the bf16x6 tiles): x = hi + mid
+// + lo with every piece a bf16 (round to nearest even at each step; the remainders are exact in
+// f32 and the last one is exact in bf16), stored as hm = bits(hi) << 16 | bits(mid) and lo.
+void split3(const float* W, long n, unsigned* hm, unsigned short* lo, hipStream_t s);
 
 // Skinny split-K GEMM (M <= 64 rows: the FlowLM step, small prefills; one 32-row block per
 // grid z) with register-resident weights: the

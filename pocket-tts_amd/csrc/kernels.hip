@@ -600,6 +600,39 @@ __device__ __forceinline__ unsigned lds_addr(const float* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) float*)(p);
 }
 
+// bf16x6 operand pieces (k_gemm_glds PREC 2). split3_frag: 8 f32 values -> their exact three-piece
+// bf16 split by truncation (x0 = the upper 16 bits of x; r = x - x0 is exact (Sterbenz) with at
+// most 16 significant bits; x1 = the upper 16 bits of r; x2 = r - x1 is exact with at most 8
+// significant bits, so its lower 16 bits are zero): 4 VALU ops per value plus one v_perm_b32 per
+// pair and piece. hm_frag: the hi and mid pieces of 8 pre-split W values (hm = hi << 16 | mid).
+__device__ __forceinline__ void split3_frag(const float* x, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+  u32x4 h, m, l;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const unsigned u0 = __float_as_uint(x[2 * p]), u1 = __float_as_uint(x[2 * p + 1]);
+    const float r0 = x[2 * p] - __uint_as_float(u0 & 0xffff0000u), r1 = x[2 * p + 1] - __uint_as_float(u1 & 0xffff0000u);
+    const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+    const float s0 = r0 - __uint_as_float(v0 & 0xffff0000u), s1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+    h[p] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+    m[p] = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+    l[p] = __builtin_amdgcn_perm(__float_as_uint(s1), __float_as_uint(s0), 0x07060302u);
+  }
+  p0 = __builtin_bit_cast(bf16x8, h);
+  p1 = __builtin_bit_cast(bf16x8, m);
+  p2 = __builtin_bit_cast(bf16x8, l);
+}
+__device__ __forceinline__ void hm_frag(const float* w, bf16x8& p0, bf16x8& p1) {
+  u32x4 h, m;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const unsigned e0 = __float_as_uint(w[2 * p]), e1 = __float_as_uint(w[2 * p + 1]);
+    h[p] = __builtin_amdgcn_perm(e1, e0, 0x07060302u);
+    m[p] = __builtin_amdgcn_perm(e1, e0, 0x05040100u);
+  }
+  p0 = __builtin_bit_cast(bf16x8, h);
+  p1 = __builtin_bit_cast(bf16x8, m);
+}
+
 // s_waitcnt with only vmcnt = n (expcnt/lgkmcnt left at "no wait"), gfx9 simm16 encoding
 #define PTTS_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
 
@@ -610,25 +643,41 @@ __device__ __forceinline__ unsigned lds_addr(const float* p) {
 // SIMD = MINB). ILV: the DMAs of chunk c + NBUF - 1 are issued between the MFMAs of chunk c (one
 // per 16 / IPW k-steps) instead of as a burst ahead of its fragment reads: an f32 MFMA leaves 56
 // of its 64 issue cycles free, so the DMA issue (60-185 cycles each) hides behind the matrix pipe.
-// BF16 (engine back_bf16, a variant beside the f32 path): the same tiles, operands still f32 in
-// HBM and LDS, rounded to bf16 (v_cvt_pk_bf16_f32, RNE) as the fragments are read, and multiplied
-// on v_mfma_f32_32x32x16_bf16 with f32 accumulation: lane half h feeds elements j of MFMA q from
-// its chunk columns 16h + 8q + j for A and B alike, so each chunk's 32 k are summed once (2 MFMAs
-// per 32-k chunk instead of 16). The next chunk's DMAs are issued after the two MFMAs.
+// PREC 1, bf16 (engine back_mfma = PTTS_BACK_BF16, a variant beside the f32 path): the same tiles,
+// operands still f32 in HBM and LDS, rounded to bf16 (v_cvt_pk_bf16_f32, RNE) as the fragments are
+// read, and multiplied on v_mfma_f32_32x32x16_bf16 with f32 accumulation: lane half h feeds
+// elements j of MFMA q from its chunk columns 16h + 8q + j for A and B alike, so each chunk's 32 k
+// are summed once (2 MFMAs per 32-k chunk instead of 16). The next chunk's DMAs are issued after
+// the two MFMAs.
+// PREC 2, bf16x6 (PTTS_BACK_F32X6): f32 products on the bf16 matrix pipe. Every f32 operand is the
+// exact sum of three bf16 pieces, x = x0 + x1 + x2 (split3: |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|),
+// and the tile sums the six products whose order is <= 2, a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 +
+// a2 b0: each piece product is exact, the dropped three are below 2^-24 |a b| together, so the
+// result has f32 accuracy (test_gpu_gemm_core: error against fp64 no larger than the f32 MFMA
+// tile's) at 6 bf16 MFMAs (32 cycles each) per 16 k instead of 8 f32 ones (64 cycles each). W
+// comes pre-split from finalize (GemmArgs::Whm = hi | mid in W's f32 layout, Wlo = lo: one more
+// 64-B LDS row per W row and chunk, its 16-B columns swizzled by (row >> 2) & 3 so the ds_read_b128
+// of a 16-lane group hit distinct banks); A is split as its fragments are read (truncation:
+// x0 = x & 0xffff0000, x1 = trunc(x - x0), x2 = x - x0 - x1, all exact).
 template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1, int MINB = 1, bool ILV = false,
-          bool BF16 = false>
+          int PREC = 0>
 __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
   if (a.front) front_prio();
   else back_prio();
+  constexpr bool BF16 = PREC == 1, X6 = PREC == 2;
   constexpr int TM = 32 * WM * TMW, TN = 32 * WN * TNW, ROWS = TM + TN;
   constexpr int CPR = BK / 4;        // 16-byte columns per LDS row
   constexpr int RPI = 64 / CPR;      // rows per 1-KiB wave instruction
-  constexpr int NINS = ROWS / RPI;   // DMA instructions per chunk (whole workgroup)
+  constexpr int NMAIN = ROWS / RPI;  // DMA instructions per chunk for the A and W rows
+  constexpr int NLO = X6 ? TN / 16 : 0;  // ... for the W lo rows (64 B each: 16 per instruction)
+  constexpr int NINS = NMAIN + NLO;  // DMA instructions per chunk (whole workgroup)
   static_assert(NINS % 4 == 0, "every wave issues the same number of DMAs per chunk");
+  static_assert(!X6 || BK == 32, "bf16x6 tiles: BK 32");
   constexpr int IPW = NINS / 4;
   constexpr int DIST = NBUF - 1;     // chunks in flight ahead of the one being multiplied
   static_assert(NBUF >= 2 && NBUF <= 4, "counted waits below cover up to 3 chunks in flight");
-  __shared__ __attribute__((aligned(16))) float lds[NBUF * ROWS * BK];
+  constexpr int BUF = ROWS * BK + (X6 ? TN * 16 : 0);  // floats per LDS buffer (A | W | W lo)
+  __shared__ __attribute__((aligned(16))) float lds[NBUF * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -665,18 +714,26 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
     cb = (int)((long)nchunks * zt / a.tail_S);
     ce = (int)((long)nchunks * (zt + 1) / a.tail_S);
   }
-  const float* Wp = a.W + (long)phase * a.w_phase_stride;
+  const float* Wp = (X6 ? reinterpret_cast<const float*>(a.Whm) : a.W) + (long)phase * a.w_phase_stride;
   const unsigned lds_base = lds_addr(lds);
   // this lane's DMA sources: instruction j = wave + 4*ins covers rows j*RPI .. +RPI-1, all of
   // them A rows or all of them W rows (TM % RPI == 0), so the A/W choice is wave-uniform.
   // Conv A rows keep two base pointers (activation X and history H, both at time index 0 and
   // this lane's column); a chunk picks one per lane with a select, never a branch.
+  // bf16x6: instructions j >= NMAIN move W lo rows (16 per instruction, 4 lanes of 16 B each).
   const float* src_base[IPW];
   const float* src_hist[IPW];
   int src_qs[IPW];
 #pragma unroll
   for (int ins = 0; ins < IPW; ++ins) {
     const int j = wave + 4 * ins;
+    if (X6 && j >= NMAIN) {
+      const int lrow = (j - NMAIN) * 16 + lane / 4;
+      const int lcol = (lane % 4) ^ ((lrow >> 2) & 3);
+      const int n = min(n0 + lrow, a.Nw - 1);
+      src_base[ins] = reinterpret_cast<const float*>(a.Wlo + (long)phase * a.w_phase_stride + (long)n * a.K + 8 * lcol);
+      continue;
+    }
     const int row = (j < NINS ? j : 0) * RPI + lane / CPR;
     const int lcol = (lane % CPR) ^ swz<BK>(row);
     if ((j < NINS ? j : 0) * RPI < TM) {
@@ -700,6 +757,8 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
   auto dma_src = [&](int c, int ins) -> const float* {
     const int j = wave + 4 * ins;
     const int k0 = c * BK;
+    if (X6 && j >= NMAIN)  // W lo row: bf16 elements
+      return reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(src_base[ins]) + k0);
     if (MODE != 0 && j * RPI < TM) {
       const int tap = k0 / a.cin;  // scalar
       const int ci = k0 - tap * a.cin;
@@ -716,7 +775,8 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
     const int j = wave + 4 * ins;
     if (j >= NINS) return;  // wave-uniform
     // wave-uniform LDS base of this instruction; lane l -> + 16*l bytes
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)((buf * ROWS * BK + j * RPI * BK) * 4));
+    const int off = X6 && j >= NMAIN ? buf * BUF + ROWS * BK + (j - NMAIN) * 256 : buf * BUF + j * RPI * BK;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_base + (unsigned)(off * 4));
     if (a.w_nt && j * RPI >= TM) glds16_nt(src, dst);  // wave-uniform: a W row instruction
     else glds16(src, dst);
   };
@@ -769,7 +829,7 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
 #pragma unroll
         for (int ii = 0; ii < TMW; ++ii) {
           const int row = arow + 32 * ii;
-          const float* la = lds + buf * ROWS * BK + row * BK;
+          const float* la = lds + buf * BUF + row * BK;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int lc = 8 * half + 4 * h + i;
@@ -784,7 +844,7 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
 #pragma unroll
         for (int jj = 0; jj < TNW; ++jj) {
           const int row = brow + 32 * jj;
-          const float* lb = lds + buf * ROWS * BK + row * BK;
+          const float* lb = lds + buf * BUF + row * BK;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int lc = 8 * half + 4 * h + i;
@@ -819,6 +879,37 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
           if (ILV && pf) {
 #pragma unroll
             for (int ins = 0; ins < IPW; ++ins) dma(nsrc[ins], pbuf, ins);
+          }
+        } else if (X6) {
+          const float* llo = lds + buf * BUF + ROWS * BK;  // W lo rows, 16 floats (32 bf16) each
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            bf16x8 a0[TMW], a1[TMW], a2[TMW], b0[TNW], b1[TNW], b2[TNW];
+#pragma unroll
+            for (int ii = 0; ii < TMW; ++ii) split3_frag(&af[ii][8 * q], a0[ii], a1[ii], a2[ii]);
+#pragma unroll
+            for (int jj = 0; jj < TNW; ++jj) {
+              hm_frag(&bf[jj][8 * q], b0[jj], b1[jj]);
+              const int lrow = brow - TM + 32 * jj;
+              const int lc = (2 * h + q) ^ ((lrow >> 2) & 3);
+              b2[jj] = *reinterpret_cast<const bf16x8*>(llo + lrow * 16 + 4 * lc);
+            }
+#pragma unroll
+            for (int ii = 0; ii < TMW; ++ii)
+#pragma unroll
+              for (int jj = 0; jj < TNW; ++jj) {
+                floatx16 t = acc[ii][jj];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[ii], b0[jj], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ii], b1[jj], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ii], b2[jj], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ii], b0[jj], t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ii], b1[jj], t, 0, 0, 0);
+                acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ii], b0[jj], t, 0, 0, 0);
+              }
+            if (ILV && pf && q == 0) {  // the next chunk's DMAs between the two halves
+#pragma unroll
+              for (int ins = 0; ins < IPW; ++ins) dma(nsrc[ins], pbuf, ins);
+            }
           }
         } else if (!(PTTS_PROBE(a) & 1)) {
 #pragma unroll
@@ -1529,7 +1620,7 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     // bf16 operands (GemmArgs layout + 100; engine back_bf16): the ILV tiles of the back part
 #define PTTS_GLB(L, WM_, WN_, NB_, TMW_, TNW_, MINB_)                                                 \
   case 100 + L:                                                                                       \
-    launch_tiled((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_, MINB_, true, true>),                \
+    launch_tiled((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_, MINB_, true, 1>),                   \
                  dim3((a.N + 32 * WN_ * TNW_ - 1) / (32 * WN_ * TNW_),                                \
                       (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z), 256, s, a);            \
     return;
@@ -1542,6 +1633,19 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     PTTS_GLB(39, 2, 2, 3, 1, 2, 2)  //  64 x 128, 2 per CU
 #endif
 #undef PTTS_GLB
+    // bf16x6 f32 (GemmArgs layout + 200; engine back_mfma = PTTS_BACK_F32X6): W pre-split (Whm, Wlo)
+#define PTTS_GLX6(L, WM_, WN_, NB_, TMW_, TNW_, MINB_)                                                \
+  case 200 + L:                                                                                       \
+    if (!a.Whm || !a.Wlo) throw std::runtime_error("gemm: bf16x6 layout without its split weights"); \
+    launch_tiled((k_gemm_glds<MODE, WM_, WN_, 32, NB_, TMW_, TNW_, MINB_, true, 2>),                   \
+                 dim3((a.N + 32 * WN_ * TNW_ - 1) / (32 * WN_ * TNW_),                                \
+                      (a.M + 32 * WM_ * TMW_ - 1) / (32 * WM_ * TMW_), grid_z), 256, s, a);            \
+    return;
+    PTTS_GLX6(32, 2, 2, 3, 1, 1, 2)  //  64 x  64, 2 per CU
+    PTTS_GLX6(36, 2, 2, 3, 1, 2, 1)  //  64 x 128
+    PTTS_GLX6(39, 2, 2, 3, 1, 2, 2)  //  64 x 128, 2 per CU
+    PTTS_GLX6(35, 2, 2, 2, 2, 1, 2)  // 128 x  64, 2 per CU
+#undef PTTS_GLX6
     default:
       break;
   }
@@ -1589,6 +1693,24 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     default:
       throw std::runtime_error("gemm: tile layout " + std::to_string(a.layout) + " is not in this build");
   }
+}
+
+// split3 (kernels.h): round-to-nearest-even pieces, each remainder exact in f32
+__global__ __launch_bounds__(256) void k_split3(const float* __restrict__ W, long n, unsigned* __restrict__ hm,
+                                                unsigned short* __restrict__ lo) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float x = W[i];
+    const __bf16 p0 = (__bf16)x;
+    const float r = x - (float)p0;
+    const __bf16 p1 = (__bf16)r;
+    const __bf16 p2 = (__bf16)(r - (float)p1);
+    hm[i] = (unsigned)__builtin_bit_cast(unsigned short, p0) << 16 | __builtin_bit_cast(unsigned short, p1);
+    lo[i] = __builtin_bit_cast(unsigned short, p2);
+  }
+}
+void split3(const float* W, long n, unsigned* hm, unsigned short* lo, hipStream_t s) {
+  const long blocks = std::min<long>((n + 255) / 256, 4096);
+  if (blocks > 0) hipLaunchKernelGGL(k_split3, dim3((unsigned)blocks), dim3(256), 0, s, W, n, hm, lo);
 }
 
 void gemm(const GemmArgs& a, int grid_z, hipStream_t s) {

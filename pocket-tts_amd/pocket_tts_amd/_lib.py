@@ -18,7 +18,8 @@ LDIM = 32
 DIM = 1024
 SAMPLE_RATE = 24000
 QUANT_NONE, QUANT_FLOW_LM, QUANT_ALL = 0, 1, 2
-ABI_VERSION = 5  # PTTS_ABI_VERSION of include/pocket_tts.h that the structs below mirror
+BACK_F32, BACK_BF16, BACK_F32X6 = 0, 1, 2  # ptts_engine_config.back_mfma (PTTS_BACK_*)
+ABI_VERSION = 6  # PTTS_ABI_VERSION of include/pocket_tts.h that the structs below mirror
 
 F32P = C.POINTER(C.c_float)
 U8P = C.POINTER(C.c_uint8)
@@ -40,7 +41,7 @@ class EngineConfig(C.Structure):
         ("fp8_gemm", C.c_int),
         ("cfg_yaml", C.c_char_p),
         ("back_frames", C.c_int),
-        ("back_bf16", C.c_int),
+        ("back_mfma", C.c_int),
     ]
 
 

@@ -7,7 +7,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import (DIM, F32P, FRAME, LDIM, EngineConfig, GenParams, check, fptr, lib, u8ptr)
+from ._lib import (BACK_BF16, BACK_F32, BACK_F32X6, DIM, F32P, FRAME, LDIM, EngineConfig, GenParams, check, fptr, lib,
+                   u8ptr)
 
 
 @dataclass
@@ -68,7 +69,8 @@ class Engine:
     def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
                  seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
                  defer_weights: bool = False, pipeline: bool = False, weight_quant: int = 0, fp8_gemm: bool = False,
-                 cfg_yaml: str | None = None, back_frames: int = 1, back_bf16: bool = False):
+                 cfg_yaml: str | None = None, back_frames: int = 1, back_bf16: bool = False,
+                 back_mfma: int | None = None):
         """pipeline=True: overlapped stepping, each step() returns the frame produced by the
         previous call (see ptts_engine_config.pipeline). weight_quant: QUANT_NONE / QUANT_FLOW_LM /
         QUANT_ALL, the reference's simulated int8 weight quantization (quantize.rs), with the
@@ -76,13 +78,17 @@ class Engine:
         fp8 W8A8 MFMA (accuracy-gated; see ptts_engine_config.fp8_gemm). cfg_yaml: the reference's
         model config (config/b6369a24.yaml), checked against the compiled dimensions.
         back_frames=2 (pipelined only): two frames per Mimi-decode pass; a step() returns the frame
-        computed three calls earlier (`frame_lag`). back_bf16=True: the Mimi decode's GEMMs and convs
-        on bf16 MFMA (f32 accumulation; a variant gated on PCM accuracy, ptts_engine_config.back_bf16)."""
+        computed three calls earlier (`frame_lag`). back_mfma (ptts_engine_config.back_mfma): how the
+        Mimi decode's GEMMs and convs use the matrix cores, BACK_F32 (exact f32 FMA chain), BACK_F32X6
+        (f32 products as six bf16 piece products, f32 accuracy) or BACK_BF16 (operands rounded to
+        bf16: a variant gated on PCM accuracy); back_bf16=True is BACK_BF16."""
+        if back_mfma is None:
+            back_mfma = BACK_BF16 if back_bf16 else BACK_F32
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
                            weight_blob or None, int(defer_weights), int(pipeline), int(weight_quant),
                            int(fp8_gemm), cfg_yaml.encode() if cfg_yaml else None, int(back_frames),
-                           int(back_bf16))
+                           int(back_mfma))
         h = C.c_void_p()
         check(lib().ptts_engine_create(C.byref(cfg), C.byref(h)))
         self.handle = h
@@ -92,7 +98,8 @@ class Engine:
         self.lsd_decode_steps = lsd_decode_steps
         self.pipeline = bool(pipeline)
         self.back_frames = int(back_frames) if pipeline else 1
-        self.back_bf16 = bool(back_bf16)
+        self.back_mfma = int(back_mfma)
+        self.back_bf16 = self.back_mfma == BACK_BF16
 
     def test_gemm(self, layout: int, x: np.ndarray, w: np.ndarray, splits: int = 1, tail_slices: int = 0) -> np.ndarray:
         """GEMM-core test hook (ptts_test_gemm): x [m][k] @ w [n][k]^T on tile `layout`; splits > 1

@@ -97,7 +97,7 @@ def test_library_is_built_from_these_sources():
     import pocket_tts_amd as pt
     from pocket_tts_amd import _lib
 
-    assert _lib.lib().ptts_abi_version() == _lib.ABI_VERSION == 5
+    assert _lib.lib().ptts_abi_version() == _lib.ABI_VERSION == 6
     assert len(pt.source_build_id()) == 16
     assert pt.build_id() == pt.source_build_id()
     assert pt.check_build_id() == pt.build_id()

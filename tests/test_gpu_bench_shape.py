@@ -1,6 +1,8 @@
 """GPU parity at the benchmark's own shape (BASELINE configs[2]): f32 engine, 32 rows, 125-frame
 voice prompts, 40 text tokens, 132 free-running frames at temperature 0, pipelined stepping with
-frame pairs (the bench's mode: one Mimi decode pass per two frames) and with one frame per pass. The FlowLM context of every row grows 165 -> 297 positions, so the step attention
+frame pairs (the bench's mode: one Mimi decode pass per two frames) and with one frame per pass, and
+with frame pairs on the bf16x6 back part (back_mfma = BACK_F32X6: f32 GEMMs as exact bf16 piece
+products) at the same gates. The FlowLM context of every row grows 165 -> 297 positions, so the step attention
 (k_attn_decode_qkv) takes its second 256-key round for the last 40 frames, and the Mimi decoder's
 250-key window slides over 2,112 ring positions (four wraps of the 512-slot ring).
 
@@ -54,9 +56,9 @@ def _oracle_run(oracle, prompt, ids, n):
     return out
 
 
-def _engine_frames(pt, inputs, back_frames):
+def _engine_frames(pt, inputs, back_frames, back_mfma=0):
     eng = pt.Engine(device=0, max_slots=B, max_ctx=320, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
-                    back_frames=back_frames)
+                    back_frames=back_frames, back_mfma=back_mfma)
     try:
         voices = [eng.voice_from_prompt(p) for p, _ in inputs]
         params = pt.GenerationParams(temp=0.0, eos_threshold=float("inf"), frames_after_eos=3,
@@ -86,7 +88,8 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
     workers = max(1, min(16, len(os.sched_getaffinity(0))))
     with ThreadPoolExecutor(workers) as ex:  # the oracle runs free (temp 0): precompute them
         futs = {b: ex.submit(_oracle_run, oracle, *inputs[b], FRAMES) for b in range(B)}
-        runs = {bf: _engine_frames(pt, inputs, bf) for bf in (2, 1)}
+        runs = {(bf, mf): _engine_frames(pt, inputs, bf, mf)
+                for bf, mf in ((2, pt.BACK_F32), (1, pt.BACK_F32), (2, pt.BACK_F32X6))}
         ref = {b: f.result() for b, f in futs.items()}
 
     worst = {"golden": [0.0, 0.0, 0.0], "oracle": [0.0, 0.0, 0.0]}
@@ -102,7 +105,8 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
                 cmp("oracle", frames[i][b], ref[b][i], (bf, i, b))
             if i < d["latent"].shape[0]:
                 cmp("golden", frames[i][0], (d["eos_logit"][i], d["latent"][i], d["pcm"][i]), (bf, i, 0))
-        print(f"back_frames={bf}: worst |d| eos/latent/pcm: vs golden {worst['golden']}, vs oracle {worst['oracle']}")
+        print(f"back_frames, back_mfma={bf}: worst |d| eos/latent/pcm: vs golden {worst['golden']}, "
+              f"vs oracle {worst['oracle']}")
 
 
 def _oracle_run_noisy(oracle, prompt, ids, n, seed, temp):

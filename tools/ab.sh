@@ -5,7 +5,8 @@
 #   ARMS="label:K=V,K=V label2:- ..." [REPS=3] [BENCH_ARGS="..."] [METRIC=steady_ms_per_step] \
 #       [PRE="command run once before the arms, e.g. a pytest subset"] bash tools/ab.sh [summary.txt]
 #
-# An arm is a label and a comma-separated list of environment settings ("-" = none). The usual ones:
+# An arm is a label and a comma-separated list of environment settings ("-" = none); the pseudo
+# setting BENCH=a+b+c appends the bench.py arguments "a b c" for that arm only. The usual ones:
 #   PTTS_LIB=abl/libbase.so                                  a base library (tools/build_base.sh REV)
 #   PTTS_LIB=pocket-tts_amd/lib-probes/libpocket_tts_hip.so  the measurement build (make -C pocket-tts_amd probes)
 #   PTTS_BACK_PRIO / PTTS_FRONT_PRIO / PTTS_BACK_WG_CAP / PTTS_OVR=op=layout:splits ...  probe knobs
@@ -28,10 +29,16 @@ for r in $(seq 1 "$REPS"); do
     label=${arm%%:*}
     envs=${arm#*:}
     settings=()
-    if [ "$envs" != "-" ]; then IFS=',' read -ra settings <<< "$envs"; fi
+    extra=""
+    if [ "$envs" != "-" ]; then IFS=',' read -ra all <<< "$envs"; fi
+    for kv in "${all[@]:-}"; do
+      [ -z "$kv" ] && continue
+      if [ "${kv%%=*}" = "BENCH" ]; then extra="${kv#BENCH=}"; extra="${extra//+/ }"; else settings+=("$kv"); fi
+    done
+    all=()
     log=gpurun_out/ab_${label}_$r.log
     env "${settings[@]}" timeout -k 10 240 python bench.py --no-cpu-baseline --no-quant-variant --no-op-times \
-        --no-latency --no-distinct-voices --no-voice-bench --no-text-bench ${BENCH_ARGS:-} > "$log" 2>&1 \
+        --no-latency --no-distinct-voices --no-voice-bench --no-text-bench ${BENCH_ARGS:-} $extra > "$log" 2>&1 \
       || { echo "arm $label failed (round $r)"; tail -5 "$log"; exit 1; }
     python - "$label" "$r" "$log" "$METRIC" "$RAW" <<'PY'
 import json, sys
