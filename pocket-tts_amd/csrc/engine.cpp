@@ -61,7 +61,7 @@ static void tile_override(const std::string& name, int& layout, int& ksplit) {
 // layouts served by k_gemm_glds (kernels.hip gemm_launch): the only ones that split a conv's K
 static bool lds_dma_layout(int layout) {
   return (layout >= 6 && layout <= 8) || (layout >= 11 && layout <= 16) || (layout >= 21 && layout <= 27) ||
-         (layout >= 30 && layout <= 42) || (layout >= 130 && layout <= 139);
+         (layout >= 30 && layout <= 42) || (layout >= 130 && layout <= 139) || (layout >= 230 && layout <= 239);
 }
 
 float* Engine::dalloc(size_t n) {
