@@ -28,8 +28,8 @@ __device__ __forceinline__ void front_prio() {
   else if (p == 2) __builtin_amdgcn_s_setprio(2);
   else if (p == 1) __builtin_amdgcn_s_setprio(1);
 }
-// the back part's GEMM / conv tile waves: product builds issue at priority 0 (back_prio below);
-// probe builds take the level from PTTS_BACK_PRIO (set_back_prio, default 0)
+// the back part's GEMM / conv tile waves: product builds issue at priority 3 (back_prio below);
+// probe builds take the level from PTTS_BACK_PRIO (set_back_prio, default 3, 0 = off)
 extern __device__ int g_back_prio;
 __device__ __forceinline__ void back_prio() {
   const int p = __builtin_amdgcn_readfirstlane(g_back_prio);
@@ -43,13 +43,12 @@ extern __device__ int g_front_skip;
 __device__ __forceinline__ int front_skip() { return __builtin_amdgcn_readfirstlane(g_front_skip); }
 #else
 __device__ __forceinline__ void front_prio() {}
-// Issue priority of the back part's GEMM / conv tile waves (k_gemm_glds launches outside the front
-// part, k_gemm_rb, k_resblock): the default level 0, like the front part's waves. Round 4 raised it
-// to 3 while the back stream bounded the frame-pair step (0.5569 -> 0.5513 ms,
-// profiles/r04/interference_probes.txt); once the front part bounded it again, level 3 cost the
-// step 3.4 % against 0 (probe-build arms, same box: 0.5775 vs 0.5578 ms, profiles/r05/prio_ab.txt)
-// and was dropped (product A/B in profiles/r05/prio_product_ab.txt).
-__device__ __forceinline__ void back_prio() {}
+// Issue priority 3 for the back part's GEMM / conv tile waves (k_gemm_glds launches outside the
+// front part, k_gemm_rb, k_resblock): where a back wave and a front wave are both ready on a SIMD,
+// the back wave issues first. In the frame-pair step the back stream runs end to end (graph stamps,
+// tools/stamps.py); steady step 0.5569 -> 0.5513 and 0.5674 -> 0.5631 ms on two boxes
+// (profiles/r04/interference_probes.txt, interleaved repeats).
+__device__ __forceinline__ void back_prio() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ constexpr int front_skip() { return 0; }
 #endif
 

@@ -36,7 +36,7 @@ void set_front_prio(int prio) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_front_prio), &prio, sizeof prio) != hipSuccess)
     throw std::runtime_error("set_front_prio failed");
 }
-__device__ int g_back_prio = 0;  // the product level (devfn.h back_prio)
+__device__ int g_back_prio = 3;  // the product level (devfn.h back_prio)
 __device__ int g_front_skip = 0;
 void set_front_skip(int v) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_front_skip), &v, sizeof v) != hipSuccess)
