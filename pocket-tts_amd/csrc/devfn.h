@@ -47,7 +47,11 @@ __device__ __forceinline__ void front_prio() {}
 // front part, k_gemm_rb, k_resblock): where a back wave and a front wave are both ready on a SIMD,
 // the back wave issues first. In the frame-pair step the back stream runs end to end (graph stamps,
 // tools/stamps.py); steady step 0.5569 -> 0.5513 and 0.5674 -> 0.5631 ms on two boxes
-// (profiles/r04/interference_probes.txt, interleaved repeats).
+// (profiles/r04/interference_probes.txt, interleaved repeats). Re-measured in round 5 with the
+// front part bounding the step: level 0 in a product build 0.5533 against 0.5496 ms for 3
+// (profiles/r05/prio_product_ab.txt; the probe build's knob read 0.5578 vs 0.5775 there,
+// profiles/r05/prio_probe_ab.txt, but a probe build's per-launch priority load slows every launch
+// and does not transfer): 3 stays.
 __device__ __forceinline__ void back_prio() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ constexpr int front_skip() { return 0; }
 #endif
