@@ -1645,6 +1645,8 @@ static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
     PTTS_GLX6(36, 2, 2, 3, 1, 2, 1)  //  64 x 128
     PTTS_GLX6(39, 2, 2, 3, 1, 2, 2)  //  64 x 128, 2 per CU
     PTTS_GLX6(35, 2, 2, 2, 2, 1, 2)  // 128 x  64, 2 per CU
+    PTTS_GLX6(31, 2, 2, 2, 2, 2, 2)  // 128 x 128, 2 per CU
+    PTTS_GLX6(30, 2, 2, 3, 2, 2, 1)  // 128 x 128
 #undef PTTS_GLX6
     default:
       break;
