@@ -399,16 +399,6 @@ void Engine::derive_gemv() {
       PTTS_HIP(hipMemsetD32Async(ffn_hand_, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, stream_));
     }
   }
-  // layers >= 1 of a step pass: the ff2 reduce + norm1 + QKV launch (ln_gemv) wherever the QKV
-  // matrix is register-resident; PTTS_NO_LNQKV (probe builds) keeps the two launches
-  if ((mask & 1) && !probe_env("PTTS_NO_LNQKV")) {
-    void* hnd = nullptr;
-    PTTS_HIP(hipMalloc(&hnd, sizeof(float) * (2 * LN_HAND_FLOATS + (size_t)8 * 32 * 3 * D)));
-    allocs_.push_back(hnd);
-    ln_hand_ = (float*)hnd;  // two sets, empty (0xFFFFFFFF) before the first launch
-    qkv_part_ = ln_hand_ + 2 * LN_HAND_FLOATS;
-    PTTS_HIP(hipMemsetD32Async(ln_hand_, 0xFFFFFFFFu, 2 * LN_HAND_FLOATS, stream_));
-  }
   size_t total = 0;
   for (const M& m : mats)
     if ((mask & m.bit) && gemv_supported(m.g, m.N, m.K)) total += (size_t)m.N * m.K;
@@ -802,15 +792,6 @@ void Engine::conv_op(std::vector<Op>& ops, const std::string& name, const float*
 // FlowLM transformer layers over M rows (x_ holds the residual stream, h_ = norm1_0(x_)).
 // StreamingTransformerLayer::forward (transformer.rs:66-90).
 void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag) {
-  // step passes: layer l >= 1 takes the previous layer's ff2 reduce + its own norm1 + its QKV
-  // projection as ONE launch (ln_gemv: the QKV weight stream under the reduce); hand-off set of
-  // layer l = (l + 1) % 2, the QKV slabs into qkv_part_
-  auto fused_qkv = [&](int l) {
-    if (qg != 1 || l < 1 || !ln_hand_ || !ln_gemv_supported(M, 3 * D, D)) return false;
-    auto it = gvmap_.find(W(L_.fl[l].in_proj));
-    return it != gvmap_.end() && it->second.g.wn == 4 && it->second.g.kw == 128;
-  };
-  int S_ff2 = 1;  // slabs of the previous layer's linear2 (a fused launch sums them)
   for (int l = 0; l < NL; ++l) {
     const Layout::TL& t = L_.fl[l];
     const std::string p = tag + ".l" + std::to_string(l);
@@ -821,34 +802,9 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       kv.layer = l;
     }
     int S = 1;
-    const float* qkv_slabs = partial_;
-    if (fused_qkv(l)) {
-      LnGemvArgs g{};
-      g.P = partial_;
-      g.S = S_ff2;
-      g.M = M;
-      g.x = x_;
-      g.lnw = W(t.n1w);
-      g.lnb = W(t.n1b);
-      g.eps = 1e-5f;
-      g.packed = gvmap_.at(W(t.in_proj)).packed;
-      g.hand = ln_hand_ + (size_t)((l + 1) % 2) * LN_HAND_FLOATS;
-      g.hand_next = ln_hand_ + (size_t)(l % 2) * LN_HAND_FLOATS;
-      g.partial = qkv_part_;
-      g.err = herr_;
-      const double mn = (double)M * D;
-      Op op{p + ".ln_qkv", [g](hipStream_t s) { ln_gemv(g, s); }, 2.0 * M * 3 * D * D + mn * (S_ff2 + 10),
-            4.0 * (3.0 * D * D + mn * (S_ff2 + 2) + 2.0 * D + 8.0 * M * 3 * D + 2 * mn)};
-      float* hand = g.hand;
-      op.prep = [hand](hipStream_t s) { PTTS_HIP(hipMemsetD32Async(hand, 0xFFFFFFFFu, LN_HAND_FLOATS, s)); };
-      ops.push_back(op);
-      S = 8;
-      qkv_slabs = qkv_part_;
-    } else {
-      linear_split(ops, p + ".qkv_gemm", h_, D, M, W(t.in_proj), 3 * D, D, &S);
-    }
+    linear_split(ops, p + ".qkv_gemm", h_, D, M, W(t.in_proj), 3 * D, D, &S);
     if (qg == 1) {  // step: slab sum + RoPE + KV append fused into the attention kernel
-      const float* P = qkv_slabs;
+      const float* P = partial_;
       float* O = o_;
       const float* rope = rope_;
       // K and V of every head over the cached positions the launch reads (8,192 B per position):
@@ -929,31 +885,10 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       }
       linear_split(ops, p + ".ff2_gemm", u_, FF, M, W(t.l2), D, FF, &S);
     }
-    if (l + 1 < NL) {
-      if (fused_qkv(l + 1)) S_ff2 = S;  // the next layer's ln_qkv launch reduces these slabs
-      else rr(p + ".ff2_reduce_ln1", S, D, ACT_NONE, true, x_, W(L_.fl[l + 1].n1w), W(L_.fl[l + 1].n1b), true, h_);
-    } else {
-      RowReduceArgs a{};
-      a.P = partial_;
-      a.S = S;
-      a.M = M;
-      a.N = D;
-      a.R = x_;
-      a.ldr = D;
-      a.Y = x_;
-      a.ldy = D;
-      a.ln = out_norm ? 1 : 0;
-      a.ln_w = W(L_.out_norm_w);
-      a.ln_b = W(L_.out_norm_b);
-      a.eps = 1e-5f;
-      a.Hout = h_;
-      a.ldh = D;
-      if (fused_qkv(1)) {  // side job: empty layer 1's hand-off set (the last ln_qkv launch read it)
-        a.fill = ln_hand_ + (size_t)(2 % 2) * LN_HAND_FLOATS;
-        a.fill_n4 = LN_HAND_FLOATS / 4;
-      }
-      push_rr(ops, p + ".ff2_reduce_outnorm", a);
-    }
+    if (l + 1 < NL)
+      rr(p + ".ff2_reduce_ln1", S, D, ACT_NONE, true, x_, W(L_.fl[l + 1].n1w), W(L_.fl[l + 1].n1b), true, h_);
+    else
+      rr(p + ".ff2_reduce_outnorm", S, D, ACT_NONE, true, x_, W(L_.out_norm_w), W(L_.out_norm_b), out_norm, h_);
   }
 }
 

@@ -134,8 +134,6 @@ class Engine {
   std::map<const float*, const float*> ffnmap_;
   float* ffn_hand_ = nullptr;
   int ffn_groups_ = 8;  // linear2 K slices (slabs) of the fused feed-forward
-  // ff2 reduce + norm1 + QKV of step passes (ln_gemv): two hand-off sets, its QKV slab buffer
-  float *ln_hand_ = nullptr, *qkv_part_ = nullptr;
   int gemv_mask_ = 0;  // matrices that take the register-resident GEMM
   void derive_gemv();
   bool own_blob_ = true, ready_ = false;

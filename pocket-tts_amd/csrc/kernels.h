@@ -185,30 +185,6 @@ void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStre
 void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
                  hipStream_t s);
 
-// The row reduce that ends a FlowLM layer of a step pass (the S linear2 slabs + residual -> x, the
-// next layer's norm1 -> h) and that layer's QKV projection (gemv_splitk {4, 128}: 24 tiles x 8 K
-// slices) as ONE launch: M producer workgroups (one row each, the arithmetic of row_reduce) and
-// 192 consumer workgroups that request their whole weight fragment first, then take h's K slice
-// from a hand-off region where the data is its own flag (hand: LN_HAND_FLOATS floats, all
-// 0xFFFFFFFF at launch, [8 slices][32 rows][128]; sc1 stores / loads, bounded sweep -> *err), so
-// the 12.6-MB weight stream runs under the reduce instead of after it. The consumers with tile 0
-// empty their slice of `hand_next` (the set of the next such launch). Output: the qkv slabs
-// P [8][M][3072] (= gemv_splitk's). M <= 32, K = 1024, N = 3072.
-constexpr long LN_HAND_FLOATS = 32L * 1024;
-struct LnGemvArgs {
-  const float* P;  // linear2 slabs [S][M][1024]
-  int S, M;
-  float* x;        // residual stream [M][1024], in / out
-  const float *lnw, *lnb;
-  float eps;
-  const float* packed;  // pack_gemv {4, 128} copy of the qkv weight [3072][1024]
-  float *hand, *hand_next;
-  float* partial;  // [8][M][3072]
-  int* err;
-};
-bool ln_gemv_supported(int M, int N, int K);
-void ln_gemv(const LnGemvArgs& a, hipStream_t s);
-
 // int8 codes of a quantized weight matrix: q[n][k] = W[n][k] / s[n] (exact integers in
 // [-127, 127] for a blob packed by the quantizer); rows with s[n] == 0 get code 0. Any element
 // with float(q) * s[n] != W[n][k] (bitwise) increments *bad.

@@ -2323,125 +2323,6 @@ void row_reduce(const RowReduceArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL(k_row_reduce<16>, grid, dim3(256), cap_lds(k_row_reduce<16>, g_wg_cap), s, a);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Row reduce + norm1 + QKV projection in one launch (kernels.h ln_gemv). Workgroups 0 .. M-1 are
-// the producers (row m: the k_row_reduce<8> arithmetic, then h's 1024 values into the hand-off
-// region, slice z = n / 128 at [(z * 32 + m) * 128 + n % 128]); workgroups M .. M + 191 are
-// k_gemv<4, 128> tiles (t, z) whose X slice comes from the region instead of h. The producers are
-// dispatched first (lower ids), so they are resident before any consumer spins; a consumer's
-// sweep is bounded (a lost hand-off sets *err, the next fetch reports it).
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ln_gemv(LnGemvArgs a) {
-  front_prio();
-  constexpr int KS = 128, NV = 16, LDA = KS + 4, NT = 24;
-  __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
-  __shared__ float sh[4];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int L = blockIdx.x;
-  if (L < a.M) {  // ---- producer: row m
-    RowReduceArgs r{};
-    r.P = a.P;
-    r.S = a.S;
-    r.M = a.M;
-    r.N = 1024;
-    r.R = a.x;
-    r.ldr = 1024;
-    r.Y = a.x;
-    r.ldy = 1024;
-    r.ln = 1;
-    r.ln_w = a.lnw;
-    r.ln_b = a.lnb;
-    r.eps = a.eps;
-    const int m = L, n = 4 * tid;
-    const float4 v = rr_value<8>(r, m, n);
-    rr_store(r, m, n, v);
-    const float sm = (v.x + v.y) + (v.z + v.w);
-    const float mean = block_sum(sm, sh) / 1024.f;
-    const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
-    const float q = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
-    const float den = sqrtf(block_sum(q, sh) / 1024.f + r.eps);
-    const float4 hv = rr_ln(r, m, n, d, den);
-    fh_put(sc1_rsrc(a.hand), ((n >> 7) * 32 * 128 + m * 128 + (n & 127)) * 4, hv);
-    return;
-  }
-  // ---- consumer: QKV tile t (128 columns), K slice z
-  const int c = L - a.M, t = c % NT, z = c / NT;
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v* wp = reinterpret_cast<const f4v*>(a.packed) + (((long)t * 8 + z) * 4 + wave) * NV * 64 + lane;
-  f4v w[NV];
-#pragma unroll
-  for (int j = 0; j < NV; ++j)
-    w[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);  // once-read
-  if (t == 0) {  // empty slice z of the next launch's set (every row: the next launch may have more)
-    const auto er = sc1_rsrc(a.hand_next);
-    const float4 e = make_float4(__uint_as_float(~0u), __uint_as_float(~0u), __uint_as_float(~0u), __uint_as_float(~0u));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fh_st(er, (z * 32 * 128 + 4 * (tid + 256 * i)) * 4, e);
-  }
-  // h's slice z: rows 0 .. 31 x 128 (4 float4 per thread), swept until no word is empty
-  const auto hr = sc1_rsrc(a.hand);
-  float4 av[4];
-  bool need[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = tid + 256 * i, row = e >> 5;
-    need[i] = row < a.M;
-    av[i] = need[i] ? fh_ld(hr, (z * 32 * 128 + 4 * e) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  {
-    unsigned spins = 0;
-    while (true) {
-      bool ok = true;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ok &= !(need[i] && fh_empty(av[i]));
-      if (__syncthreads_and(ok)) break;
-      __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (need[i] && fh_empty(av[i])) av[i] = fh_ld(hr, (z * 32 * 128 + 4 * (tid + 256 * i)) * 4);
-      if (++spins > (1u << 20)) {
-        if (tid == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = tid + 256 * i, row = e >> 5, c4 = e & 31;
-    *reinterpret_cast<float4*>(&sA[row * LDA + 4 * c4]) = av[i];
-  }
-  __syncthreads();
-  const int m = lane & 31, h = lane >> 5;
-  const float* ar = &sA[m * LDA + h * (KS / 2)];
-  floatx16 acc;
-#pragma unroll
-  for (int g = 0; g < 16; ++g) acc[g] = 0.f;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    if (front_skip() & 2) break;
-    const float4 av4 = *reinterpret_cast<const float4*>(ar + 4 * j);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av4.x, w[j].x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av4.y, w[j].y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av4.z, w[j].z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av4.w, w[j].w, acc, 0, 0, 0);
-  }
-  const int n = t * 128 + wave * 32 + m;
-  float* out = a.partial + (long)z * a.M * 3072;
-#pragma unroll
-  for (int g = 0; g < 16; ++g) {
-    const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
-    if (row < a.M) out[(long)row * 3072 + n] = acc[g];
-  }
-}
-
-bool ln_gemv_supported(int M, int N, int K) { return M >= 1 && M <= 32 && N == 3072 && K == 1024; }
-
-void ln_gemv(const LnGemvArgs& a, hipStream_t s) {
-  if (!ln_gemv_supported(a.M, 3072, 1024) || a.S < 1 || a.S > 8) throw std::runtime_error("ln_gemv: bad shape");
-  hipLaunchKernelGGL(k_ln_gemv, dim3((unsigned)(a.M + 24 * 8)), dim3(256), cap_lds(k_ln_gemv, g_wg_cap), s, a);
-}
-
 // LayerNorm, one wave per row (N <= 1024, multiple of 64).
 __global__ __launch_bounds__(256) void k_layernorm(const float* x, long ldx, float* y, long ldy, int M, int N,
                                                    const float* w, const float* b, float eps) {
