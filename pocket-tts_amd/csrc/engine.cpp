@@ -1950,6 +1950,54 @@ void Engine::overlap_probe(int B, int reps, double* us) {
     us[4 + v] = 1000.0 * ms / reps;
     (void)hipStreamDestroy(sm);
   }
+  // PTTS_PROBE_SPLITS="F:K,...": spatial partition. The front part launched op by op on a stream
+  // whose CU mask keeps the CUs with cu % 8 < F, the back part op by op on the CUs with
+  // cu % 8 >= 8 - K (disjoint when F + K <= 8); F or K = 0 leaves that part out (alone timings).
+  // One line per split on stderr: microseconds per step (front + back per call).
+  if (probe_env("PTTS_PROBE_SPLITS")) {
+    auto make_masked = [&](int lo, int hi) {  // CUs with lo <= cu % 8 < hi
+      std::vector<uint32_t> m(8, 0u);
+      for (int cu = 0; cu < 256; ++cu)
+        if ((cu % 8) >= lo && (cu % 8) < hi) m[cu / 32] |= 1u << (cu % 32);
+      hipStream_t st = nullptr;
+      PTTS_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()));
+      return st;
+    };
+    const std::string spec = probe_env("PTTS_PROBE_SPLITS");
+    size_t p = 0;
+    while (p < spec.size()) {
+      size_t q = spec.find(',', p);
+      if (q == std::string::npos) q = spec.size();
+      const std::string item = spec.substr(p, q - p);
+      p = q + 1;
+      const int F = atoi(item.c_str()), K = atoi(item.substr(item.find(':') + 1).c_str());
+      hipStream_t sf = F > 0 ? make_masked(0, F) : nullptr, sb = K > 0 ? make_masked(8 - K, 8) : nullptr;
+      auto one = [&]() {
+        if (sf)
+          for (size_t i = 0; i < cut; ++i) ops[i].fn(sf);
+        if (sb) {
+          set_wg_cap(back_cap_);
+          for (size_t i = cut; i < ops.size(); ++i) ops[i].fn(sb);
+          set_wg_cap(0);
+        }
+      };
+      for (int w = 0; w < 2; ++w) one();
+      PTTS_HIP(hipDeviceSynchronize());
+      hipStream_t s0 = sf ? sf : sb, s1 = sb ? sb : sf;
+      PTTS_HIP(hipEventRecord(e0, s0));
+      PTTS_HIP(hipStreamWaitEvent(s1, e0, 0));
+      for (int r = 0; r < reps; ++r) one();
+      PTTS_HIP(hipEventRecord(e2, s1));
+      PTTS_HIP(hipStreamWaitEvent(s0, e2, 0));
+      PTTS_HIP(hipEventRecord(e1, s0));
+      PTTS_HIP(hipEventSynchronize(e1));
+      float ms = 0.f;
+      PTTS_HIP(hipEventElapsedTime(&ms, e0, e1));
+      fprintf(stderr, "split front %d/8 back %d/8: %.1f us per step\n", F, K, 1000.0 * ms / reps);
+      if (sf) (void)hipStreamDestroy(sf);
+      if (sb) (void)hipStreamDestroy(sb);
+    }
+  }
   for (int part = 0; part < 2; ++part) {
     (void)hipGraphExecDestroy(ge[part]);
     (void)hipGraphDestroy(g[part]);
