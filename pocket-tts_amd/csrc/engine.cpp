@@ -343,6 +343,27 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
 // this way (qkv 8.1 -> 4.9 us, out 4.5 -> 3.2, linear1 8.1 -> 5.2, linear2 7.9 -> 5.3); in the
 // pipelined step only out + linear2 + adaLN pay (steady step 0.6595 -> 0.6326 ms, medians of 3):
 // the qkv / linear1 versions on any tile slow the concurrent back part more than they gain.
+// The int8 codes of quantized weight W [N][K] (derive_int8) in pack_q8 order: the codes widened
+// to f32 (temporary), fragment-packed by `pack` exactly as the f32 weight would be, then one byte
+// per element with a lane's four fragment groups per 16-B load (nj: groups per lane and wave).
+const uint32_t* Engine::pack_codes(const float* W, int N, int K, int nj,
+                                   const std::function<void(const float*, float*)>& pack) {
+  auto it = q8map_.find(W);
+  if (it == q8map_.end()) return nullptr;
+  const size_t n = (size_t)N * K;
+  float* tmp = nullptr;
+  PTTS_HIP(hipMalloc(&tmp, sizeof(float) * 2 * n));
+  void* q = nullptr;
+  PTTS_HIP(hipMalloc(&q, n));
+  allocs_.push_back(q);
+  codes_to_f32(it->second.first, (long)n, tmp, stream_);
+  pack(tmp, tmp + n);
+  pack_q8(tmp + n, (long)(n / 4), nj, (uint32_t*)q, stream_);
+  PTTS_HIP(hipStreamSynchronize(stream_));
+  PTTS_HIP(hipFree(tmp));
+  return (const uint32_t*)q;
+}
+
 void Engine::derive_gemv() {
   // sequential stepping (the B = 1 first-chunk path, no concurrent back part) and frame-pair
   // pipelined stepping (the front part bounds the step): every matrix. Single-frame pipelined
@@ -394,6 +415,13 @@ void Engine::derive_gemv() {
         pack_ffn2(W(L_.fl[l].l2), ffn_groups_, fd, stream_);
         ffnmap_[W(L_.fl[l].l2)] = fd;
         fd += (size_t)D * FF;
+        // weight_quant engines: both matrices also as int8 codes (the fused launch then streams
+        // a quarter of the bytes; the same f32 values reach the MFMAs)
+        const float *w1 = W(L_.fl[l].l1), *w2 = W(L_.fl[l].l2);
+        const int G = ffn_groups_;
+        const uint32_t* q1 = pack_codes(w1, FF, D, 8, [&](const float* c, float* o) { pack_gemv_fk(c, FF, D, o, stream_); });
+        const uint32_t* q2 = pack_codes(w2, D, FF, 8, [&](const float* c, float* o) { pack_ffn2(c, G, o, stream_); });
+        if (q1 && q2) ffn8map_[w2] = {{q1, q8map_.at(w1).second}, {q2, q8map_.at(w2).second}};
       }
       ffn_hand_ = fd;  // both sets empty (0xFFFFFFFF) before the first launch
       PTTS_HIP(hipMemsetD32Async(ffn_hand_, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, stream_));
@@ -410,7 +438,13 @@ void Engine::derive_gemv() {
   for (const M& m : mats) {
     if (!(mask & m.bit) || !gemv_supported(m.g, m.N, m.K)) continue;
     pack_gemv(m.w, m.N, m.K, m.g, dst, stream_);
-    gvmap_[m.w] = Gemv{dst, m.g, m.bit};
+    Gemv gv{dst, m.g, m.bit, nullptr, nullptr};
+    // weight_quant engines: the int8 codes of a quantized matrix in the same fragment order
+    const GemvShape g = m.g;
+    const int N = m.N, K = m.K;
+    gv.q8 = pack_codes(m.w, N, K, g.kw / 8, [&](const float* c, float* o) { pack_gemv(c, N, K, g, o, stream_); });
+    if (gv.q8) gv.scale = q8map_.at(m.w).second;
+    gvmap_[m.w] = gv;
     dst += (size_t)m.N * m.K;
   }
   PTTS_HIP(hipGetLastError());
@@ -466,7 +500,7 @@ void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   if (fp8_ && f8map_.empty()) derive_fp8();
-  if (wq_ == QUANT_NONE && !fp8_ && gvmap_.empty()) derive_gemv();
+  if (!fp8_ && gvmap_.empty()) derive_gemv();
   if (back_mfma_ == PTTS_BACK_F32X6 && split_.empty()) derive_split();
   if (!inw_t_) {  // every element is written by the transpose below: no (null-stream) memset
     void* p = nullptr;
@@ -618,11 +652,13 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
   if (gv != gvmap_.end() && M <= 64 && (gemv_mask_ & gv->second.bit)) {  // register-resident weights (derive_gemv)
     const GemvShape g = gv->second.g;
     const float* P = gv->second.packed;
+    const uint32_t* q8 = gv->second.q8;
+    const float* sc = gv->second.scale;
     const int Sg = K / g.ks();
     PTTS_REQUIRE((size_t)Sg * M * N <= pcap_, "split-K partial buffer too small");
     float* part = partial_;
-    ops.push_back({name, [=](hipStream_t s) { gemv_splitk(X, ldx, M, N, K, P, g, part, s); }, 2.0 * M * N * K,
-                   4.0 * N * K + 4.0 * ((double)M * K + (double)Sg * M * N)});
+    ops.push_back({name, [=](hipStream_t s) { gemv_splitk(X, ldx, M, N, K, P, g, part, s, q8, sc); }, 2.0 * M * N * K,
+                   (q8 ? 1.0 * N * K + 4.0 * N : 4.0 * N * K) + 4.0 * ((double)M * K + (double)Sg * M * N)});
     *S_out = Sg;
     return;
   }
@@ -866,8 +902,18 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       int* err = herr_;
       const int set = l & 1;
       const int groups = ffn_groups_;
-      Op op{p + ".ffn", [=](hipStream_t s) { ffn_fused(A, M, P1, P2, groups, hand, set, Pp, err, s); },
-            2.0 * M * FF * D * 2, 4.0 * (2.0 * FF * D + (double)M * D + (double)groups * M * D)};
+      auto f8 = ffn8map_.find(W(t.l2));  // weight_quant engines: int8 codes of both matrices
+      const uint32_t *Q1 = nullptr, *Q2 = nullptr;
+      const float *s1 = nullptr, *s2 = nullptr;
+      if (f8 != ffn8map_.end()) {
+        Q1 = f8->second.first.first;
+        s1 = f8->second.first.second;
+        Q2 = f8->second.second.first;
+        s2 = f8->second.second.second;
+      }
+      Op op{p + ".ffn", [=](hipStream_t s) { ffn_fused(A, M, P1, P2, groups, hand, set, Pp, err, s, Q1, s1, Q2, s2); },
+            2.0 * M * FF * D * 2,
+            (Q1 ? 2.0 * FF * D + 8.0 * (FF + D) : 8.0 * FF * D) + 4.0 * ((double)M * D + (double)groups * M * D)};
       // an isolated replay (time_op, overlap_probe) finds its set empty again
       op.prep = [hand](hipStream_t s) { PTTS_HIP(hipMemsetD32Async(hand, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, s)); };
       ops.push_back(op);
@@ -1970,12 +2016,26 @@ void Engine::overlap_probe(int B, int reps, double* us) {
       if (q == std::string::npos) q = spec.size();
       const std::string item = spec.substr(p, q - p);
       p = q + 1;
-      const int F = atoi(item.c_str()), K = atoi(item.substr(item.find(':') + 1).c_str());
+      // the back side may be a stand-in on the other CUs: "F:eN" N empty launches per step, "F:mN"
+      // one copy kernel moving N MB (read + write) per step
+      const std::string bs = item.substr(item.find(':') + 1);
+      const char kind = bs.empty() ? '0' : bs[0];
+      const bool dummy = kind == 'e' || kind == 'm';
+      const int F = atoi(item.c_str()), K = dummy ? 8 - F : atoi(bs.c_str()), N = dummy ? atoi(bs.c_str() + 1) : 0;
+      float* big = nullptr;
+      if (kind == 'm') PTTS_HIP(hipMalloc(&big, (size_t)N << 20));
+      fprintf(stderr, "split %d:%s: streams\n", F, bs.c_str());
       hipStream_t sf = F > 0 ? make_masked(0, F) : nullptr, sb = K > 0 ? make_masked(8 - K, 8) : nullptr;
+      fprintf(stderr, "split %d:%s: warm\n", F, bs.c_str());
       auto one = [&]() {
         if (sf)
           for (size_t i = 0; i < cut; ++i) ops[i].fn(sf);
-        if (sb) {
+        if (sb && kind == 'e') {
+          for (int i = 0; i < N; ++i) copy2d(x_, 1, q_, 1, 1, 1, sb);
+        } else if (sb && kind == 'm') {
+          const long half = ((long)N << 20) / 8;  // floats copied: N/2 MB read + N/2 MB written
+          copy2d(big, 1024, big + half, 1024, (int)(half / 1024), 1024, sb);
+        } else if (sb) {
           set_wg_cap(back_cap_);
           for (size_t i = cut; i < ops.size(); ++i) ops[i].fn(sb);
           set_wg_cap(0);
@@ -1993,9 +2053,11 @@ void Engine::overlap_probe(int B, int reps, double* us) {
       PTTS_HIP(hipEventSynchronize(e1));
       float ms = 0.f;
       PTTS_HIP(hipEventElapsedTime(&ms, e0, e1));
-      fprintf(stderr, "split front %d/8 back %d/8: %.1f us per step\n", F, K, 1000.0 * ms / reps);
+      fprintf(stderr, "split front %d/8 back %d/8 (%s): %.1f us per step\n", F, K, dummy ? bs.c_str() : "ops",
+              1000.0 * ms / reps);
       if (sf) (void)hipStreamDestroy(sf);
       if (sb) (void)hipStreamDestroy(sb);
+      if (big) (void)hipFree(big);
     }
   }
   for (int part = 0; part < 2; ++part) {

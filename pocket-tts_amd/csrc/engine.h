@@ -124,7 +124,14 @@ class Engine {
     const float* packed;
     GemvShape g;
     int bit;  // PTTS_GEMV mask bit of the matrix
+    const uint32_t* q8;   // weight_quant engines: the int8 codes in pack_q8 order, or nullptr
+    const float* scale;   // their row scales
   };
+  // int8 codes of a quantized matrix in the fragment order `pack` gives its f32 values (pack_q8)
+  const uint32_t* pack_codes(const float* W, int N, int K, int nj, const std::function<void(const float*, float*)>& pack);
+  // fused feed-forward of weight_quant engines: linear2 weight -> ((linear1 codes, scales), (linear2 codes, scales))
+  std::map<const float*, std::pair<std::pair<const uint32_t*, const float*>, std::pair<const uint32_t*, const float*>>>
+      ffn8map_;
   std::map<const float*, Gemv> gvmap_;
   // whole-K copies of the FlowLM linear1 matrices for gemv_fk (weight -> packed copy), and the
   // A-fragment-order copy of the norm2 output the step's out reduce writes for it

@@ -179,11 +179,24 @@ constexpr long FFN_HAND_FLOATS = 16L * 32 * 256;
 bool ffn_fused_supported(int M, int D, int FF);
 // groups: 16 (linear2 K slices of 256, 16 slabs) or 8 (slices of 512 with 32 members, 8 slabs)
 void pack_ffn2(const float* W2, int groups, float* packed, hipStream_t s);  // linear2 [1024][4096] -> fragment order
+// Q1 / Q2 (optional, weight_quant engines): linear1 / linear2 as int8 codes in pack_q8 order with
+// their row scales s1 / s2 (float(q) * s == the quantized f32 weight, bit for bit, derive_int8):
+// the codes are widened to f32 in registers, so the MFMA chain and the result are those of the f32
+// fragments (P1 / P2 unused when the codes are given)
 void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, int groups, float* hand, int set, float* P,
-               int* err, hipStream_t s);
+               int* err, hipStream_t s, const uint32_t* Q1 = nullptr, const float* s1 = nullptr,
+               const uint32_t* Q2 = nullptr, const float* s2 = nullptr);
 void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStream_t s);
+// q8 / scale (optional): the weight as int8 codes in pack_q8 order + row scales, as for ffn_fused
 void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
-                 hipStream_t s);
+                 hipStream_t s, const uint32_t* q8 = nullptr, const float* scale = nullptr);
+// int8 codes of the register-resident GEMMs: a fragment-packed copy (pack_gemv / pack_gemv_fk /
+// pack_ffn2 applied to the codes widened to f32, codes_to_f32) re-packed to one byte per element
+// with a lane's four consecutive fragment groups in one 16-B load: u32x4 (P * NJ / 4 + J) * 64 + l
+// holds the groups 4 J .. 4 J + 3 of f32 float4 index (P * NJ + j) * 64 + l (NJ: groups per lane
+// and wave, a multiple of 4; n4 float4 in the f32 copy)
+void codes_to_f32(const int8_t* q, long n, float* out, hipStream_t s);
+void pack_q8(const float* packed_codes, long n4, int nj, uint32_t* q8, hipStream_t s);
 
 // int8 codes of a quantized weight matrix: q[n][k] = W[n][k] / s[n] (exact integers in
 // [-127, 127] for a blob packed by the quantizer); rows with s[n] == 0 get code 0. Any element

@@ -1757,9 +1757,16 @@ __global__ void k_pack_gemv(const float* __restrict__ W, int N, int K, int wn, i
   reinterpret_cast<float4*>(P)[i4] = *reinterpret_cast<const float4*>(W + (long)n * K + k);
 }
 
-template <int WN, int KW>
+// int8 weight codes (engines with weight_quant): code word -> the f32 weight quad float(q) * s
+__device__ __forceinline__ float4 q8_quad(unsigned q, float sc) {
+  return make_float4((float)(int)(signed char)(q & 0xff) * sc, (float)(int)(signed char)((q >> 8) & 0xff) * sc,
+                     (float)(int)(signed char)((q >> 16) & 0xff) * sc, (float)((int)q >> 24) * sc);
+}
+
+template <int WN, int KW, bool Q8 = false>
 __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long ldx, int M, int N,
-                                              const float* __restrict__ P, float* __restrict__ partial) {
+                                              const float* __restrict__ P, float* __restrict__ partial,
+                                              const uint32_t* __restrict__ P8, const float* __restrict__ scale) {
   front_prio();
   constexpr int WK = 4 / WN, KS = KW * WK, NV = KW / 8, LDA = KS + 4;  // +4: conflict-free b128 rows
   __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
@@ -1778,17 +1785,27 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   }
   typedef float f4v __attribute__((ext_vector_type(4)));
   const f4v* wp = reinterpret_cast<const f4v*>(P) + (((long)t * S + z) * 4 + wave) * NV * 64 + lane;
-  f4v w[NV];
+  f4v w[Q8 ? 1 : NV];
+  u32x4 wq[Q8 ? NV / 4 : 1];
+  const int m = lane & 31, h = lane >> 5, wn = wave % WN, wk = wave / WN;
+  const int n = t * 32 * WN + wn * 32 + m;
+  if (Q8) {  // codes: NV / 4 16-B loads per lane (pack_q8 order)
+    const u32x4* qp = reinterpret_cast<const u32x4*>(P8) + (((long)t * S + z) * 4 + wave) * (NV / 4) * 64 + lane;
 #pragma unroll
-  for (int j = 0; j < NV; ++j)
-    w[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);  // once-read
+    for (int j = 0; j < NV / 4; ++j)
+      wq[j] = (front_skip() & 1) ? u32x4{0u, 0u, 0u, 0u} : __builtin_nontemporal_load(qp + j * 64);
+  } else {
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      w[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);  // once-read
+  }
+  const float sc = Q8 ? scale[n] : 0.f;
 #pragma unroll
   for (int i = 0; i < AV; ++i) {
     const int e = tid + 256 * i, row = e / (KS / 4), c4 = e % (KS / 4);
     *reinterpret_cast<float4*>(&sA[row * LDA + 4 * c4]) = av[i];
   }
   __syncthreads();
-  const int m = lane & 31, h = lane >> 5, wn = wave % WN, wk = wave / WN;
   const float* ar = &sA[m * LDA + wk * KW + h * (KW / 2)];
   floatx16 acc;
 #pragma unroll
@@ -1797,12 +1814,14 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   for (int j = 0; j < NV; ++j) {
     if (front_skip() & 2) break;
     const float4 a = *reinterpret_cast<const float4*>(ar + 4 * j);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, w[j].x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, w[j].y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, w[j].z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, w[j].w, acc, 0, 0, 0);
+    float4 b;
+    if (Q8) b = q8_quad(wq[j / 4][j % 4], sc);
+    else b = make_float4(w[j].x, w[j].y, w[j].z, w[j].w);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
   }
-  const int n = t * 32 * WN + wn * 32 + m;
   float* out = partial + (long)z * M * N;
   if (WK == 1) {
 #pragma unroll
@@ -1939,10 +1958,12 @@ __global__ void k_pack_ffn2(const float* __restrict__ W, float* __restrict__ P) 
   reinterpret_cast<float4*>(P)[f] = *reinterpret_cast<const float4*>(W + (long)n * 4096 + k);
 }
 
-template <int NG>
+template <int NG, bool Q8 = false>
 __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, int M, const float* __restrict__ P1,
                                                    const float* __restrict__ P2, float* __restrict__ hand, int set,
-                                                   float* __restrict__ P, int* err) {
+                                                   float* __restrict__ P, int* err, const uint32_t* __restrict__ Q1,
+                                                   const float* __restrict__ s1, const uint32_t* __restrict__ Q2,
+                                                   const float* __restrict__ s2) {
   constexpr int MB = 256 / NG;        // members per group
   constexpr int CT = 1024 / MB / 32;  // linear2 32-column tiles per member
   constexpr int KG = 4096 / NG;       // linear2 K slice of a group = linear1 columns of the group
@@ -1968,28 +1989,50 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
   const f4v* wp = reinterpret_cast<const f4v*>(P1) + ((long)(ct * 8 + w) * 8) * 64 + lane;
   const f4v* ap = reinterpret_cast<const f4v*>(A) + ((long)(w * 2) * 8) * 64 + lane;
   const f4v* w2p = reinterpret_cast<const f4v*>(P2) + ((long)((z * MB + i) * 8 + w) * 8) * 64 + lane;
-  f4v b[8], a0[8], a1[8], b2[8];
+  f4v b[Q8 ? 1 : 8], a0[8], a1[8], b2[Q8 ? 1 : 8];
+  u32x4 q1[Q8 ? 2 : 1], q2[Q8 ? 2 : 1];
+  if (Q8) {  // int8 codes (pack_q8 order): two 16-B loads per lane and matrix
+    const u32x4* q1p = reinterpret_cast<const u32x4*>(Q1) + ((long)(ct * 8 + w) * 2) * 64 + lane;
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    b[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);
+    for (int j = 0; j < 2; ++j)
+      q1[j] = (front_skip() & 1) ? u32x4{0u, 0u, 0u, 0u} : __builtin_nontemporal_load(q1p + j * 64);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      b[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     a0[j] = ap[j * 64];
     a1[j] = ap[(8 + j) * 64];
   }
+  if (Q8) {
+    const u32x4* q2p = reinterpret_cast<const u32x4*>(Q2) + ((long)((z * MB + i) * 8 + w) * 2) * 64 + lane;
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    b2[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(w2p + j * 64);
+    for (int j = 0; j < 2; ++j)
+      q2[j] = (front_skip() & 1) ? u32x4{0u, 0u, 0u, 0u} : __builtin_nontemporal_load(q2p + j * 64);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      b2[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(w2p + j * 64);
+  }
+  // row scales of this lane's linear1 column and linear2 column (int8 codes)
+  const float sc1 = Q8 ? s1[ct * 16 + (lane & 15)] : 0.f;
+  const float sc2 = Q8 ? s2[(1024 / MB) * i + 32 * (w % CT) + (lane & 31)] : 0.f;
   __builtin_amdgcn_sched_barrier(0);
   // ---- linear1 + GELU (k_gemv_fk): two 16-row tiles, the 8 waves' partial tiles summed in LDS
   floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (front_skip() & 2) break;
+    float4 bq;
+    if (Q8) bq = q8_quad(q1[j / 4][j % 4], sc1);
+    else bq = make_float4(b[j][0], b[j][1], b[j][2], b[j][3]);
+    const float be[4] = {bq.x, bq.y, bq.z, bq.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][e], b[j][e], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][e], b[j][e], c1, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][e], be[e], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][e], be[e], c1, 0, 0, 0);
     }
   }
 #pragma unroll
@@ -2046,10 +2089,13 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (front_skip() & 2) break;
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, b2[j].x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, b2[j].y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, b2[j].z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, b2[j].w, acc, 0, 0, 0);
+    float4 bq;
+    if (Q8) bq = q8_quad(q2[j / 4][j % 4], sc2);
+    else bq = make_float4(b2[j][0], b2[j][1], b2[j][2], b2[j][3]);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, bq.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, bq.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, bq.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, bq.w, acc, 0, 0, 0);
   }
   // the 8 / CT k parts of each column tile summed in k order; slab z of P
 #pragma unroll
@@ -2087,15 +2133,51 @@ void pack_ffn2(const float* W2, int groups, float* packed, hipStream_t s) {
 }
 
 void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, int groups, float* hand, int set, float* P,
-               int* err, hipStream_t s) {
+               int* err, hipStream_t s, const uint32_t* Q1, const float* s1, const uint32_t* Q2, const float* s2) {
   if (!ffn_fused_supported(M, 1024, 4096) || (set != 0 && set != 1) || (groups != 8 && groups != 16))
     throw std::runtime_error("ffn_fused: bad shape");
-  if (groups == 16)
+  if (!Q1 != !Q2 || (Q1 && (!s1 || !s2))) throw std::runtime_error("ffn_fused: int8 codes of both matrices, with scales");
+  if (Q1 && groups == 8)
+    hipLaunchKernelGGL((k_ffn_fused<8, true>), dim3(256), dim3(512), cap_lds(k_ffn_fused<8, true>, g_wg_cap), s, Afrag, M,
+                       P1, P2, hand, set, P, err, Q1, s1, Q2, s2);
+  else if (Q1)
+    hipLaunchKernelGGL((k_ffn_fused<16, true>), dim3(256), dim3(512), cap_lds(k_ffn_fused<16, true>, g_wg_cap), s,
+                       Afrag, M, P1, P2, hand, set, P, err, Q1, s1, Q2, s2);
+  else if (groups == 16)
     hipLaunchKernelGGL(k_ffn_fused<16>, dim3(256), dim3(512), cap_lds(k_ffn_fused<16>, g_wg_cap), s, Afrag, M, P1, P2,
-                       hand, set, P, err);
+                       hand, set, P, err, nullptr, nullptr, nullptr, nullptr);
   else
     hipLaunchKernelGGL(k_ffn_fused<8>, dim3(256), dim3(512), cap_lds(k_ffn_fused<8>, g_wg_cap), s, Afrag, M, P1, P2,
-                       hand, set, P, err);
+                       hand, set, P, err, nullptr, nullptr, nullptr, nullptr);
+}
+
+__global__ void k_codes_to_f32(const int8_t* __restrict__ q, long n, float* __restrict__ out) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = (float)q[i];
+}
+void codes_to_f32(const int8_t* q, long n, float* out, hipStream_t s) {
+  const long blocks = std::min<long>((n + 255) / 256, 8192);
+  if (blocks > 0) hipLaunchKernelGGL(k_codes_to_f32, dim3((unsigned)blocks), dim3(256), 0, s, q, n, out);
+}
+__global__ void k_pack_q8(const float* __restrict__ pf, long n16, int nj, uint32_t* __restrict__ q8) {
+  const long gi = (long)blockIdx.x * 256 + threadIdx.x;  // u32x4 index
+  if (gi >= n16) return;
+  const int l = (int)(gi & 63);
+  const long q = gi >> 6;
+  const int J = (int)(q % (nj / 4));
+  const long P = q / (nj / 4);
+  u32x4 o;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const float4 f = reinterpret_cast<const float4*>(pf)[(P * nj + 4 * J + jj) * 64 + l];
+    o[jj] = ((unsigned)(int)f.x & 0xffu) | (((unsigned)(int)f.y & 0xffu) << 8) | (((unsigned)(int)f.z & 0xffu) << 16) |
+            ((unsigned)(int)f.w << 24);
+  }
+  reinterpret_cast<u32x4*>(q8)[gi] = o;
+}
+void pack_q8(const float* packed_codes, long n4, int nj, uint32_t* q8, hipStream_t s) {
+  if (nj % 4 != 0 || n4 % ((long)nj * 64) != 0) throw std::runtime_error("pack_q8: bad shape");
+  const long n16 = n4 / 4;
+  hipLaunchKernelGGL(k_pack_q8, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, s, packed_codes, n16, nj, q8);
 }
 
 bool gemv_supported(GemvShape g, int N, int K) {
@@ -2112,13 +2194,18 @@ void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStre
 }
 
 void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
-                 hipStream_t s) {
+                 hipStream_t s, const uint32_t* q8, const float* scale) {
   if (M < 1 || M > 64 || !gemv_supported(g, N, K)) throw std::runtime_error("gemv_splitk: unsupported shape");
+  if (q8 && (!scale || g.kw % 32 != 0)) throw std::runtime_error("gemv_splitk: int8 codes need scales, kw % 32 == 0");
   const dim3 grid((unsigned)(N / (32 * g.wn)), (unsigned)(K / g.ks()), (unsigned)((M + 31) / 32));
 #define PTTS_GEMV(WN_, KW_)                                                                              \
   if (g.wn == WN_ && g.kw == KW_) {                                                                      \
-    hipLaunchKernelGGL((k_gemv<WN_, KW_>), grid, dim3(256), cap_lds(k_gemv<WN_, KW_>, g_wg_cap), s, X, ldx, M, N, \
-                       packed, partial);                                                                 \
+    if (q8)                                                                                              \
+      hipLaunchKernelGGL((k_gemv<WN_, KW_, true>), grid, dim3(256), cap_lds(k_gemv<WN_, KW_, true>, g_wg_cap), s, X, \
+                         ldx, M, N, packed, partial, q8, scale);                                         \
+    else                                                                                                 \
+      hipLaunchKernelGGL((k_gemv<WN_, KW_>), grid, dim3(256), cap_lds(k_gemv<WN_, KW_>, g_wg_cap), s, X, ldx, M, \
+                         N, packed, partial, nullptr, nullptr);                                          \
     return;                                                                                              \
   }
   PTTS_GEMV(4, 128)
