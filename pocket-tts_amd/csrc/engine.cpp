@@ -346,17 +346,20 @@ void Engine::load_blob(const float* host, size_t n_bytes) {
 // The int8 codes of quantized weight W [N][K] (derive_int8) in pack_q8 order: the codes widened
 // to f32 (temporary), fragment-packed by `pack` exactly as the f32 weight would be, then one byte
 // per element with a lane's four fragment groups per 16-B load (nj: groups per lane and wave).
+// fp8_gemm engines: the e4m3 codes of fp8_codes (f8map_) the same way.
 const uint32_t* Engine::pack_codes(const float* W, int N, int K, int nj,
                                    const std::function<void(const float*, float*)>& pack) {
   auto it = q8map_.find(W);
-  if (it == q8map_.end()) return nullptr;
+  auto it8 = f8map_.find(W);
+  if (it == q8map_.end() && it8 == f8map_.end()) return nullptr;
   const size_t n = (size_t)N * K;
   float* tmp = nullptr;
   PTTS_HIP(hipMalloc(&tmp, sizeof(float) * 2 * n));
   void* q = nullptr;
   PTTS_HIP(hipMalloc(&q, n));
   allocs_.push_back(q);
-  codes_to_f32(it->second.first, (long)n, tmp, stream_);
+  if (it != q8map_.end()) codes_to_f32(it->second.first, (long)n, tmp, stream_);
+  else codes_u8_to_f32(it8->second.first, (long)n, tmp, stream_);
   pack(tmp, tmp + n);
   pack_q8(tmp + n, (long)(n / 4), nj, (uint32_t*)q, stream_);
   PTTS_HIP(hipStreamSynchronize(stream_));
@@ -421,7 +424,8 @@ void Engine::derive_gemv() {
         const int G = ffn_groups_;
         const uint32_t* q1 = pack_codes(w1, FF, D, 8, [&](const float* c, float* o) { pack_gemv_fk(c, FF, D, o, stream_); });
         const uint32_t* q2 = pack_codes(w2, D, FF, 8, [&](const float* c, float* o) { pack_ffn2(c, G, o, stream_); });
-        if (q1 && q2) ffn8map_[w2] = {{q1, q8map_.at(w1).second}, {q2, q8map_.at(w2).second}};
+        auto sc = [&](const float* w) { return fp8_ ? f8map_.at(w).second : q8map_.at(w).second; };
+        if (q1 && q2) ffn8map_[w2] = {{q1, sc(w1)}, {q2, sc(w2)}};
       }
       ffn_hand_ = fd;  // both sets empty (0xFFFFFFFF) before the first launch
       PTTS_HIP(hipMemsetD32Async(ffn_hand_, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, stream_));
@@ -439,11 +443,14 @@ void Engine::derive_gemv() {
     if (!(mask & m.bit) || !gemv_supported(m.g, m.N, m.K)) continue;
     pack_gemv(m.w, m.N, m.K, m.g, dst, stream_);
     Gemv gv{dst, m.g, m.bit, nullptr, nullptr};
-    // weight_quant engines: the int8 codes of a quantized matrix in the same fragment order
+    // weight_quant engines: the int8 codes of a quantized matrix in the same fragment order;
+    // fp8_gemm engines: the e4m3 codes of the {4, 128} matrices (qkv, adaLN; W8A8 tiles)
     const GemvShape g = m.g;
     const int N = m.N, K = m.K;
-    gv.q8 = pack_codes(m.w, N, K, g.kw / 8, [&](const float* c, float* o) { pack_gemv(c, N, K, g, o, stream_); });
-    if (gv.q8) gv.scale = q8map_.at(m.w).second;
+    if (!fp8_ || (g.wn == 4 && g.kw == 128)) {
+      gv.q8 = pack_codes(m.w, N, K, g.kw / 8, [&](const float* c, float* o) { pack_gemv(c, N, K, g, o, stream_); });
+      if (gv.q8) gv.scale = fp8_ ? f8map_.at(m.w).second : q8map_.at(m.w).second;
+    }
     gvmap_[m.w] = gv;
     dst += (size_t)m.N * m.K;
   }
@@ -500,7 +507,7 @@ void Engine::finalize() {
   PTTS_HIP(hipSetDevice(dev_));
   if (wq_ != QUANT_NONE && q8map_.empty()) derive_int8();
   if (fp8_ && f8map_.empty()) derive_fp8();
-  if (!fp8_ && gvmap_.empty()) derive_gemv();
+  if (gvmap_.empty()) derive_gemv();
   if (back_mfma_ == PTTS_BACK_F32X6 && split_.empty()) derive_split();
   if (!inw_t_) {  // every element is written by the transpose below: no (null-stream) memset
     void* p = nullptr;
@@ -657,7 +664,8 @@ void Engine::linear_split(std::vector<Op>& ops, const std::string& name, const f
     const int Sg = K / g.ks();
     PTTS_REQUIRE((size_t)Sg * M * N <= pcap_, "split-K partial buffer too small");
     float* part = partial_;
-    ops.push_back({name, [=](hipStream_t s) { gemv_splitk(X, ldx, M, N, K, P, g, part, s, q8, sc); }, 2.0 * M * N * K,
+    const bool f8 = fp8_ && q8;
+    ops.push_back({name, [=](hipStream_t s) { gemv_splitk(X, ldx, M, N, K, P, g, part, s, q8, sc, f8); }, 2.0 * M * N * K,
                    (q8 ? 1.0 * N * K + 4.0 * N : 4.0 * N * K) + 4.0 * ((double)M * K + (double)Sg * M * N)});
     *S_out = Sg;
     return;
@@ -911,7 +919,8 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
         Q2 = f8->second.second.first;
         s2 = f8->second.second.second;
       }
-      Op op{p + ".ffn", [=](hipStream_t s) { ffn_fused(A, M, P1, P2, groups, hand, set, Pp, err, s, Q1, s1, Q2, s2); },
+      const bool e4m3 = fp8_ && Q1;
+      Op op{p + ".ffn", [=](hipStream_t s) { ffn_fused(A, M, P1, P2, groups, hand, set, Pp, err, s, Q1, s1, Q2, s2, e4m3); },
             2.0 * M * FF * D * 2,
             (Q1 ? 2.0 * FF * D + 8.0 * (FF + D) : 8.0 * FF * D) + 4.0 * ((double)M * D + (double)groups * M * D)};
       // an isolated replay (time_op, overlap_probe) finds its set empty again

@@ -183,19 +183,22 @@ void pack_ffn2(const float* W2, int groups, float* packed, hipStream_t s);  // l
 // their row scales s1 / s2 (float(q) * s == the quantized f32 weight, bit for bit, derive_int8):
 // the codes are widened to f32 in registers, so the MFMA chain and the result are those of the f32
 // fragments (P1 / P2 unused when the codes are given)
+// fp8: Q1 / Q2 are e4m3 codes (fp8_codes) and both GEMMs run W8A8 on the fp8 MFMA (8 groups)
 void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, int groups, float* hand, int set, float* P,
                int* err, hipStream_t s, const uint32_t* Q1 = nullptr, const float* s1 = nullptr,
-               const uint32_t* Q2 = nullptr, const float* s2 = nullptr);
+               const uint32_t* Q2 = nullptr, const float* s2 = nullptr, bool fp8 = false);
 void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStream_t s);
-// q8 / scale (optional): the weight as int8 codes in pack_q8 order + row scales, as for ffn_fused
+// q8 / scale (optional): the weight as int8 codes in pack_q8 order + row scales, as for ffn_fused;
+// fp8: the codes are e4m3 (fp8_codes) and the tile runs W8A8 on the fp8 MFMA ({4, 128} tiles)
 void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
-                 hipStream_t s, const uint32_t* q8 = nullptr, const float* scale = nullptr);
+                 hipStream_t s, const uint32_t* q8 = nullptr, const float* scale = nullptr, bool fp8 = false);
 // int8 codes of the register-resident GEMMs: a fragment-packed copy (pack_gemv / pack_gemv_fk /
 // pack_ffn2 applied to the codes widened to f32, codes_to_f32) re-packed to one byte per element
 // with a lane's four consecutive fragment groups in one 16-B load: u32x4 (P * NJ / 4 + J) * 64 + l
 // holds the groups 4 J .. 4 J + 3 of f32 float4 index (P * NJ + j) * 64 + l (NJ: groups per lane
 // and wave, a multiple of 4; n4 float4 in the f32 copy)
 void codes_to_f32(const int8_t* q, long n, float* out, hipStream_t s);
+void codes_u8_to_f32(const uint8_t* q, long n, float* out, hipStream_t s);  // fp8 codes as their byte values
 void pack_q8(const float* packed_codes, long n4, int nj, uint32_t* q8, hipStream_t s);
 
 // int8 codes of a quantized weight matrix: q[n][k] = W[n][k] / s[n] (exact integers in

@@ -1763,10 +1763,29 @@ __device__ __forceinline__ float4 q8_quad(unsigned q, float sc) {
                      (float)(int)(signed char)((q >> 16) & 0xff) * sc, (float)((int)q >> 24) * sc);
 }
 
-template <int WN, int KW, bool Q8 = false>
+// fp8 A operand: 8 f32 values * inv -> 8 e4m3 bytes (one MFMA operand)
+__device__ __forceinline__ long f8_pack8(const float* v, float inv) {
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, hi, true);
+  return (long)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ long u32x2_long(unsigned lo, unsigned hi) {
+  return (long)(((unsigned long)hi << 32) | lo);
+}
+
+// WQ: the weight form. 0 f32 fragments; 1 int8 codes of a quantized matrix (weight_quant: widened
+// to the same f32 weights in registers); 2 e4m3 codes (fp8_gemm, W8A8: {4, 128} tiles only) - the
+// 32 rows of the X slice quantized to e4m3 with one scale per (row, slice) = max |x| / 448 (every
+// wave computes the same scales from the LDS slice), v_mfma_f32_32x32x16_fp8_fp8 over the slice
+// (lane (r, h) supplies k 64 h + 8 s .. + 7 of step s for A and B alike), slab = acc * sa * sw.
+template <int WN, int KW, int WQ = 0>
 __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long ldx, int M, int N,
                                               const float* __restrict__ P, float* __restrict__ partial,
                                               const uint32_t* __restrict__ P8, const float* __restrict__ scale) {
+  static_assert(WQ != 2 || (WN == 4 && KW == 128), "fp8 gemv: {4, 128} tiles");
+  constexpr bool Q8 = WQ == 1;
   front_prio();
   constexpr int WK = 4 / WN, KS = KW * WK, NV = KW / 8, LDA = KS + 4;  // +4: conflict-free b128 rows
   __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
@@ -1785,11 +1804,11 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   }
   typedef float f4v __attribute__((ext_vector_type(4)));
   const f4v* wp = reinterpret_cast<const f4v*>(P) + (((long)t * S + z) * 4 + wave) * NV * 64 + lane;
-  f4v w[Q8 ? 1 : NV];
-  u32x4 wq[Q8 ? NV / 4 : 1];
+  f4v w[WQ ? 1 : NV];
+  u32x4 wq[WQ ? NV / 4 : 1];
   const int m = lane & 31, h = lane >> 5, wn = wave % WN, wk = wave / WN;
   const int n = t * 32 * WN + wn * 32 + m;
-  if (Q8) {  // codes: NV / 4 16-B loads per lane (pack_q8 order)
+  if (WQ) {  // codes: NV / 4 16-B loads per lane (pack_q8 order)
     const u32x4* qp = reinterpret_cast<const u32x4*>(P8) + (((long)t * S + z) * 4 + wave) * (NV / 4) * 64 + lane;
 #pragma unroll
     for (int j = 0; j < NV / 4; ++j)
@@ -1799,7 +1818,7 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
     for (int j = 0; j < NV; ++j)
       w[j] = (front_skip() & 1) ? f4v{0.f, 0.f, 0.f, 0.f} : __builtin_nontemporal_load(wp + j * 64);  // once-read
   }
-  const float sc = Q8 ? scale[n] : 0.f;
+  const float sc = WQ ? scale[n] : 0.f;
 #pragma unroll
   for (int i = 0; i < AV; ++i) {
     const int e = tid + 256 * i, row = e / (KS / 4), c4 = e % (KS / 4);
@@ -1810,6 +1829,35 @@ __global__ __launch_bounds__(256) void k_gemv(const float* __restrict__ X, long 
   floatx16 acc;
 #pragma unroll
   for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+  if (WQ == 2) {  // ---- fp8 W8A8: this lane's 64 values of row m, the row scale, 8 fp8 MFMAs
+    float xv[KW / 2];
+#pragma unroll
+    for (int j = 0; j < KW / 8; ++j) {
+      const float4 a = *reinterpret_cast<const float4*>(ar + 4 * j);
+      xv[4 * j] = a.x, xv[4 * j + 1] = a.y, xv[4 * j + 2] = a.z, xv[4 * j + 3] = a.w;
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < KW / 2; ++j) mx = fmaxf(mx, fabsf(xv[j]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float inv = mx > 0.f ? 448.f / mx : 0.f, sa = mx / 448.f;
+#pragma unroll
+    for (int st = 0; st < KW / 16; ++st) {
+      const long a8 = f8_pack8(&xv[8 * st], inv);
+      const u32x4 q = wq[st >> 1];
+      const long b8 = (st & 1) ? u32x2_long(q[2], q[3]) : u32x2_long(q[0], q[1]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a8, b8, acc, 0, 0, 0);
+    }
+    // slab value acc * sa(row) * sw(column): the row of register g is (g & 3) + 8 (g >> 2) + 4 h
+    float* out = partial + (long)z * M * N;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int rl = (g & 3) + 8 * (g >> 2) + 4 * h, row = m0 + rl;
+      const float sar = __shfl(sa, rl, 64);
+      if (row < M) out[(long)row * N + n] = acc[g] * sar * sc;
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     if (front_skip() & 2) break;
@@ -1958,7 +2006,13 @@ __global__ void k_pack_ffn2(const float* __restrict__ W, float* __restrict__ P) 
   reinterpret_cast<float4*>(P)[f] = *reinterpret_cast<const float4*>(W + (long)n * 4096 + k);
 }
 
-template <int NG, bool Q8 = false>
+// WQ as k_gemv: 0 f32, 1 int8 codes widened to f32, 2 e4m3 codes W8A8 on the fp8 MFMA - linear1:
+// each wave quantizes its two 16-row A tiles over its 128 k (one scale per (row, wave), max |a| /
+// 448 over the 4 lane groups of the row) and runs v_mfma_f32_16x16x32_fp8_fp8 (lane group g
+// supplies k 128 w + 32 g + 8 s .. + 7 of step s for A and B alike); linear2: each wave its 32 rows
+// over its 64-k part (lanes r, r + 32), v_mfma_f32_32x32x16_fp8_fp8; a wave's partial tile is
+// scaled by its row scales before the cross-wave sums, the column scale applied after them.
+template <int NG, int WQ = 0>
 __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, int M, const float* __restrict__ P1,
                                                    const float* __restrict__ P2, float* __restrict__ hand, int set,
                                                    float* __restrict__ P, int* err, const uint32_t* __restrict__ Q1,
@@ -1989,9 +2043,10 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
   const f4v* wp = reinterpret_cast<const f4v*>(P1) + ((long)(ct * 8 + w) * 8) * 64 + lane;
   const f4v* ap = reinterpret_cast<const f4v*>(A) + ((long)(w * 2) * 8) * 64 + lane;
   const f4v* w2p = reinterpret_cast<const f4v*>(P2) + ((long)((z * MB + i) * 8 + w) * 8) * 64 + lane;
+  constexpr bool Q8 = WQ != 0;
   f4v b[Q8 ? 1 : 8], a0[8], a1[8], b2[Q8 ? 1 : 8];
   u32x4 q1[Q8 ? 2 : 1], q2[Q8 ? 2 : 1];
-  if (Q8) {  // int8 codes (pack_q8 order): two 16-B loads per lane and matrix
+  if (Q8) {  // int8 / e4m3 codes (pack_q8 order): two 16-B loads per lane and matrix
     const u32x4* q1p = reinterpret_cast<const u32x4*>(Q1) + ((long)(ct * 8 + w) * 2) * 64 + lane;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -2022,17 +2077,47 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
   __builtin_amdgcn_sched_barrier(0);
   // ---- linear1 + GELU (k_gemv_fk): two 16-row tiles, the 8 waves' partial tiles summed in LDS
   floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+  if (WQ == 2) {
+    float x0[32], x1[32];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (front_skip() & 2) break;
-    float4 bq;
-    if (Q8) bq = q8_quad(q1[j / 4][j % 4], sc1);
-    else bq = make_float4(b[j][0], b[j][1], b[j][2], b[j][3]);
-    const float be[4] = {bq.x, bq.y, bq.z, bq.w};
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][e], be[e], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][e], be[e], c1, 0, 0, 0);
+      for (int e = 0; e < 4; ++e) x0[4 * j + e] = a0[j][e], x1[4 * j + e] = a1[j][e];
+    float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) m0 = fmaxf(m0, fabsf(x0[j])), m1 = fmaxf(m1, fabsf(x1[j]));
+    m0 = fmaxf(m0, __shfl_xor(m0, 16, 64));
+    m0 = fmaxf(m0, __shfl_xor(m0, 32, 64));
+    m1 = fmaxf(m1, __shfl_xor(m1, 16, 64));
+    m1 = fmaxf(m1, __shfl_xor(m1, 32, 64));
+    const float i0 = m0 > 0.f ? 448.f / m0 : 0.f, i1 = m1 > 0.f ? 448.f / m1 : 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const u32x4 q = q1[st >> 1];
+      const long b8 = (st & 1) ? u32x2_long(q[2], q[3]) : u32x2_long(q[0], q[1]);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(f8_pack8(&x0[8 * st], i0), b8, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(f8_pack8(&x1[8 * st], i1), b8, c1, 0, 0, 0);
+    }
+    // C register r of lane l: row (l >> 4) * 4 + r of the tile, whose scale lane that row holds
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = (lane >> 4) * 4 + r;
+      c0[r] *= __shfl(m0, rl, 64) / 448.f;
+      c1[r] *= __shfl(m1, rl, 64) / 448.f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (front_skip() & 2) break;
+      float4 bq;
+      if (Q8) bq = q8_quad(q1[j / 4][j % 4], sc1);
+      else bq = make_float4(b[j][0], b[j][1], b[j][2], b[j][3]);
+      const float be[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][e], be[e], c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][e], be[e], c1, 0, 0, 0);
+      }
     }
   }
 #pragma unroll
@@ -2047,6 +2132,7 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
 #pragma unroll
     for (int ww = 1; ww < 8; ++ww) v += red[((ww * 2 + t) * 4 + r) * 64 + ll];
     const int row = 16 * t + (ll >> 4) * 4 + r;
+    if (WQ == 2) v *= s1[ct * 16 + (ll & 15)];  // the e4m3 weight column's scale, after the wave sums
     sU[row * 16 + (ll & 15)] = row < M ? gelu_tanh(v) : 0.f;  // rows past M: handed off as 0
   }
   __syncthreads();
@@ -2086,16 +2172,35 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
   floatx16 acc;
 #pragma unroll
   for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+  if (WQ == 2) {
+    float xv[32];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (front_skip() & 2) break;
-    float4 bq;
-    if (Q8) bq = q8_quad(q2[j / 4][j % 4], sc2);
-    else bq = make_float4(b2[j][0], b2[j][1], b2[j][2], b2[j][3]);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, bq.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, bq.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, bq.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, bq.w, acc, 0, 0, 0);
+    for (int j = 0; j < 8; ++j) xv[4 * j] = av[j].x, xv[4 * j + 1] = av[j].y, xv[4 * j + 2] = av[j].z, xv[4 * j + 3] = av[j].w;
+    float mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) mx = fmaxf(mx, fabsf(xv[j]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float inv = mx > 0.f ? 448.f / mx : 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const u32x4 q = q2[st >> 1];
+      const long b8 = (st & 1) ? u32x2_long(q[2], q[3]) : u32x2_long(q[0], q[1]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(f8_pack8(&xv[8 * st], inv), b8, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] *= __shfl(mx, (g & 3) + 8 * (g >> 2) + 4 * (lane >> 5), 64) / 448.f;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (front_skip() & 2) break;
+      float4 bq;
+      if (Q8) bq = q8_quad(q2[j / 4][j % 4], sc2);
+      else bq = make_float4(b2[j][0], b2[j][1], b2[j][2], b2[j][3]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].x, bq.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].y, bq.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].z, bq.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j].w, bq.w, acc, 0, 0, 0);
+    }
   }
   // the 8 / CT k parts of each column tile summed in k order; slab z of P
 #pragma unroll
@@ -2111,7 +2216,9 @@ __global__ __launch_bounds__(512) void k_ffn_fused(const float* __restrict__ A, 
 #pragma unroll
       for (int qq = 1; qq < 8 / CT; ++qq) v += red[((qq * CT + c) * 16 + g) * 64 + ll];
       const int row = (g & 3) + 8 * (g >> 2) + 4 * (ll >> 5);
-      if (row < M) out[(long)row * 1024 + (1024 / MB) * i + 32 * c + (ll & 31)] = v;
+      const int col = (1024 / MB) * i + 32 * c + (ll & 31);
+      if (WQ == 2) v *= s2[col];  // the e4m3 weight column's scale, after the k-part sums
+      if (row < M) out[(long)row * 1024 + col] = v;
     }
   }
   // empty this workgroup's float4s of the other set for the next launch
@@ -2133,15 +2240,21 @@ void pack_ffn2(const float* W2, int groups, float* packed, hipStream_t s) {
 }
 
 void ffn_fused(const float* Afrag, int M, const float* P1, const float* P2, int groups, float* hand, int set, float* P,
-               int* err, hipStream_t s, const uint32_t* Q1, const float* s1, const uint32_t* Q2, const float* s2) {
+               int* err, hipStream_t s, const uint32_t* Q1, const float* s1, const uint32_t* Q2, const float* s2,
+               bool fp8) {
   if (!ffn_fused_supported(M, 1024, 4096) || (set != 0 && set != 1) || (groups != 8 && groups != 16))
     throw std::runtime_error("ffn_fused: bad shape");
   if (!Q1 != !Q2 || (Q1 && (!s1 || !s2))) throw std::runtime_error("ffn_fused: int8 codes of both matrices, with scales");
-  if (Q1 && groups == 8)
-    hipLaunchKernelGGL((k_ffn_fused<8, true>), dim3(256), dim3(512), cap_lds(k_ffn_fused<8, true>, g_wg_cap), s, Afrag, M,
+  if (Q1 && fp8 && groups == 8)
+    hipLaunchKernelGGL((k_ffn_fused<8, 2>), dim3(256), dim3(512), cap_lds(k_ffn_fused<8, 2>, g_wg_cap), s, Afrag, M, P1,
+                       P2, hand, set, P, err, Q1, s1, Q2, s2);
+  else if (Q1 && fp8)
+    throw std::runtime_error("ffn_fused: fp8 codes with 8 groups only");
+  else if (Q1 && groups == 8)
+    hipLaunchKernelGGL((k_ffn_fused<8, 1>), dim3(256), dim3(512), cap_lds(k_ffn_fused<8, 1>, g_wg_cap), s, Afrag, M,
                        P1, P2, hand, set, P, err, Q1, s1, Q2, s2);
   else if (Q1)
-    hipLaunchKernelGGL((k_ffn_fused<16, true>), dim3(256), dim3(512), cap_lds(k_ffn_fused<16, true>, g_wg_cap), s,
+    hipLaunchKernelGGL((k_ffn_fused<16, 1>), dim3(256), dim3(512), cap_lds(k_ffn_fused<16, 1>, g_wg_cap), s,
                        Afrag, M, P1, P2, hand, set, P, err, Q1, s1, Q2, s2);
   else if (groups == 16)
     hipLaunchKernelGGL(k_ffn_fused<16>, dim3(256), dim3(512), cap_lds(k_ffn_fused<16>, g_wg_cap), s, Afrag, M, P1, P2,
@@ -2157,6 +2270,13 @@ __global__ void k_codes_to_f32(const int8_t* __restrict__ q, long n, float* __re
 void codes_to_f32(const int8_t* q, long n, float* out, hipStream_t s) {
   const long blocks = std::min<long>((n + 255) / 256, 8192);
   if (blocks > 0) hipLaunchKernelGGL(k_codes_to_f32, dim3((unsigned)blocks), dim3(256), 0, s, q, n, out);
+}
+__global__ void k_codes_u8_to_f32(const uint8_t* __restrict__ q, long n, float* __restrict__ out) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = (float)q[i];
+}
+void codes_u8_to_f32(const uint8_t* q, long n, float* out, hipStream_t s) {
+  const long blocks = std::min<long>((n + 255) / 256, 8192);
+  if (blocks > 0) hipLaunchKernelGGL(k_codes_u8_to_f32, dim3((unsigned)blocks), dim3(256), 0, s, q, n, out);
 }
 __global__ void k_pack_q8(const float* __restrict__ pf, long n16, int nj, uint32_t* __restrict__ q8) {
   const long gi = (long)blockIdx.x * 256 + threadIdx.x;  // u32x4 index
@@ -2194,15 +2314,20 @@ void pack_gemv(const float* W, int N, int K, GemvShape g, float* packed, hipStre
 }
 
 void gemv_splitk(const float* X, long ldx, int M, int N, int K, const float* packed, GemvShape g, float* partial,
-                 hipStream_t s, const uint32_t* q8, const float* scale) {
+                 hipStream_t s, const uint32_t* q8, const float* scale, bool fp8) {
   if (M < 1 || M > 64 || !gemv_supported(g, N, K)) throw std::runtime_error("gemv_splitk: unsupported shape");
   if (q8 && (!scale || g.kw % 32 != 0)) throw std::runtime_error("gemv_splitk: int8 codes need scales, kw % 32 == 0");
   const dim3 grid((unsigned)(N / (32 * g.wn)), (unsigned)(K / g.ks()), (unsigned)((M + 31) / 32));
 #define PTTS_GEMV(WN_, KW_)                                                                              \
   if (g.wn == WN_ && g.kw == KW_) {                                                                      \
-    if (q8)                                                                                              \
-      hipLaunchKernelGGL((k_gemv<WN_, KW_, true>), grid, dim3(256), cap_lds(k_gemv<WN_, KW_, true>, g_wg_cap), s, X, \
+    if (q8 && fp8 && WN_ == 4 && KW_ == 128)                                                             \
+      hipLaunchKernelGGL((k_gemv<4, 128, 2>), grid, dim3(256), cap_lds(k_gemv<4, 128, 2>, g_wg_cap), s, X, ldx, M, \
+                         N, packed, partial, q8, scale);                                                 \
+    else if (q8 && !fp8)                                                                                 \
+      hipLaunchKernelGGL((k_gemv<WN_, KW_, 1>), grid, dim3(256), cap_lds(k_gemv<WN_, KW_, 1>, g_wg_cap), s, X, \
                          ldx, M, N, packed, partial, q8, scale);                                         \
+    else if (q8)                                                                                         \
+      throw std::runtime_error("gemv_splitk: fp8 codes on {4, 128} tiles only");                        \
     else                                                                                                 \
       hipLaunchKernelGGL((k_gemv<WN_, KW_>), grid, dim3(256), cap_lds(k_gemv<WN_, KW_>, g_wg_cap), s, X, ldx, M, \
                          N, packed, partial, nullptr, nullptr);                                          \
