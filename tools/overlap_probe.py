@@ -1,6 +1,7 @@
 """Time the FlowLM+flow-head part and the Mimi part of a B=32 step alone and concurrently."""
 import ctypes as C
 import faulthandler
+import os
 import sys
 from pathlib import Path
 
@@ -12,7 +13,7 @@ import pocket_tts_amd as pt  # noqa: E402
 from pocket_tts_amd._lib import check, lib  # noqa: E402
 
 faulthandler.dump_traceback_later(60, repeat=True)  # a stall shows where it sits
-B = 32
+B = int(os.environ.get("ROWS", "32"))  # rows of the step
 print("engine", flush=True)
 eng = pt.Engine(device=0, max_slots=B, max_ctx=400, lsd_decode_steps=1, seed=0x5EED)
 voice = eng.voice_from_prompt(bench.synth_prompt())
