@@ -1176,8 +1176,10 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
 // Tiles of the back part's GEMMs and convs at B >= 16 (the MFMA-bound shapes), one row per launch:
 // LDS-DMA tile layout (kernels.hip gemm_launch) and split-K slices. Chosen from tools/mm_bench.hip
 // (each launch alone on the chip, B = 32) and A/B runs of the pipelined step, where the back part
-// shares every CU with the latency-bound front part. Below B = 16 every GEMM runs on
-// the 32x32 register tile (layout 0) with the split-K noted at the launch.
+// shares every CU with the latency-bound front part. Pipelined split-K at most 2
+// since round 5 (the front part bounds the step, and 4 slices' slab traffic slowed it: 0.549 ->
+// 0.530 ms, profiles/r05/back_splits_ab.txt). Below B = 16 every GEMM runs on the 32x32 register
+// tile (layout 0) with the split-K noted at the launch.
 struct BackTile {
   int layout, splits;
 };
@@ -1187,11 +1189,11 @@ static BackTile back_tile(const std::string& op, bool pipeline) {
     BackTile seq, pipe;
   } table[] = {
       {"mimi.qkv", {32, 1}, {32, 1}},
-      {"mimi.out", {32, 4}, {32, 4}},
+      {"mimi.out", {32, 4}, {32, 2}},
       {"mimi.ff1", {32, 1}, {32, 1}},
-      {"mimi.ff2", {32, 4}, {32, 4}},
-      {"seanet.conv0", {32, 4}, {32, 4}},
-      {"seanet.up0.convtr", {32, 4}, {32, 4}},
+      {"mimi.ff2", {32, 4}, {32, 2}},
+      {"seanet.conv0", {32, 4}, {32, 2}},
+      {"seanet.up0.convtr", {32, 4}, {32, 2}},
       {"seanet.up1.convtr", {32, 1}, {32, 1}},
       {"seanet.up2.convtr", {32, 1}, {32, 1}},
       // the stage-0/1 residual convs when not fused (see resblock_fused)

@@ -270,9 +270,11 @@ class Engine {
   int* h_err_ = nullptr;  // copy of herr_ made at the end of every front graph
   // probe builds (PTTS_STAMPS=path): realtime stamps at the start / end of every part graph,
   // written to the file at destruction (tools/stamps.py)
+#ifdef PTTS_PROBES
   unsigned long long* stamp_ring_ = nullptr;
   unsigned* stamp_ctr_ = nullptr;
   std::vector<std::string> stamp_names_[2];  // op names of the stamped graphs (PTTS_STAMP_OPS)
+#endif
   int head_resident_ = 0;  // k_flow_head workgroups that can be co-resident on this device
   int *h_slots_ = nullptr, *h_fp_ = nullptr, *h_ids_ = nullptr, *h_tab_ = nullptr;  // admission staging
   SlotState* h_st_ = nullptr;
