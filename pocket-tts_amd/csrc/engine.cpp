@@ -145,6 +145,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
     eos_out_[q] = meta_[q] + (size_t)B * (LDIM + 2);
     pcm_[q] = dalloc((size_t)B * FRAME);
   }
+  fin_side_ = dalloc((size_t)B * (2 * FRAME / RESBLOCK_FIN_TT) * 2);  // fused final conv's boundary shares
   PTTS_HIP(hipHostMalloc((void**)&h_act_, sizeof(SlotState) * B, hipHostMallocDefault));
   // back part's own split-K slabs: up to 8 slices of the Mimi / conv0 rows (B * 16 x 512), 4 of the
   // stage-0 transposed conv (B * 16 x 6 * 256), per frame of a pass
@@ -1379,6 +1380,8 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   }
   const float* cin_buf = a0_;
   int T = 16 * nfr, ch = 512;
+  float* pcm_out = nfr == 1 ? pcm_[hb] : pcmp_[hb / 2];  // a pair's PCM is [B][2][1920]
+  bool fin_fused = false;  // the final conv ran in the stage-2 residual block's epilogue
   for (int i = 0; i < 3; ++i) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
@@ -1410,12 +1413,22 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     int fused_stages = 4;
     if (probe_env("PTTS_RESBLOCK_STAGES")) fused_stages = atoi(probe_env("PTTS_RESBLOCK_STAGES"));
     if (big && (fused_stages >> i & 1) && back_mfma_ == PTTS_BACK_F32) {  // (f32 only: its own MFMA loop)
-      const ResBlockArgs rb{ce_[i], hist_[2 + 2 * i], cb_[i], W(L_.dra_w[i]), W(L_.dra_b[i]), W(L_.drb_w[i]),
-                            W(L_.drb_b[i]), ca_[i], B, T, ch};
+      ResBlockArgs rb{ce_[i], hist_[2 + 2 * i], cb_[i], W(L_.dra_w[i]), W(L_.dra_b[i]), W(L_.drb_w[i]),
+                      W(L_.drb_b[i]), ca_[i], B, T, ch};
       const double hd = ch / 2;
-      ops.push_back({p + ".resblock", [rb](hipStream_t s) { resblock(rb, s); },
-                     2.0 * B * T * (hd * 3 * ch + ch * hd),
-                     4.0 * ((double)B * T * ch * 3 + B * 2.0 * ch + hd * 3 * ch + ch * hd + hd + ch)});
+      double fl = 2.0 * B * T * (hd * 3 * ch + ch * hd);
+      double by = 4.0 * ((double)B * T * ch * 3 + B * 2.0 * ch + hd * 3 * ch + ch * hd + hd + ch);
+      if (i == 2 && T % RESBLOCK_FIN_TT == 0) {  // + the final conv (64 -> 1, k = 3) of the tile's rows
+        rb.fw = W(L_.dfin_w);
+        rb.fb = W(L_.dfin_b);
+        rb.fH = hist_[7];
+        rb.fout = pcm_out;
+        rb.fside = fin_side_;
+        fin_fused = true;
+        fl += 2.0 * B * T * 3 * 64;
+        by += 4.0 * ((double)B * T + B * 2.0 * 64 + 3 * 64 + 1);
+      }
+      ops.push_back({p + ".resblock", [rb](hipStream_t s) { resblock(rb, s); }, fl, by});
     } else {  // the two convs (few rows: 32x32 tiles, more workgroups than the fused tiles)
       const int lr3 = big ? tile(p + ".res_conv3", 1).layout : 0, lr1 = big ? tile(p + ".res_conv1", 1).layout : 0;
       conv_op(ops, p + ".res_conv3", ce_[i], B, T, ch, hist_[2 + 2 * i], 2, 1, 0, W(L_.dra_w[i]), ch / 2, 3, 1,
@@ -1425,9 +1438,9 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     }
     cin_buf = ca_[i];
   }
-  {
+  if (!fin_fused) {
     const float *X = ca_[2], *H = hist_[7], *w = W(L_.dfin_w), *b = W(L_.dfin_b);
-    float* Y = nfr == 1 ? pcm_[hb] : pcmp_[hb / 2];  // a pair's PCM is [B][2][1920]
+    float* Y = pcm_out;
     const int TF = FRAME * nfr;
     ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, TF, 64, 3, w, b, Y, 0, s); },
                    2.0 * B * TF * 3 * 64, 4.0 * ((double)B * TF * 64 + B * 2.0 * 64 + B * TF + 3 * 64 + 1)});
@@ -1445,6 +1458,11 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     c.mpos = mpos_;
     c.qcur = qcur_;
     c.qprev = qprev_;
+    if (fin_fused) {
+      c.fin_pcm = pcm_out;
+      c.fin_side = fin_side_;
+      c.fin_T = FRAME * nfr;
+    }
     double hb_bytes = 0;  // every history row is read from its activation and stored
     for (int i = 0; i < 8; ++i) hb_bytes += 8.0 * B * hist_P_[i] * hist_C_[i];
     ops.push_back({"commit", [c](hipStream_t s) { step_commit(c, s); }, 0.0, hb_bytes + 16.0 * B});

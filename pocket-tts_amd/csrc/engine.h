@@ -220,6 +220,7 @@ class Engine {
   // frame-pair mode: PCM of one pair [B][2][1920] per pair parity, and its pinned host copy
   float* pcmp_[NHB / 2] = {};
   float* h_pcmp_[NHB / 2] = {};
+  float* fin_side_ = nullptr;  // [slot][2 * FRAME / 128][2]: the fused final conv's tile-boundary shares
   // rows admitted at an odd call under frame pairs start one call later: their SlotState (active)
   // is written right before the next front part (pinned staging)
   SlotState* h_act_ = nullptr;

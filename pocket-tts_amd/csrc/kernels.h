@@ -394,6 +394,11 @@ struct CommitArgs {
   int* mpos;  // Mimi decoder positions, += 16 per committed frame
   const float* qcur;  // the pass's quantizer outputs [B][2][512] (quant_upsample)
   float* qprev;       // overlap-add history [B][512] <- qcur[b][last valid frame]
+  // the fused final conv's tile-boundary shares (ResBlockArgs::fside): pcm[b][x * 128 + k] +=
+  // fin_side[b][x][k], k < 2, for tiles x = 1 .. fin_T / 128 - 1 (fin_side == nullptr: none)
+  float* fin_pcm = nullptr;
+  const float* fin_side = nullptr;
+  int fin_T = 0;
 };
 void step_commit(const CommitArgs& a, hipStream_t s);
 
@@ -448,7 +453,15 @@ struct ResBlockArgs {
   const float *E, *HE, *R, *W3, *b3, *W1, *b1;
   float* Y;
   int B, T, C;
+  // stage 2 only (C == 64), optional: the final conv (64 -> 1, k = 3, seanet.rs:396-402) of the
+  // tile's own rows in the epilogue, into fout [B][T]. A tile's first two outputs also need the
+  // previous tile's last two rows: the tile stores its part of them, and its own two-row share of
+  // the next tile's (fside [B][T / 128][2]) is added by the commit (CommitArgs::fin_*). The
+  // utterance's first tile reads the conv history fH [B][2][64] instead.
+  const float *fw = nullptr, *fb = nullptr, *fH = nullptr;
+  float *fout = nullptr, *fside = nullptr;
 };
+constexpr int RESBLOCK_FIN_TT = 128;  // stage-2 time tile (the side buffer's granularity)
 void resblock(const ResBlockArgs& a, hipStream_t s);
 
 // Encoder first conv (Cin == 1): Y[b][t][co] = bias[co] + sum_j w[co][j] * xpad[t + j], with

@@ -3378,6 +3378,11 @@ void quant_upsample(const float* const latent[2], const FrameFlags* const fl[2],
 // workgroup per (history, row) took two rounds of scalar copies).
 __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
   const int b = blockIdx.x;
+  if (a.fin_side) {  // every row (as the final conv computes every row): tile-boundary shares
+    const int nx = a.fin_T / RESBLOCK_FIN_TT;
+    for (int e = 2 + threadIdx.x; e < 2 * nx; e += 256)
+      a.fin_pcm[(long)b * a.fin_T + (e >> 1) * RESBLOCK_FIN_TT + (e & 1)] += a.fin_side[(long)b * 2 * nx + e];
+  }
   const int nv = !a.flags[b].valid ? 0 : (a.nfr > 1 && a.flags1[b].valid ? 2 : 1);  // valid frames: a prefix
   if (nv == 0) return;
   for (int i = 0; i < a.nh; ++i) {
@@ -3687,8 +3692,55 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) rv[g] = a.R[base + (long)(32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h) * C];
 #pragma unroll
-    for (int g = 0; g < 16; ++g)
-      a.Y[base + (long)(32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h) * C] = elu1(acc[g] + bias + rv[g]);
+    for (int g = 0; g < 16; ++g) {
+      const int row = 32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h;
+      const float y = elu1(acc[g] + bias + rv[g]);
+      a.Y[base + (long)row * C] = y;
+      if (C == 64 && a.fw) sE[row * LDE + col] = y;  // (sE is free: GEMM 1 is behind the barrier)
+    }
+  }
+  if constexpr (C == 64) {
+    if (!a.fw) return;  // uniform
+    // ---- final conv (64 -> 1, k = 3) of this tile: out[t] = b + d0[t-2] + d1[t-1] + d2[t],
+    // d_j[r] = w[j] . Y[r]. Rows -2, -1 (the utterance's first tile only) are the conv history.
+    static_assert(TT == RESBLOCK_FIN_TT, "the side buffer is laid out for 128-row tiles");
+    float* sD = sV;  // [3][TT + 2] (row r at index r + 2); sV is free once GEMM 2 is done
+    __syncthreads();
+    for (int e = tid; e < 2 * (TT + 2); e += 256) {
+      const int r = e / 2 - 2, half = e & 1;  // two threads per row (adjacent lanes), 32 channels each
+      const bool live = r >= 0 || t0 == 0;
+      const float* yr = r >= 0 ? sE + r * LDE + 32 * half : a.fH + ((long)b * 2 + (live ? r + 2 : 0)) * 64 + 32 * half;
+      float d[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 y = *reinterpret_cast<const float4*>(yr + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const float4 w = *reinterpret_cast<const float4*>(a.fw + j * 64 + 32 * half + 4 * q);
+          d[j] += (y.x * w.x + y.y * w.y) + (y.z * w.z + y.w * w.w);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        d[j] += __shfl_xor(d[j], 1, 64);
+        if (half == 0) sD[j * (TT + 2) + r + 2] = live ? d[j] : 0.f;
+      }
+    }
+    __syncthreads();
+    const float fb = a.fb[0];
+    const int nx = a.T / TT, x = blockIdx.x;
+    if (tid < TT) {
+      const int r = tid;
+      const float d0 = sD[r], d1 = sD[(TT + 2) + r + 1], d2 = sD[2 * (TT + 2) + r + 2];
+      // rows 0, 1 of a later tile: the terms from this tile's rows only (the rest via the side buffer)
+      const float v = r >= 2 || t0 == 0 ? ((d0 + d1) + d2) + fb : (r == 0 ? d2 : d1 + d2) + fb;
+      a.fout[(long)b * a.T + t0 + r] = v;
+    } else if (tid < TT + 2 && x + 1 < nx) {  // this tile's share of the next tile's rows 0, 1
+      const int k = tid - TT;
+      const float v = k == 0 ? sD[TT] + sD[(TT + 2) + TT + 1]  // d0[TT-2] + d1[TT-1]
+                             : sD[TT + 1];                     // d0[TT-1]
+      a.fside[((long)b * nx + x + 1) * 2 + k] = v;
+    }
   }
 }
 
@@ -3700,7 +3752,7 @@ void resblock(const ResBlockArgs& a, hipStream_t s) {
   else if (a.C == 128 && a.T % 96 == 0)
     hipLaunchKernelGGL((k_resblock<128, 64, 96>), dim3(a.T / 96, a.B), dim3(256),
                        cap_lds(k_resblock<128, 64, 96>, g_wg_cap), s, a);
-  else if (a.C == 64 && a.T % 128 == 0)
+  else if (a.C == 64 && a.T % 128 == 0 && (!a.fw || (a.fb && a.fH && a.fout && a.fside)))
     hipLaunchKernelGGL((k_resblock<64, 32, 128>), dim3(a.T / 128, a.B), dim3(256),
                        cap_lds(k_resblock<64, 32, 128>, g_wg_cap), s, a);
   else
