@@ -1382,6 +1382,19 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   int T = 16 * nfr, ch = 512;
   float* pcm_out = nfr == 1 ? pcm_[hb] : pcmp_[hb / 2];  // a pair's PCM is [B][2][1920]
   bool fin_fused = false;  // the final conv ran in the stage-2 residual block's epilogue
+  // fused residual blocks (k3 conv + ELU + k1 conv + skip + ELU, the hidden rows in LDS) where they
+  // beat the two conv launches: stage 2 (480 workgroups; 22.5 us against 16.8 + 11.0). Stages
+  // 0 and 1 have 96 / 160 workgroups of it and measured slower than their two tuned launches.
+  // PTTS_RESBLOCK_STAGES (probe builds): bit mask of the stages that fuse.
+#ifdef PTTS_RESBLOCK_DEFAULT
+  int fused_stages = PTTS_RESBLOCK_DEFAULT;
+#else
+  int fused_stages = 4;
+#endif
+  if (probe_env("PTTS_RESBLOCK_STAGES")) fused_stages = atoi(probe_env("PTTS_RESBLOCK_STAGES"));
+  // (f32 only: its own MFMA loop). A fused stage's (unsplit) transposed conv stores no ELU'd copy:
+  // the block ELUs the raw rows as they enter LDS
+  auto fuse_res = [&](int i) { return big && (fused_stages >> i & 1) && back_mfma_ == PTTS_BACK_F32; };
   for (int i = 0; i < 3; ++i) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
@@ -1401,20 +1414,19 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
       rr.ldy = r * (ch / 2);
       ops.push_back(rr_op(p + ".convtr_reduce", rr));
     } else {
+      // stage 2 fused below: no ELU'd copy (the residual block ELUs the raw rows as it loads them)
       conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1 + 2 * i], 1, 1, 0, W(L_.dtr_w[i]), r * (ch / 2), 2, 1,
-              trb_[i], nullptr, cb_[i], T, 1, tt.layout, 0, ce_[i]);
+              trb_[i], nullptr, cb_[i], T, 1, tt.layout, 0, fuse_res(i) ? nullptr : ce_[i]);
     }
     T *= r;
     ch /= 2;
-    // fused residual block (k3 conv + ELU + k1 conv + skip + ELU, the hidden rows in LDS) where it
-    // beats the two conv launches: stage 2 (480 workgroups; 22.5 us against 16.8 + 11.0). Stages
-    // 0 and 1 have 96 / 160 workgroups of it and measured slower than their two tuned launches.
-    // PTTS_RESBLOCK_STAGES (probe builds): bit mask of the stages that fuse.
-    int fused_stages = 4;
-    if (probe_env("PTTS_RESBLOCK_STAGES")) fused_stages = atoi(probe_env("PTTS_RESBLOCK_STAGES"));
-    if (big && (fused_stages >> i & 1) && back_mfma_ == PTTS_BACK_F32) {  // (f32 only: its own MFMA loop)
+    if (fuse_res(i)) {
       ResBlockArgs rb{ce_[i], hist_[2 + 2 * i], cb_[i], W(L_.dra_w[i]), W(L_.dra_b[i]), W(L_.drb_w[i]),
                       W(L_.drb_b[i]), ca_[i], B, T, ch};
+      if (i > 0) {  // E = elu(R) as the rows enter LDS (stage 0's split-K reduce stores both)
+        rb.E = cb_[i];
+        rb.e_raw = 1;
+      }
       const double hd = ch / 2;
       double fl = 2.0 * B * T * (hd * 3 * ch + ch * hd);
       double by = 4.0 * ((double)B * T * ch * 3 + B * 2.0 * ch + hd * 3 * ch + ch * hd + hd + ch);
@@ -1450,6 +1462,8 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     CommitArgs c{};
     const float* srcs[8] = {mx_, a0_, ce_[0], ca_[0], ce_[1], ca_[1], ce_[2], ca_[2]};
     for (int i = 0; i < 8; ++i) c.h[i] = HistDesc{srcs[i], hist_[i], hist_T_[i] * nfr, hist_C_[i], hist_P_[i]};
+    for (int i = 1; i < 3; ++i)  // a fused stage's k3-conv history: elu(raw rows)
+      if (fuse_res(i)) c.h[2 + 2 * i] = HistDesc{cb_[i], hist_[2 + 2 * i], hist_T_[2 + 2 * i] * nfr, hist_C_[2 + 2 * i], hist_P_[2 + 2 * i], 1};
     c.nh = 8;
     c.B = B;
     c.flags = flags_[hb];

@@ -383,6 +383,7 @@ struct HistDesc {
   const float* src;  // [B][T][C]
   float* dst;        // [B][P][C]
   int T, C, P;
+  int elu = 0;  // dst = elu(src): the history of an ELU'd activation kept only raw (ResBlockArgs::e_raw)
 };
 struct CommitArgs {
   HistDesc h[10];
@@ -460,6 +461,9 @@ struct ResBlockArgs {
   // utterance's first tile reads the conv history fH [B][2][64] instead.
   const float *fw = nullptr, *fb = nullptr, *fH = nullptr;
   float *fout = nullptr, *fside = nullptr;
+  // E == R (the raw transposed-conv output): the k3 conv's input is elu(R), applied as the rows
+  // enter LDS, so the transposed conv stores no ELU'd copy (HE stays ELU'd: the commit ELUs it)
+  int e_raw = 0;
 };
 constexpr int RESBLOCK_FIN_TT = 128;  // stage-2 time tile (the side buffer's granularity)
 void resblock(const ResBlockArgs& a, hipStream_t s);

@@ -3391,7 +3391,14 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
     const int tv = hd.T / a.nfr * nv;  // rows through the last valid frame
     const float4* src = reinterpret_cast<const float4*>(hd.src + ((long)b * hd.T + (tv - hd.P)) * hd.C);
     float4* dst = reinterpret_cast<float4*>(hd.dst + (long)b * hd.P * hd.C);
-    for (long e = threadIdx.x; e < n4; e += 256) dst[e] = src[e];
+    if (hd.elu) {
+      for (long e = threadIdx.x; e < n4; e += 256) {
+        const float4 v = src[e];
+        dst[e] = make_float4(elu1(v.x), elu1(v.y), elu1(v.z), elu1(v.w));
+      }
+    } else {
+      for (long e = threadIdx.x; e < n4; e += 256) dst[e] = src[e];
+    }
   }
   // the overlap-add history of the next pass: the last valid frame's quantizer output
   if (threadIdx.x < 128)
@@ -3611,7 +3618,9 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
     const int row = e / C4, c4 = e - row * C4;
     const int t = t0 - 2 + row;
     const float* src = t >= 0 ? a.E + ((long)b * a.T + t) * C : a.HE + ((long)b * 2 + (t + 2)) * C;
-    *reinterpret_cast<float4*>(sE + row * LDE + 4 * c4) = *reinterpret_cast<const float4*>(src + 4 * c4);
+    float4 v = *reinterpret_cast<const float4*>(src + 4 * c4);
+    if (a.e_raw && t >= 0) v = make_float4(elu1(v.x), elu1(v.y), elu1(v.z), elu1(v.w));
+    *reinterpret_cast<float4*>(sE + row * LDE + 4 * c4) = v;
   }
   __syncthreads();
   // ---- GEMM 1: v[TT][H] = E3[TT][3C] . W3[H][3C]^T, k = tap * C + c reads sE[i + tap][c]
