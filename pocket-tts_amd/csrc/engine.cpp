@@ -1423,13 +1423,14 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     if (fuse_res(i)) {
       ResBlockArgs rb{ce_[i], hist_[2 + 2 * i], cb_[i], W(L_.dra_w[i]), W(L_.dra_b[i]), W(L_.drb_w[i]),
                       W(L_.drb_b[i]), ca_[i], B, T, ch};
-      if (i > 0) {  // E = elu(R) as the rows enter LDS (stage 0's split-K reduce stores both)
-        rb.E = cb_[i];
-        rb.e_raw = 1;
-      }
       const double hd = ch / 2;
       double fl = 2.0 * B * T * (hd * 3 * ch + ch * hd);
       double by = 4.0 * ((double)B * T * ch * 3 + B * 2.0 * ch + hd * 3 * ch + ch * hd + hd + ch);
+      if (i > 0) {  // E = elu(R) as the rows enter LDS (stage 0's split-K reduce stores both)
+        rb.E = cb_[i];
+        rb.e_raw = 1;
+        by -= 4.0 * B * T * ch;  // E and R are the same rows: read once
+      }
       if (i == 2 && T % RESBLOCK_FIN_TT == 0) {  // + the final conv (64 -> 1, k = 3) of the tile's rows
         rb.fw = W(L_.dfin_w);
         rb.fb = W(L_.dfin_b);
