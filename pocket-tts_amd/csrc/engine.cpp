@@ -41,6 +41,9 @@ int pick_splits(int M, int N, int K) {
 // PTTS_OVR="name=L[:S],...", read at every plan build.
 static void tile_override(const std::string& name, int& layout, int& ksplit) {
   const char* e = probe_env("PTTS_OVR");
+#ifdef PTTS_OVR_BUILTIN  // A/B variant libraries (tools/ab.sh): the override compiled in
+  if (!e) e = PTTS_OVR_BUILTIN;
+#endif
   if (!e) return;
   const std::string s(e);
   size_t p = 0;
