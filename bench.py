@@ -87,6 +87,41 @@ def measured_in_step_all():
     return {r["op"]: float(r["rocprof_avg_us"]) for r in csv.DictReader(open(path)) if r["rocprof_avg_us"]}
 
 
+def kernel_aggregates(top=3):
+    """Per kernel (template instance) over the committed in-step trace (profiles/op_stats.csv): its
+    total time per step pass (sum over its ops of in-step average x launches) and its algorithmic
+    flops / bytes over the same launches, ranked by total time. The first entry is the kernel that
+    dominates the GPU time of the measured step; its fraction is its total work over its total
+    time against the peak of its bound (MFMA for flop-heavy kernels, HBM otherwise)."""
+    path = ROOT / "profiles" / "op_stats.csv"
+    if not path.exists():
+        return None
+    import csv
+    agg = {}
+    for r in csv.DictReader(open(path)):
+        if not r["rocprof_avg_us"]:
+            continue
+        a = agg.setdefault(r["kernel"], {"us": 0.0, "flops": 0.0, "bytes": 0.0, "launches": 0, "ops": []})
+        n = int(r["calls"])
+        a["us"] += float(r["rocprof_avg_us"]) * n
+        a["flops"] += float(r["flops"] or 0) * n
+        a["bytes"] += float(r["bytes"] or 0) * n
+        a["launches"] += n
+        a["ops"].append(r["op"])
+    total = sum(a["us"] for a in agg.values())
+    ridge = F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    out = []
+    for k, a in sorted(agg.items(), key=lambda kv: -kv[1]["us"])[:top]:
+        mfma = a["bytes"] == 0 or a["flops"] / a["bytes"] >= ridge
+        ach = a["flops"] / (a["us"] * 1e-6) / 1e12 if mfma else a["bytes"] / (a["us"] * 1e-6) / 1e9
+        peak = F32_PEAK_TFLOPS if mfma else HBM_PEAK_GBS
+        out.append({"kernel": k, "share_of_gpu_time": round(a["us"] / total, 4), "launches": a["launches"],
+                    "avg_us": round(a["us"] / a["launches"], 2), "bound": "mfma" if mfma else "hbm",
+                    "achieved": round(ach, 2), "unit": "TFLOP/s" if mfma else "GB/s", "peak": peak,
+                    "frac": round(ach / peak, 4), "ops": sorted(set(a["ops"]))})
+    return out
+
+
 def front_bytes(B, K, distinct_voices=1):
     """Algorithmic HBM bytes of one front part (FlowLM step): the f32 step weights once
     (84,527,137 floats) plus the KV the six layers read (49,152 B per cached position = 6 layers x
@@ -381,7 +416,7 @@ def main():
     ap.add_argument("--no-quant-variant", action="store_true",
                     help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM), fp8_gemm and "
                          "back_bf16 engines")
-    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2),
+    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2, 4),
                     help="frames per Mimi-decode pass of pipelined stepping (ptts_engine_config.back_frames; "
                          "2, the throughput configuration: 0.559 vs 0.584 ms per steady step, DESIGN.md section 1)")
     ap.add_argument("--back-mfma", choices=("f32", "f32x6"), default="f32",
@@ -537,20 +572,51 @@ def main():
         return elapsed, admit_s, job_s
 
     def pcm_sample(e, n_frames=24):
-        """Every row's PCM of n_frames frames at temp 0 (no EOS) from the bench's voice and texts:
-        [rows][frames][1920] (the bf16 variant's accuracy against this engine's f32 PCM)."""
+        """Every row's PCM, latents and EOS logits of n_frames frames at temp 0 (no EOS) from the
+        bench's voice and texts: ([rows][frames][1920], [rows][frames][32], [rows][frames]) (the
+        reduced-precision variants' accuracy against this engine's f32 outputs)."""
         voice = e.voice_from_prompt(synth_prompt())
         e.open_many(list(range(B)), [voice] * B, [text_ids(b) for b in range(B)],
                     [pt.GenerationParams(temp=0.0, eos_threshold=float("inf"), max_frames=n_frames, seed=b + 1)
                      for b in range(B)])
-        out = [[] for _ in range(B)]
+        out, lat, eos = [[] for _ in range(B)], [[] for _ in range(B)], [[] for _ in range(B)]
         for _ in range(n_frames + sum(e.frame_lag())):
             r = e.step(B)
             for b in range(B):
                 if r.valid[b]:
                     out[b].append(r.pcm[b].copy())
+                    lat[b].append(r.latents[b].copy())
+                    eos[b].append(float(r.eos_logits[b]))
         assert all(len(o) == n_frames for o in out)
-        return np.asarray(out, np.float64)
+        return np.asarray(out, np.float64), np.asarray(lat, np.float64), np.asarray(eos, np.float64)
+
+    def snr_rows(ref, x):
+        """Per-row SNR (dB) of x against ref over all frames and channels of the row."""
+        err = ((x - ref) ** 2).reshape(ref.shape[0], -1).sum(-1)
+        return 10 * np.log10((ref ** 2).reshape(ref.shape[0], -1).sum(-1) / np.maximum(err, 1e-30))
+
+    def accuracy_vs_f32(sample, ref):
+        """A variant's accuracy against the f32 engine on the same 24-frame temp-0 sample: latent and
+        PCM SNR (per row: min / median), EOS-logit error, and stop-frame agreement — per row, for
+        thresholds at the f32 run's EOS-logit quartiles, the first frame above each (the reference's
+        stop rule, tts_model.rs:1055-1063) on both engines (tests/test_fp8.py's measure)."""
+        pcm, lat, eos = sample
+        rpcm, rlat, reos = ref
+        ls, ps = snr_rows(rlat, lat), snr_rows(rpcm, pcm)
+        diffs = []
+        for b in range(reos.shape[0]):
+            for thr in np.quantile(reos[b], [0.25, 0.5, 0.75]):
+                def stop(tr):
+                    above = np.nonzero(tr > thr)[0]
+                    return int(above[0]) if above.size else tr.size
+                diffs.append(abs(stop(reos[b]) - stop(eos[b])))
+        diffs = np.asarray(diffs)
+        return {"latent_snr_db": {"min": round(float(ls.min()), 2), "median": round(float(np.median(ls)), 2)},
+                "pcm_snr_db": {"min": round(float(ps.min()), 2), "median": round(float(np.median(ps)), 2)},
+                "eos_logit_abs_err_max": round(float(np.abs(eos - reos).max()), 4),
+                "stop_frame_same": round(float(np.mean(diffs == 0)), 3),
+                "stop_frame_within_1": round(float(np.mean(diffs <= 1)), 3),
+                "sample": f"{B} rows x {rpcm.shape[1]} frames, temp 0, bench voice and texts, against the f32 engine"}
 
     elapsed, admit_s, job_s = timed_job(eng)
     steps = jobs * K
@@ -587,7 +653,7 @@ def main():
     # large FlowLM step GEMMs as fp8 W8A8 (accuracy-gated against the f32 oracle, tests/test_fp8.py).
     # Reported beside `value`, never as it (different numerics from the f32 reference).
     quant = fp8 = bf16 = None
-    ref_pcm = pcm_sample(eng) if not args.no_quant_variant and world == 1 and not selftest else None
+    ref_sample = pcm_sample(eng) if not args.no_quant_variant and world == 1 and not selftest else None
     # the same job with B distinct voices: every row reads its own 125-frame prefix (6 MB of KV)
     # instead of the bench's one shared voice; the headline's shared-prefix benefit, made visible
     distinct = None
@@ -619,7 +685,17 @@ def main():
             us = eng.time_kernel(B, name, reps=20)
             per_op.append((us, name, fl, by))
         per_op.sort(reverse=True)
-        us, name, fl, by = per_op[0]
+        # the dominant op is the LONGEST IN-STEP launch of the measured configuration (committed
+        # kernel trace of this bench, profiles/op_stats.csv), where front and back share every CU;
+        # the ops' isolated HIP-event times rank differently (in-step inflation differs per op).
+        # Without a trace covering the plan, the longest isolated op stands in.
+        ins = measured_in_step_all()
+        alone = {n: (u, fl_, by_) for u, n, fl_, by_ in per_op}
+        if ins and all(n in ins for n in alone):
+            name = max(alone, key=lambda n: ins[n])
+        else:
+            name = per_op[0][1]
+        us, fl, by = alone[name]
         intensity = fl / by if by else 0.0
         ridge = F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
         if by and intensity < ridge:
@@ -651,7 +727,15 @@ def main():
                                        "--kernel-trace of bench.py, tools/prof_ops.py piped)")
         roof["algorithmic_bytes"] = by
         roof["algorithmic_flops"] = fl
-        top = [{"op": n, "avg_us": round(u, 2)} for u, n, _, _ in per_op[:8]]
+        roof["kernel_aggregate"] = kernel_aggregates()
+        # top_ops: the step's longest launches IN STEP (what the step pays for), each with its
+        # isolated time and the in-step / alone inflation
+        if ins and all(n in ins for n in alone):
+            ranked = sorted(alone, key=lambda n: -ins[n])[:8]
+            top = [{"op": n, "avg_us_in_step": round(ins[n], 2), "avg_us_alone": round(alone[n][0], 2),
+                    "inflation": round(ins[n] / alone[n][0], 3)} for n in ranked]
+        else:
+            top = [{"op": n, "avg_us_alone": round(u, 2)} for u, n, _, _ in per_op[:8]]
         sum_ops_ms = round(sum(u for u, _, _, _ in per_op) / 1000.0, 3)
         roof["phases"] = phase_rooflines(per_op, plan, B, K, back_frames)
         roof["step"] = step_roofline(plan, B, K, back_frames, 1e6 * (elapsed - admit_s) / steps)
@@ -669,29 +753,35 @@ def main():
         eq = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                        pipeline=pipeline, back_frames=back_frames, weight_quant=pt.QUANT_FLOW_LM)
         q_el, q_ad, _ = timed_job(eq)
+        q_acc = accuracy_vs_f32(pcm_sample(eq), ref_sample)
         quant = {"value": round(jobs * B * K * 1920 / 24000.0 / q_el, 2), "unit": "audio-sec/wall-sec",
                  "ms_per_step": round(1000.0 * q_el / steps, 4),
                  "steady_ms_per_step": round(1000.0 * (q_el - q_ad) / steps, 4),
-                 "weight_quant": "flow_lm int8 (quantize.rs QuantizeConfig::default, per-tensor symmetric)",
-                 "int8_matrices": eq.int8_matrices}
+                 "weight_quant": "flow_lm int8 (quantize.rs QuantizeConfig::default, per-tensor symmetric; equals "
+                                 "the quantized oracle at the f32 gates, tests/test_quantize.py)",
+                 "int8_matrices": eq.int8_matrices, "accuracy_vs_f32": q_acc}
         eq.close()
         ef = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                        pipeline=pipeline, back_frames=back_frames, fp8_gemm=True)
         f_el, f_ad, _ = timed_job(ef)
+        f_acc = accuracy_vs_f32(pcm_sample(ef), ref_sample)
         fp8 = {"value": round(jobs * B * K * 1920 / 24000.0 / f_el, 2), "unit": "audio-sec/wall-sec",
                "ms_per_step": round(1000.0 * f_el / steps, 4),
                "steady_ms_per_step": round(1000.0 * (f_el - f_ad) / steps, 4),
                "gemm": "fp8 e4m3 W8A8 on v_mfma_f32_32x32x16_fp8_fp8 (row-scaled weights, per-slice "
                        "activation scales), FlowLM qkv/linear1/linear2/adaLN",
-               "fp8_matrices": ef.fp8_matrices}
+               "numerics": f"reduced precision, NOT the reference's: latent SNR "
+                           f"{f_acc['latent_snr_db']['min']:.1f} dB (worst row) against f32",
+               "fp8_matrices": ef.fp8_matrices, "accuracy_vs_f32": f_acc}
         ef.close()
         # the Mimi decode (back part) on bf16 MFMA: the same job, and its PCM against the f32
         # engine's (= the f32 oracle within 1e-7, tests/test_gpu_bench_shape.py) on a 24-frame sample
         eb = pt.Engine(device=local_rank, max_slots=B, max_ctx=max_ctx, lsd_decode_steps=1, seed=0x5EED,
                        pipeline=pipeline, back_frames=back_frames, back_bf16=True)
         b_el, b_ad, _ = timed_job(eb)
-        bp = pcm_sample(eb)
+        bp = pcm_sample(eb)[0]
         eb.close()
+        ref_pcm = ref_sample[0]
         err = ((bp - ref_pcm) ** 2).sum(-1)
         snr = 10 * np.log10((ref_pcm ** 2).sum(-1) / np.maximum(err, 1e-30))
         bf16 = {"value": round(jobs * B * K * 1920 / 24000.0 / b_el, 2), "unit": "audio-sec/wall-sec",
@@ -756,8 +846,8 @@ def main():
                                "(BASELINE configs[2])",
                    "global_batch": B * world, "utterance_frames": K, "jobs": jobs, "prompt_frames": PROMPT_FRAMES,
                    "text_tokens": TEXT_TOKENS, "temp": 0.7, "parallelism": f"replicas x{world}",
-                   "stepping": ("pipelined, frame pairs (one Mimi decode pass per two frames, overlapping "
-                                "FlowLM steps k and k+1)" if back_frames == 2 else
+                   "stepping": (f"pipelined, {back_frames} frames per Mimi decode pass (overlapping the "
+                                "FlowLM steps of the next frames)" if back_frames > 1 else
                                 "pipelined (Mimi decode of frame k overlaps FlowLM step k+1)") if pipeline
                    else "sequential",
                    "pcm_to_host": "every frame, async D2H into pinned memory inside the step graphs"},

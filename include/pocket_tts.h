@@ -89,14 +89,14 @@ typedef struct ptts_engine_config {
                                naming the key): another variant is a rebuild. Checked, not read
                                for shapes. ptts_config_check() is the same check alone. */
   int back_frames;          /* pipelined engines only: frames per Mimi-decode pass, 1 (default;
-                               0 means 1) or 2. With 2, frames 2j and 2j+1 of every row are
-                               decoded by ONE back pass (the streaming codec state advances as for
-                               two passes; PCM identical within float rounding), a call returns the
-                               frame computed three calls earlier, and rows admitted at an odd
-                               call start one call later (an utterance's frames pair up from its
-                               first). ptts_frame_lag() reports both delays. 2 is the
-                               throughput setting (bench.py's default: 0.561 against 0.583 ms per
-                               steady step at B = 32), 1 the low-latency one. */
+                               0 means 1), 2 or 4. With n > 1, frames n j .. n j + n - 1 of every
+                               row are decoded by ONE back pass (the streaming codec state advances
+                               as for n passes; PCM identical within float rounding), a call
+                               returns the frame computed 2 n - 1 calls earlier, and rows admitted
+                               inside a pass start at the next pass boundary (an utterance's frames
+                               group into passes from its first). ptts_frame_lag() reports both
+                               delays. 2 is the throughput setting (bench.py's default; 4 measured
+                               in DESIGN.md section 14), 1 the low-latency one. */
   int back_mfma;            /* PTTS_BACK_*: how the Mimi decoder transformer GEMMs and the SEANet
                                decoder convs (the back part, at >= 16 rows) use the matrix cores.
                                PTTS_BACK_F32 (0): v_mfma_f32_32x32x2_f32, an exact f32 FMA chain.
@@ -243,9 +243,10 @@ int ptts_sync(ptts_engine* e);
 int ptts_fetch(ptts_engine* e, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
                float* eos_logits, float* latents);
 /* Calls by which a frame trails the call that computed its FlowLM step: 0 (sequential), 1
- * (pipelined), 3 (pipelined, back_frames = 2). *admit_delay (may be NULL): 1 if the rows of the
- * latest admission start one call late (back_frames = 2, admitted at an odd call), else 0. A row
- * admitted before call k returns its first frame from call k + lag + admit_delay. */
+ * (pipelined), 2 n - 1 (pipelined, back_frames = n > 1). *admit_delay (may be NULL): the calls by
+ * which the rows of the latest admission start late (back_frames = n > 1, admitted at a call k with
+ * k % n != 0: n - k % n), else 0. A row admitted before call k returns its first frame from call
+ * k + lag + admit_delay. */
 int ptts_frame_lag(const ptts_engine* e, int* admit_delay);
 /* ptts_fetch of an earlier call: calls_back = 0 is the latest call (= ptts_fetch), 1 the call
  * before it. Lets a driver keep one call in flight (issue call k+1, then fetch call k) so that the

@@ -13,6 +13,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -93,11 +94,12 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_REQUIRE(cfg.fp8_gemm == 0 || cfg.fp8_gemm == 1, "fp8_gemm must be 0 or 1");
   PTTS_REQUIRE(!(cfg.fp8_gemm && cfg.weight_quant != QUANT_NONE), "fp8_gemm and weight_quant are exclusive");
   fp8_ = cfg.fp8_gemm;
-  PTTS_REQUIRE(cfg.back_frames >= 0 && cfg.back_frames <= 2, "back_frames must be 0, 1 or 2");
-  nfr_ = cfg.pipeline && cfg.back_frames == 2 ? 2 : 1;
+  PTTS_REQUIRE(cfg.back_frames >= 0 && cfg.back_frames <= NFR_MAX && cfg.back_frames != 3,
+               "back_frames must be 0, 1, 2 or 4");
+  nfr_ = cfg.pipeline && cfg.back_frames >= 2 ? cfg.back_frames : 1;
   PTTS_REQUIRE(cfg.back_mfma >= PTTS_BACK_F32 && cfg.back_mfma <= PTTS_BACK_F32X6, "unknown back_mfma mode");
   back_mfma_ = cfg.back_mfma;
-  nhb_ = nfr_ == 2 ? NHB : 3;
+  nhb_ = nfr_ > 1 ? 3 * nfr_ : 3;
   int ndev = 0;
   PTTS_HIP(hipGetDeviceCount(&ndev));
   PTTS_REQUIRE(dev_ >= 0 && dev_ < ndev, "HIP device ordinal out of range");
@@ -125,30 +127,31 @@ Engine::Engine(const ptts_engine_config& cfg) {
   lat_in_ = dalloc((size_t)B * LDIM);
   cur_ = dalloc((size_t)B * LDIM);
   // overlap-add history [slot][512] (the last committed frame's quantizer output) and the
-  // pass's quantizer outputs [slot][2][512], copied into it by the commit (quant_upsample)
-  qprev_ = dalloc((size_t)3 * B * MD);
+  // pass's quantizer outputs [slot][NFR_MAX][512], copied into it by the commit (quant_upsample)
+  qprev_ = dalloc((size_t)(1 + NFR_MAX) * B * MD);
   qcur_ = qprev_ + (size_t)B * MD;
   eos_ = dalloc(B);
   static_assert(sizeof(FrameFlags) == 2 * sizeof(float), "FrameFlags packs into two floats");
   meta_floats_ = (size_t)B * (LDIM + 1 + 2);
-  // frame pairs: pair p's PCM [B][2][1920] and the meta blocks of its buffers 2p, 2p + 1 in ONE
-  // device block and ONE pinned host block, so the pass delivers both frames with one copy node
-  // (a 128-B multiple per meta block keeps FrameFlags 8-B aligned)
+  // multi-frame passes: pass p's PCM [B][nfr][1920] and the meta blocks of its buffers nfr p ..
+  // nfr p + nfr - 1 in ONE device block and ONE pinned host block, so the pass delivers its frames
+  // with one copy node (a 128-B multiple per meta block keeps FrameFlags 8-B aligned)
   const size_t mstride = (meta_floats_ + 31) / 32 * 32;
-  if (nfr_ == 2)
-    for (int p = 0; p < NHB / 2; ++p) {
-      const size_t n = (size_t)B * 2 * FRAME + 2 * mstride;
+  if (nfr_ > 1)
+    for (int p = 0; p < nhb_ / nfr_; ++p) {
+      const size_t n = (size_t)B * nfr_ * FRAME + nfr_ * mstride;
       pcmp_[p] = dalloc(n);
       PTTS_HIP(hipHostMalloc((void**)&h_pcmp_[p], sizeof(float) * n, hipHostMallocDefault));
     }
   for (int q = 0; q < NHB; ++q) {  // front -> back hand-off buffers
-    meta_[q] = nfr_ == 2 ? pcmp_[q / 2] + (size_t)B * 2 * FRAME + (q & 1) * mstride : dalloc(meta_floats_);
+    meta_[q] = nfr_ > 1 && q < nhb_ ? pcmp_[q / nfr_] + (size_t)B * nfr_ * FRAME + (q % nfr_) * mstride
+                                    : dalloc(meta_floats_);
     lat_out_[q] = meta_[q];                                  // 128-B aligned,
     flags_[q] = (FrameFlags*)(meta_[q] + (size_t)B * LDIM);  // so FrameFlags stay 8-B aligned
     eos_out_[q] = meta_[q] + (size_t)B * (LDIM + 2);
     pcm_[q] = dalloc((size_t)B * FRAME);
   }
-  fin_side_ = dalloc((size_t)B * (2 * FRAME / RESBLOCK_FIN_TT) * 2);  // fused final conv's boundary shares
+  fin_side_ = dalloc((size_t)B * (nfr_ * FRAME / RESBLOCK_FIN_TT) * 2);  // fused final conv's boundary shares
   PTTS_HIP(hipHostMalloc((void**)&h_act_, sizeof(SlotState) * B, hipHostMallocDefault));
   // back part's own split-K slabs: up to 8 slices of the Mimi / conv0 rows (B * 16 x 512), 4 of the
   // stage-0 transposed conv (B * 16 x 6 * 256), per frame of a pass
@@ -241,8 +244,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
 
   for (int q = 0; q < NHB; ++q) {
     PTTS_HIP(hipHostMalloc((void**)&h_pcm_[q], sizeof(float) * B * FRAME, hipHostMallocDefault));
-    if (nfr_ == 2)  // inside the pair's pinned block (above)
-      h_meta_[q] = h_pcmp_[q / 2] + (size_t)B * 2 * FRAME + (q & 1) * ((meta_floats_ + 31) / 32 * 32);
+    if (nfr_ > 1 && q < nhb_)  // inside the pass's pinned block (above)
+      h_meta_[q] = h_pcmp_[q / nfr_] + (size_t)B * nfr_ * FRAME + (q % nfr_) * ((meta_floats_ + 31) / 32 * 32);
     else
       PTTS_HIP(hipHostMalloc((void**)&h_meta_[q], sizeof(float) * meta_floats_, hipHostMallocDefault));
     memset(h_meta_[q], 0, sizeof(float) * meta_floats_);
@@ -315,7 +318,7 @@ Engine::~Engine() {
   for (void* p : allocs_) (void)hipFree(p);
   for (int q = 0; q < NHB; ++q) {
     if (h_pcm_[q]) (void)hipHostFree(h_pcm_[q]);
-    if (h_meta_[q] && nfr_ != 2) (void)hipHostFree(h_meta_[q]);
+    if (h_meta_[q] && !(nfr_ > 1 && q < nhb_)) (void)hipHostFree(h_meta_[q]);
   }
   for (int p = 0; p < NHB / 2; ++p)
     if (h_pcmp_[p]) (void)hipHostFree(h_pcmp_[p]);
@@ -397,66 +400,91 @@ void Engine::derive_gemv() {
   }
   const GemvShape ada{4, 128};  // flow-head adaLN matrix: 0.6365 -> 0.6315 ms
   mats.push_back({W(L_.ada_w), NADA, FD, 16, ada});
+  // Code-carrying matrices (weight_quant: int8, fp8_gemm: e4m3) are read from their codes only
+  // (k_gemv / k_ffn_fused with WQ != 0 never touch an f32 packed copy), so they get no f32 copy.
+  auto scale_of = [&](const float* w) { return fp8_ ? f8map_.at(w).second : q8map_.at(w).second; };
   // linear1 on the whole-K GEMM (gemv_fk: GELU in its epilogue, no split-K slabs, no reduce launch)
   // wherever the register-resident linear1 is used; PTTS_NO_FK (probe builds) keeps the split-K form
   if ((mask & 4) && !probe_env("PTTS_NO_FK") && gemv_fk_supported(1, FF, D)) {
+    // linear1 + linear2 as ONE launch (ffn_fused) wherever the whole-K linear1 is used;
+    // PTTS_NO_FFN (probe builds) keeps the two launches
+    const bool ffn = !probe_env("PTTS_NO_FFN") && ffn_fused_supported(1, D, FF);
+    if (ffn) ffn_groups_ = probe_env("PTTS_FFN16") ? 16 : 8;  // probe builds: the 16-group form, for A/B runs
+    const int G = ffn_groups_;
+    // weight_quant / fp8 engines: both matrices as codes (the fused launch then streams a quarter
+    // of the bytes)
+    std::vector<std::pair<const uint32_t*, const uint32_t*>> codes(NL, {nullptr, nullptr});
+    bool all_codes = ffn;
+    for (int l = 0; l < NL && ffn; ++l) {
+      const float *w1 = W(L_.fl[l].l1), *w2 = W(L_.fl[l].l2);
+      codes[l].first = pack_codes(w1, FF, D, 8, [&](const float* c, float* o) { pack_gemv_fk(c, FF, D, o, stream_); });
+      codes[l].second = pack_codes(w2, D, FF, 8, [&](const float* c, float* o) { pack_ffn2(c, G, o, stream_); });
+      if (codes[l].first && codes[l].second) ffn8map_[w2] = {{codes[l].first, scale_of(w1)}, {codes[l].second, scale_of(w2)}};
+      else all_codes = false;
+    }
+    const bool f32_copies = !all_codes;
     void* q = nullptr;
-    PTTS_HIP(hipMalloc(&q, sizeof(float) * ((size_t)NL * FF * D + FK_A_FLOATS)));  // all written before read
+    PTTS_HIP(hipMalloc(&q, sizeof(float) * ((f32_copies ? (size_t)NL * FF * D : 0) + FK_A_FLOATS)));  // all written before read
     allocs_.push_back(q);
     float* dst = (float*)q;
     for (int l = 0; l < NL; ++l) {
-      pack_gemv_fk(W(L_.fl[l].l1), FF, D, dst, stream_);
-      fkmap_[W(L_.fl[l].l1)] = dst;
-      dst += (size_t)FF * D;
+      if (f32_copies) pack_gemv_fk(W(L_.fl[l].l1), FF, D, dst, stream_);
+      fkmap_[W(L_.fl[l].l1)] = f32_copies ? dst : nullptr;  // nullptr: the fused launch reads the codes
+      if (f32_copies) dst += (size_t)FF * D;
     }
     hfrag_ = dst;
-    // linear1 + linear2 as ONE launch (ffn_fused) wherever the whole-K linear1 is used;
-    // PTTS_NO_FFN (probe builds) keeps the two launches
-    if (!probe_env("PTTS_NO_FFN") && ffn_fused_supported(1, D, FF)) {
-      ffn_groups_ = probe_env("PTTS_FFN16") ? 16 : 8;  // probe builds: the 16-group form, for A/B runs
+    if (ffn) {
       void* f = nullptr;
-      PTTS_HIP(hipMalloc(&f, sizeof(float) * ((size_t)NL * D * FF + 2 * FFN_HAND_FLOATS)));
+      PTTS_HIP(hipMalloc(&f, sizeof(float) * ((f32_copies ? (size_t)NL * D * FF : 0) + 2 * FFN_HAND_FLOATS)));
       allocs_.push_back(f);
       float* fd = (float*)f;
       for (int l = 0; l < NL; ++l) {
-        pack_ffn2(W(L_.fl[l].l2), ffn_groups_, fd, stream_);
-        ffnmap_[W(L_.fl[l].l2)] = fd;
-        fd += (size_t)D * FF;
-        // weight_quant engines: both matrices also as int8 codes (the fused launch then streams
-        // a quarter of the bytes; the same f32 values reach the MFMAs)
-        const float *w1 = W(L_.fl[l].l1), *w2 = W(L_.fl[l].l2);
-        const int G = ffn_groups_;
-        const uint32_t* q1 = pack_codes(w1, FF, D, 8, [&](const float* c, float* o) { pack_gemv_fk(c, FF, D, o, stream_); });
-        const uint32_t* q2 = pack_codes(w2, D, FF, 8, [&](const float* c, float* o) { pack_ffn2(c, G, o, stream_); });
-        auto sc = [&](const float* w) { return fp8_ ? f8map_.at(w).second : q8map_.at(w).second; };
-        if (q1 && q2) ffn8map_[w2] = {{q1, sc(w1)}, {q2, sc(w2)}};
+        if (f32_copies) pack_ffn2(W(L_.fl[l].l2), G, fd, stream_);
+        ffnmap_[W(L_.fl[l].l2)] = f32_copies ? fd : nullptr;
+        if (f32_copies) fd += (size_t)D * FF;
       }
       ffn_hand_ = fd;  // both sets empty (0xFFFFFFFF) before the first launch
       PTTS_HIP(hipMemsetD32Async(ffn_hand_, 0xFFFFFFFFu, 2 * FFN_HAND_FLOATS, stream_));
     }
   }
+  std::vector<Gemv> sel;  // (matrix, codes) of every register-resident matrix
+  std::vector<const M*> selm;
   size_t total = 0;
-  for (const M& m : mats)
-    if ((mask & m.bit) && gemv_supported(m.g, m.N, m.K)) total += (size_t)m.N * m.K;
-  if (!total) return;
-  void* p = nullptr;
-  PTTS_HIP(hipMalloc(&p, sizeof(float) * total));  // every element is written by the packing
-  allocs_.push_back(p);
-  float* dst = (float*)p;
   for (const M& m : mats) {
     if (!(mask & m.bit) || !gemv_supported(m.g, m.N, m.K)) continue;
-    pack_gemv(m.w, m.N, m.K, m.g, dst, stream_);
-    Gemv gv{dst, m.g, m.bit, nullptr, nullptr};
+    Gemv gv{nullptr, m.g, m.bit, nullptr, nullptr};
     // weight_quant engines: the int8 codes of a quantized matrix in the same fragment order;
-    // fp8_gemm engines: the e4m3 codes of the {4, 128} matrices (qkv, adaLN; W8A8 tiles)
+    // fp8_gemm engines: the e4m3 codes of the {4, 128} matrices (qkv, adaLN; W8A8 tiles). An e4m3
+    // matrix on another tile (linear2's {1, 64}) gets no register-resident form at all: it stays on
+    // k_gemm_fp8 (W8A8), so every fp8 matrix runs fp8 in every stepping mode
     const GemvShape g = m.g;
     const int N = m.N, K = m.K;
     if (!fp8_ || (g.wn == 4 && g.kw == 128)) {
       gv.q8 = pack_codes(m.w, N, K, g.kw / 8, [&](const float* c, float* o) { pack_gemv(c, N, K, g, o, stream_); });
-      if (gv.q8) gv.scale = fp8_ ? f8map_.at(m.w).second : q8map_.at(m.w).second;
+      if (gv.q8) gv.scale = scale_of(m.w);
+    } else if (f8map_.count(m.w)) {
+      continue;
+    }
+    if (!gv.q8) total += (size_t)N * K;
+    sel.push_back(gv);
+    selm.push_back(&m);
+  }
+  float* dst = nullptr;
+  if (total) {
+    void* p = nullptr;
+    PTTS_HIP(hipMalloc(&p, sizeof(float) * total));  // every element is written by the packing
+    allocs_.push_back(p);
+    dst = (float*)p;
+  }
+  for (size_t i = 0; i < sel.size(); ++i) {
+    const M& m = *selm[i];
+    Gemv gv = sel[i];
+    if (!gv.q8) {
+      pack_gemv(m.w, m.N, m.K, m.g, dst, stream_);
+      gv.packed = dst;
+      dst += (size_t)m.N * m.K;
     }
     gvmap_[m.w] = gv;
-    dst += (size_t)m.N * m.K;
   }
   PTTS_HIP(hipGetLastError());
   PTTS_HIP(hipStreamSynchronize(stream_));
@@ -1217,7 +1245,8 @@ static BackTile back_tile(const std::string& op, bool pipeline) {
 // frame's parity for the quantizer history (the previous frame's quantizer output is in qp ^ 1).
 void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   PTTS_REQUIRE(nfr >= 1 && nfr <= nfr_, "frames per back pass out of range");
-  const int hb2 = (hb + 1) % nhb_;  // the second frame's hand-off buffer (nfr == 2)
+  int hbs[NFR_MAX];  // frame f's hand-off buffer (f < nfr)
+  for (int f = 0; f < NFR_MAX; ++f) hbs[f] = (hb + std::min(f, nfr - 1)) % nhb_;
   const bool big = B >= 16;  // B * 16 >= 256 Mimi rows: the LDS-DMA tiles fill the chip
   auto tile = [&](const std::string& op, int small_splits) {
     BackTile t = big ? back_tile(op, pipeline_) : BackTile{0, small_splits};
@@ -1236,16 +1265,14 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     const float* qin = qprev_;
     float* qout = qcur_;
     float *x = mx_, *h = mh_;
-    const float* lat0 = lat_out_[hb];
-    const float* lat1 = lat_out_[hb2];
-    const FrameFlags* fl0 = flags_[hb];
-    const FrameFlags* fl1 = flags_[hb2];
+    std::array<const float*, NFR_MAX> lat;
+    std::array<const FrameFlags*, NFR_MAX> fl;
+    for (int f = 0; f < NFR_MAX; ++f) {
+      lat[f] = lat_out_[hbs[f]];
+      fl[f] = flags_[hbs[f]];
+    }
     ops.push_back({"mimi.quant_upsample",
-                   [=](hipStream_t s) {
-                     const float* lat[2] = {lat0, lat1};
-                     const FrameFlags* fl[2] = {fl0, fl1};
-                     quant_upsample(lat, fl, nfr, B, sd, mn, wq, wu, qin, qout, x, h, lw, lb, s);
-                   },
+                   [=](hipStream_t s) { quant_upsample(lat.data(), fl.data(), nfr, B, sd, mn, wq, wu, qin, qout, x, h, lw, lb, s); },
                    (double)B * nfr * (2.0 * MD * LDIM + 2.0 * MD * 2 * UP + 8.0 * UP * MD),
                    4.0 * ((double)B * nfr * (LDIM + 2 * MD + 2.0 * UP * MD) + 2.0 * MD * LDIM + MD * 2.0 * UP + 2.0 * MD)});
   }
@@ -1383,7 +1410,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   }
   const float* cin_buf = a0_;
   int T = 16 * nfr, ch = 512;
-  float* pcm_out = nfr == 1 ? pcm_[hb] : pcmp_[hb / 2];  // a pair's PCM is [B][2][1920]
+  float* pcm_out = nfr == 1 ? pcm_[hb] : pcmp_[hb / nfr];  // a pass's PCM is [B][nfr][1920]
   bool fin_fused = false;  // the final conv ran in the stage-2 residual block's epilogue
   // fused residual blocks (k3 conv + ELU + k1 conv + skip + ELU, the hidden rows in LDS) where they
   // beat the two conv launches: stage 2 (480 workgroups; 22.5 us against 16.8 + 11.0). Stages
@@ -1398,10 +1425,15 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   // (f32 only: its own MFMA loop). A fused stage's (unsplit) transposed conv stores no ELU'd copy:
   // the block ELUs the raw rows as they enter LDS
   auto fuse_res = [&](int i) { return big && (fused_stages >> i & 1) && back_mfma_ == PTTS_BACK_F32; };
+  // stages whose fused residual block reads the RAW transposed-conv rows (E = elu(R) applied as the
+  // rows enter LDS): every fused stage whose transposed conv is unsplit (a split one's reduce stores
+  // both the raw and the ELU'd rows)
+  bool raw_only[3] = {false, false, false};
   for (int i = 0; i < 3; ++i) {
     const int r = RATIOS[i];
     const std::string p = "seanet.up" + std::to_string(i);
     const BackTile tt = tile(p + ".convtr", 1);
+    raw_only[i] = fuse_res(i) && !(big && tt.splits > 1);
     if (big && tt.splits > 1) {  // stage 0 (M = 16 B rows): split-K; bias + dual raw / ELU store in the reduce
       PTTS_REQUIRE(i == 0, "split-K transposed conv: stage 0 only");
       conv_op(ops, p + ".convtr", cin_buf, B, T, ch, hist_[1], 1, 1, 0, W(L_.dtr_w[0]), r * (ch / 2), 2, 1, nullptr,
@@ -1429,7 +1461,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
       const double hd = ch / 2;
       double fl = 2.0 * B * T * (hd * 3 * ch + ch * hd);
       double by = 4.0 * ((double)B * T * ch * 3 + B * 2.0 * ch + hd * 3 * ch + ch * hd + hd + ch);
-      if (i > 0) {  // E = elu(R) as the rows enter LDS (stage 0's split-K reduce stores both)
+      if (raw_only[i]) {  // E = elu(R) as the rows enter LDS (a split-K reduce stores both)
         rb.E = cb_[i];
         rb.e_raw = 1;
         by -= 4.0 * B * T * ch;  // E and R are the same rows: read once
@@ -1466,12 +1498,11 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     CommitArgs c{};
     const float* srcs[8] = {mx_, a0_, ce_[0], ca_[0], ce_[1], ca_[1], ce_[2], ca_[2]};
     for (int i = 0; i < 8; ++i) c.h[i] = HistDesc{srcs[i], hist_[i], hist_T_[i] * nfr, hist_C_[i], hist_P_[i]};
-    for (int i = 1; i < 3; ++i)  // a fused stage's k3-conv history: elu(raw rows)
-      if (fuse_res(i)) c.h[2 + 2 * i] = HistDesc{cb_[i], hist_[2 + 2 * i], hist_T_[2 + 2 * i] * nfr, hist_C_[2 + 2 * i], hist_P_[2 + 2 * i], 1};
+    for (int i = 0; i < 3; ++i)  // a raw-only fused stage's k3-conv history: elu(raw rows)
+      if (raw_only[i]) c.h[2 + 2 * i] = HistDesc{cb_[i], hist_[2 + 2 * i], hist_T_[2 + 2 * i] * nfr, hist_C_[2 + 2 * i], hist_P_[2 + 2 * i], 1};
     c.nh = 8;
     c.B = B;
-    c.flags = flags_[hb];
-    c.flags1 = flags_[hb2];
+    for (int f = 0; f < NFR_MAX; ++f) c.flags[f] = flags_[hbs[f]];
     c.nfr = nfr;
     c.mpos = mpos_;
     c.qcur = qcur_;
@@ -1573,13 +1604,13 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
     }
     if (part == 0) {  // the hand-off timeout word, read by fetch() without a device round trip
       PTTS_HIP(hipMemcpyAsync(h_err_, herr_, sizeof(int), hipMemcpyDeviceToHost, cs));
-      // frame pairs: a pass covers the larger row count of its two frames, so this frame's rows
-      // past B carry no frame
-      if (nfr_ == 2 && B < max_slots_)
+      // multi-frame passes: a pass covers the largest row count of its frames, so this frame's
+      // rows past B carry no frame
+      if (nfr_ > 1 && B < max_slots_)
         PTTS_HIP(hipMemsetAsync(flags_[hb] + B, 0, sizeof(FrameFlags) * (max_slots_ - B), cs));
-    } else if (nfr_ == 2) {  // both frames of the pair (PCM and meta) leave HBM in one copy
-      const size_t n = (size_t)max_slots_ * 2 * FRAME + 2 * ((meta_floats_ + 31) / 32 * 32);
-      PTTS_HIP(hipMemcpyAsync(h_pcmp_[hb / 2], pcmp_[hb / 2], sizeof(float) * n, hipMemcpyDeviceToHost, cs));
+    } else if (nfr_ > 1) {  // every frame of the pass (PCM and meta) leaves HBM in one copy
+      const size_t n = (size_t)max_slots_ * nfr_ * FRAME + nfr_ * ((meta_floats_ + 31) / 32 * 32);
+      PTTS_HIP(hipMemcpyAsync(h_pcmp_[hb / nfr_], pcmp_[hb / nfr_], sizeof(float) * n, hipMemcpyDeviceToHost, cs));
     } else {  // the frame of this buffer leaves HBM inside the step (fetch() reads host memory)
       PTTS_HIP(hipMemcpyAsync(h_pcm_[hb], pcm_[hb], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, cs));
       PTTS_HIP(hipMemcpyAsync(h_meta_[hb], meta_[hb], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
@@ -1617,7 +1648,7 @@ void Engine::step_async(int B) {
 // A flush call: frames already computed are decoded and delivered as by a step call, but no row
 // computes a new frame (every row pauses for the call, as rows past n_rows do). Pipelined engines
 // only, and not right after an admission (the admitted rows' first frame must fall on a step
-// call: with frame pairs it must be the first frame of a pair).
+// call: with multi-frame passes it must be the first frame of a pass).
 void Engine::flush_async(int B) {
   PTTS_REQUIRE(B >= 1 && B <= max_slots_, "n_rows out of range");
   PTTS_REQUIRE(pipeline_, "flush: pipelined engines only");
@@ -1628,11 +1659,12 @@ void Engine::flush_async(int B) {
 void Engine::call_async(int B, bool run_front) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_HIP(hipSetDevice(dev_));
-  // Frame pairs: one back pass decodes a row's frames of the pair as a prefix (frame 2j, then
-  // 2j+1). A row the even call did not cover must not produce the pair's second frame alone, so
-  // an odd call covers at most the even call's rows; rows past that are paused for the call, as
-  // rows past n_rows are (an even call that was a flush covered none: the odd call is one too).
-  if (pipeline_ && nfr_ == 2 && (k_ & 1)) {
+  // Multi-frame passes (nfr = back_frames > 1): one back pass decodes a row's frames of the pass as
+  // a prefix (frames nfr j, nfr j + 1, ..). A row the pass's first call did not cover must not
+  // produce a later frame of the pass alone, so a call inside a pass covers at most the previous
+  // call's rows; rows past that are paused for the call, as rows past n_rows are (a first call
+  // that was a flush covered none: the rest of the pass are flushes too).
+  if (pipeline_ && nfr_ > 1 && (k_ % nfr_)) {
     B = std::min(B, rows_hb_[(k_ - 1) % nhb_]);
     if (B == 0) run_front = false;
   }
@@ -1654,44 +1686,48 @@ void Engine::call_async(int B, bool run_front) {
     PTTS_HIP(hipGraphLaunch(back, stream_));
     out_hb_ = hb;
     out_rows_ = B;
-  } else if (nfr_ == 2) {
-    // Frame pairs: call k runs front(k) into buffer k % 6; at even k >= 2 one back pass decodes
-    // frames k-2 and k-1 (buffers (k-2) % 6 and + 1, quantizer parity (k-2)/2 & 1) on stream_be_,
-    // concurrently with the next fronts. Front(k) waits only for the pass over frame k-6, the
-    // last reader of its buffer. The call's frame is k-3 (its pass was launched by call k-1 or
-    // k-2; fetch() waits for it).
+  } else if (nfr_ > 1) {
+    // Multi-frame passes (nfr = 2 or 4): call k runs front(k) into buffer k % (3 nfr); at k % nfr
+    // == 0, k >= nfr, one back pass decodes frames k-nfr .. k-1 (buffers (k-nfr) % (3 nfr) ..) on
+    // stream_be_, concurrently with the next fronts. Front(k) waits only for the pass over frame
+    // k - 3 nfr, the last reader of its buffer. The call's frame is k - (2 nfr - 1) (its pass was
+    // launched by an earlier call; fetch() waits for it).
+    const int nf = nfr_, kr = (int)(k_ % nf);
     rows_hb_[hb] = B;
-    if (!act_slots_.empty() && (k_ & 1) == 0) {  // rows admitted at an odd call start now
+    if (!act_slots_.empty() && kr == 0) {  // rows admitted inside a pass start now
       for (size_t i = 0; i < act_slots_.size(); ++i)
         PTTS_HIP(hipMemcpyAsync(st_ + act_slots_[i], h_act_ + act_slots_[i], sizeof(SlotState), hipMemcpyHostToDevice,
                                 stream_));
       PTTS_HIP(hipEventRecord(ev_act_, stream_));
       act_slots_.clear();
     }
-    // front(k) overwrites hand-off buffer k % 6, last read by the pass over frames k - 6, k - 5; an
-    // even call waits for that pass, which also read the buffer of the odd call after it, so odd
-    // calls need no wait of their own (stream order). A stream wait costs the front stream ≈ 5 us
-    // at the graph boundary even on a completed event (graph stamps, profiles/r04/graph_boundary_ab.txt).
-    if ((k_ & 1) == 0) PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
+    // front(k) overwrites hand-off buffer k % (3 nfr), last read by the pass over frames k - 3 nfr
+    // .. k - 2 nfr - 1; the pass's first call waits for that pass, which also read the buffers of
+    // the pass's other calls, so they need no wait of their own (stream order). A stream wait
+    // costs the front stream ≈ 5 us at the graph boundary even on a completed event (graph
+    // stamps, profiles/r04/graph_boundary_ab.txt).
+    if (kr == 0) PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
     run_front_part();
-    // only the odd call's front part is waited for (by the pair's back pass, below)
-    if (k_ & 1) PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
-    if ((k_ & 1) == 0 && k_ >= 2) {
-      const int h0 = (int)((k_ - 2) % nhb_), h1 = (h0 + 1) % nhb_, pq = (int)(((k_ - 2) / 2) & 1);
-      const int rows = std::max(rows_hb_[h0], rows_hb_[h1]);
-      if (rows > 0) {  // no pass when both calls of the pair were flushes
+    // only the pass's last front part is waited for (by the pass, below)
+    if (kr == nf - 1) PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
+    if (kr == 0 && k_ >= nf) {
+      const int h0 = (int)((k_ - nf) % nhb_), pq = (int)(((k_ - nf) / nf) & 1);
+      int rows = 0;
+      for (int f = 0; f < nf; ++f) rows = std::max(rows, rows_hb_[(h0 + f) % nhb_]);
+      if (rows > 0) {  // no pass when every call of the pass was a flush
         hipGraphExec_t back = part_graph(1, rows, h0, pq);
-        PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[h1], 0));
+        PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[(h0 + nf - 1) % nhb_], 0));
         if (admit_pending_) {
           PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
           admit_pending_ = false;
         }
         PTTS_HIP(hipGraphLaunch(back, stream_be_));
       }
-      PTTS_HIP(hipEventRecord(ev_back_[h0], stream_be_));  // the pass of buffers h0 and h1 (fetch, waits)
+      PTTS_HIP(hipEventRecord(ev_back_[h0], stream_be_));  // the pass over buffers h0 .. (fetch waits)
     }
-    out_hb_ = (int)((k_ + nhb_ - 3) % nhb_);
-    out_rows_ = k_ >= 3 ? rows_hb_[out_hb_] : 0;
+    const int lag = 2 * nf - 1;
+    out_hb_ = (int)((k_ + nhb_ - lag) % nhb_);
+    out_rows_ = k_ >= lag ? rows_hb_[out_hb_] : 0;
   } else {
     const int prev_rows = k_ > 0 ? front_rows_ : B;  // 0: the previous call was a flush
     const int hb1 = (hb + nhb_ - 1) % nhb_, qp1 = qp ^ 1;  // frame k-1
@@ -1732,8 +1768,8 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
   // Pipelined: wait only for the back part that produced this call's frame. The front part of
   // the next frame keeps running, so the front stream never idles across calls (the next call's
   // front graph is queued behind it while this one still runs).
-  // (frame pairs: the pass of buffers 2p, 2p + 1 records only the event of 2p)
-  if (pipeline_) PTTS_HIP(hipEventSynchronize(ev_back_[nfr_ == 2 ? (q & ~1) : q]));
+  // (multi-frame passes: the pass over buffers nfr p .. records only the event of nfr p)
+  if (pipeline_) PTTS_HIP(hipEventSynchronize(ev_back_[q - q % nfr_]));
   else sync();
   const int n = std::min(B, rows);
   if (*h_err_) {  // k_flow_head's bounded hand-off waits: a timeout poisons the frame, fail loudly
@@ -1748,9 +1784,9 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
   const float* hl = h_meta_[q];
   const FrameFlags* hf = (const FrameFlags*)(h_meta_[q] + (size_t)max_slots_ * LDIM);
   const float* he = h_meta_[q] + (size_t)max_slots_ * (LDIM + 2);
-  // a pair's PCM is [B][2][1920] (the frame of buffer q is half q % 2)
+  // a pass's PCM is [B][nfr][1920] (the frame of buffer q is frame q % nfr)
   auto pcm_row = [&](int b) {
-    return nfr_ == 2 ? h_pcmp_[q / 2] + ((size_t)b * 2 + (q & 1)) * FRAME : h_pcm_[q] + (size_t)b * FRAME;
+    return nfr_ > 1 ? h_pcmp_[q / nfr_] + ((size_t)b * nfr_ + q % nfr_) * FRAME : h_pcm_[q] + (size_t)b * FRAME;
   };
   for (int b = 0; b < B; ++b) {
     const bool ok = b < n && hf[b].valid;
@@ -2459,9 +2495,10 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
   // staged through pinned buffers so the copies are truly asynchronous: admission returns with
   // the prefill still running and the caller's first step queued right behind it (no host
   // round trip in between); the event wait above guarantees the staging is free again
-  // frame pairs: an utterance's frames pair up from its first, so rows admitted before an odd
-  // call stay inactive for that call and start at the next (their state is written then)
-  admit_delay_ = nfr_ == 2 && (k_ & 1) ? 1 : 0;
+  // multi-frame passes: an utterance's frames group into passes from its first, so rows admitted
+  // inside a pass stay inactive for the pass's remaining calls and start at the next pass (their
+  // state is written then)
+  admit_delay_ = nfr_ > 1 ? (int)((nfr_ - k_ % nfr_) % nfr_) : 0;
   if (admit_delay_)
     for (int i = 0; i < n; ++i) {
       h_act_[slots[i]] = st[i];
@@ -2582,7 +2619,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
       PTTS_HIP(hipMemcpyAsync(pcm + (size_t)i * FRAME, pcm_[par] + (size_t)slot * FRAME, sizeof(float) * FRAME,
                               hipMemcpyDeviceToHost, stream_));
     if (quant)
-      PTTS_HIP(hipMemcpyAsync(quant + (size_t)i * MD, qcur_ + (size_t)slot * 2 * MD,
+      PTTS_HIP(hipMemcpyAsync(quant + (size_t)i * MD, qcur_ + (size_t)slot * NFR_MAX * MD,
                               sizeof(float) * MD, hipMemcpyDeviceToHost, stream_));
     PTTS_HIP(hipMemcpyAsync(flags_[par] + slot, &off, sizeof off, hipMemcpyHostToDevice, stream_));
     PTTS_HIP(hipStreamSynchronize(stream_));

@@ -51,7 +51,8 @@ class Engine {
   bool pipelined() const { return pipeline_; }
   // calls by which a frame trails its FlowLM step (ptts_frame_lag) and the latest admission's
   // start delay
-  int frame_lag() const { return !pipeline_ ? 0 : (nfr_ == 2 ? 3 : 1); }
+  // (a pass over nfr frames: 2 nfr - 1 calls; single frames: 1)
+  int frame_lag() const { return !pipeline_ ? 0 : 2 * nfr_ - 1; }
   int admit_delay() const { return admit_delay_; }
 
   ptts_voice* voice_from_prompt(const float* prompt, int F);
@@ -94,7 +95,7 @@ class Engine {
   // hb: front -> back hand-off buffer (frame index mod NHB); qp: parity of the back part's
   // quantizer history (frame index mod 2; the back part reads the previous frame's half)
   void build_front(std::vector<Op>& ops, int B, int hb);
-  // back part over nfr consecutive frames from hand-off buffers hb, hb + 1
+  // back part over nfr consecutive frames from hand-off buffers hb, hb + 1, .. hb + nfr - 1
   void build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp);
   hipGraphExec_t part_graph(int part, int B, int hb, int qp);
   void push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r);
@@ -205,11 +206,11 @@ class Engine {
   // front -> back hand-off per step parity, and the back part's own split-K slabs
   // Up to three hand-off buffers: front(k) writes buffer k % nhb_ and waits only for back(k - nhb_)
   // (nhb_ = 3 lets front and back drift a step apart instead of running in lockstep).
-  // Six hand-off buffers with frame pairs (back_frames = 2): the pair (2j, 2j+1) occupies two
-  // while the fronts of the next four frames fill the others (the front part may run two passes
-  // ahead of the back part).
-  static constexpr int NHB = 6;
-  int nhb_ = 3;  // buffers in use: 3, or NHB = 6 with frame pairs
+  // 3 nfr hand-off buffers with passes over nfr = back_frames > 1 frames: a pass's nfr buffers
+  // are read while the fronts of the next 2 nfr frames fill the others (the front part may run two
+  // passes ahead of the back part).
+  static constexpr int NHB = NHB_MAX;
+  int nhb_ = 3;  // buffers in use: 3, or 3 nfr with multi-frame passes
   int nfr_ = 1;  // frames per back-part pass (ptts_engine_config.back_frames)
   int back_mfma_ = PTTS_BACK_F32;  // ptts_engine_config.back_mfma: the back part's tiles' arithmetic
   // bf16x6 back part: weight matrix -> its split3 copy (hi | mid, lo), derive_split at finalize
@@ -217,12 +218,13 @@ class Engine {
   void derive_split();
   void attach_split(GemmArgs& a) const;
   int rows_hb_[NHB] = {};  // rows of the front part that filled each hand-off buffer
-  // frame-pair mode: PCM of one pair [B][2][1920] per pair parity, and its pinned host copy
+  // multi-frame passes: PCM of one pass [B][nfr][1920] followed by the meta blocks of its nfr
+  // buffers, per pass (buffers q with q / nfr = p), and its pinned host copy
   float* pcmp_[NHB / 2] = {};
   float* h_pcmp_[NHB / 2] = {};
-  float* fin_side_ = nullptr;  // [slot][2 * FRAME / 128][2]: the fused final conv's tile-boundary shares
-  // rows admitted at an odd call under frame pairs start one call later: their SlotState (active)
-  // is written right before the next front part (pinned staging)
+  float* fin_side_ = nullptr;  // [slot][nfr * FRAME / 128][2]: the fused final conv's tile-boundary shares
+  // rows admitted inside a pass's calls (not at a call k with k % nfr == 0) start at the next pass
+  // boundary: their SlotState (active) is written right before that front part (pinned staging)
   SlotState* h_act_ = nullptr;
   std::vector<int> act_slots_;
   int admit_delay_ = 0;

@@ -364,13 +364,18 @@ struct FrontCommitArgs {
 };
 void front_commit(const FrontCommitArgs& a, hipStream_t s);
 
+// Frames per back-part pass (ptts_engine_config.back_frames: 1, 2 or 4) and the front -> back
+// hand-off buffers of the largest pass (three passes' worth: the front part may run two passes ahead)
+constexpr int NFR_MAX = 4;
+constexpr int NHB_MAX = 3 * NFR_MAX;
+
 // Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0, for
-// nfr (1 or 2) consecutive frames of every row: latent[f] [B][32] -> x [B][16 nfr][512] (frame f
-// at rows 16 f..), h = LN(x). The overlap-add history [B][512] is read from qprev_in (frame 0;
-// frame 1 overlaps frame 0); the quantized rows of the pass go to qprev_out [B][2][512], and the
-// commit copies the last valid frame's into the history (rows without a frame, or outside the
-// pass, keep theirs).
-void quant_upsample(const float* const latent[2], const FrameFlags* const fl[2], int nfr, int B, const float* emb_std,
+// nfr (1, 2 or 4) consecutive frames of every row: latent[f] [B][32] -> x [B][16 nfr][512] (frame
+// f at rows 16 f..), h = LN(x). The overlap-add history [B][512] is read from qprev_in (frame 0;
+// frame f > 0 overlaps frame f - 1); the quantized rows of the pass go to qprev_out
+// [B][NFR_MAX][512], and the commit copies the last valid frame's into the history (rows without a
+// frame, or outside the pass, keep theirs).
+void quant_upsample(const float* const latent[NFR_MAX], const FrameFlags* const fl[NFR_MAX], int nfr, int B, const float* emb_std,
                     const float* emb_mean, const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
                     float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s);
 
@@ -378,7 +383,7 @@ void quant_upsample(const float* const latent[2], const FrameFlags* const fl[2],
 // into its history and the last valid frame's quantizer output into the overlap-add history,
 // advance the Mimi position. A launch over nfr frames (T rows per row of a
 // buffer = nfr frames of T / nfr rows) commits through the row's last valid frame: its valid
-// frames are a prefix (an utterance starts at a frame-pair boundary and ends with its last frame).
+// frames are a prefix (an utterance starts at a pass boundary and ends with its last frame).
 struct HistDesc {
   const float* src;  // [B][T][C]
   float* dst;        // [B][P][C]
@@ -389,11 +394,10 @@ struct CommitArgs {
   HistDesc h[10];
   int nh;
   int B;
-  const FrameFlags* flags;   // frame 0
-  const FrameFlags* flags1;  // frame 1 (nfr == 2)
+  const FrameFlags* flags[NFR_MAX];  // frame f of the pass (f < nfr)
   int nfr;
   int* mpos;  // Mimi decoder positions, += 16 per committed frame
-  const float* qcur;  // the pass's quantizer outputs [B][2][512] (quant_upsample)
+  const float* qcur;  // the pass's quantizer outputs [B][NFR_MAX][512] (quant_upsample)
   float* qprev;       // overlap-add history [B][512] <- qcur[b][last valid frame]
   // the fused final conv's tile-boundary shares (ResBlockArgs::fside): pcm[b][x * 128 + k] +=
   // fin_side[b][x][k], k < 2, for tiles x = 1 .. fin_T / 128 - 1 (fin_side == nullptr: none)
@@ -416,7 +420,7 @@ struct ResetArgs {
   const float* bos;
   const SlotState* st_src;
   const int* fpos_src;
-  FrameFlags* flags[6];  // every hand-off buffer: an undrained frame of the slot's previous
+  FrameFlags* flags[NHB_MAX];  // every hand-off buffer: an undrained frame of the slot's previous
                          // utterance is discarded (null entries skipped)
   SlotState* st;
   int* fpos;

@@ -3281,12 +3281,12 @@ void flow_cond(const float* P, int S, int B, const float* bias, const float* tem
 // (conv.rs:315-346: frame row r = q*w[r] + qprev*w[16+r], the overlap-add of the previous frame's
 // tail) + norm1 of Mimi layer 0. One workgroup per (row b, 4 of the 16 output rows): 4x the
 // workgroups of a per-row kernel, each loading only its rows' upsample taps, one LayerNorm row
-// per wave. The pass's quantizer outputs go to a scratch (qprev_out [B][2][512]) and the commit
+// per wave. The pass's quantizer outputs go to a scratch (qprev_out [B][NFR_MAX][512]) and the commit
 // moves the last valid frame's into the history, so the four workgroups of a row never race on
 // it, and a row without a frame in the pass (or outside it) keeps its history unchanged.
 struct QuantUpArgs {
-  const float* latent[2];
-  const FrameFlags* fl[2];
+  const float* latent[NFR_MAX];
+  const FrameFlags* fl[NFR_MAX];
   int nfr;
   const float *emb_std, *emb_mean, *wq, *wup, *qprev_in;
   float* qprev_out;
@@ -3295,7 +3295,7 @@ struct QuantUpArgs {
 };
 // grid (B, 4 nfr): rows 4 (y % 4).. of frame y / 4 of row b
 __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
-  __shared__ float sz[2][32];
+  __shared__ float sz[NFR_MAX][32];
   __shared__ float sx[4 * 512];
   const int b = blockIdx.x, f = blockIdx.y >> 2, r0 = (blockIdx.y & 3) * 4, tid = threadIdx.x;
   const int T = 16 * a.nfr;
@@ -3322,14 +3322,18 @@ __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
     const float* wqf = reinterpret_cast<const float*>(wqr[u]);
     const float* w0 = reinterpret_cast<const float*>(&wur[u][0]);
     const float* w1 = reinterpret_cast<const float*>(&wur[u][1]);
-    float q[2] = {0.f, 0.f};
+    float q[NFR_MAX] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < NFR_MAX; ++g)
       if (g < a.nfr) {
 #pragma unroll
         for (int k = 0; k < 32; ++k) q[g] += wqf[k] * sz[g][k];
       }
-    const float cur = f == 0 ? q[0] : q[1], prev = f == 0 ? qpv[u] : q[0];  // frame 1 overlaps frame 0
+    // frame f overlaps frame f - 1 (frame 0 the history); selects, no dynamic register indexing
+    float cur = q[0], prev = qpv[u];
+#pragma unroll
+    for (int g = 1; g < NFR_MAX; ++g)
+      if (f == g) cur = q[g], prev = q[g - 1];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float v = cur * w0[r] + prev * w1[r];
@@ -3337,8 +3341,9 @@ __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
       a.x[((long)b * T + 16 * f + r0 + r) * 512 + c] = v;
     }
     if (blockIdx.y == 0) {
-      a.qprev_out[(long)b * 1024 + c] = q[0];
-      if (a.nfr > 1) a.qprev_out[(long)b * 1024 + 512 + c] = q[1];
+#pragma unroll
+      for (int g = 0; g < NFR_MAX; ++g)
+        if (g < a.nfr) a.qprev_out[((long)b * NFR_MAX + g) * 512 + c] = q[g];
     }
   }
   __syncthreads();
@@ -3361,12 +3366,26 @@ __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
   }
 }
 
-void quant_upsample(const float* const latent[2], const FrameFlags* const fl[2], int nfr, int B, const float* emb_std,
+void quant_upsample(const float* const latent[NFR_MAX], const FrameFlags* const fl[NFR_MAX], int nfr, int B, const float* emb_std,
                     const float* emb_mean, const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
                     float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s) {
-  if (nfr < 1 || nfr > 2) throw std::runtime_error("quant_upsample: 1 or 2 frames");
-  QuantUpArgs a{{latent[0], nfr > 1 ? latent[1] : latent[0]}, {fl[0], nfr > 1 ? fl[1] : fl[0]}, nfr, emb_std, emb_mean,
-                wq, wup, qprev_in, qprev_out, x, h, ln_w, ln_b};
+  if (nfr != 1 && nfr != 2 && nfr != 4) throw std::runtime_error("quant_upsample: 1, 2 or 4 frames");
+  QuantUpArgs a{};
+  for (int g = 0; g < NFR_MAX; ++g) {
+    a.latent[g] = latent[g < nfr ? g : 0];
+    a.fl[g] = fl[g < nfr ? g : 0];
+  }
+  a.nfr = nfr;
+  a.emb_std = emb_std;
+  a.emb_mean = emb_mean;
+  a.wq = wq;
+  a.wup = wup;
+  a.qprev_in = qprev_in;
+  a.qprev_out = qprev_out;
+  a.x = x;
+  a.h = h;
+  a.ln_w = ln_w;
+  a.ln_b = ln_b;
   hipLaunchKernelGGL(k_quant_upsample, dim3(B, 4 * nfr), dim3(256), cap_lds(k_quant_upsample, g_wg_cap), s, a);
 }
 
@@ -3383,7 +3402,8 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
     for (int e = 2 + threadIdx.x; e < 2 * nx; e += 256)
       a.fin_pcm[(long)b * a.fin_T + (e >> 1) * RESBLOCK_FIN_TT + (e & 1)] += a.fin_side[(long)b * 2 * nx + e];
   }
-  const int nv = !a.flags[b].valid ? 0 : (a.nfr > 1 && a.flags1[b].valid ? 2 : 1);  // valid frames: a prefix
+  int nv = 0;  // valid frames: a prefix
+  while (nv < a.nfr && a.flags[nv][b].valid) ++nv;
   if (nv == 0) return;
   for (int i = 0; i < a.nh; ++i) {
     const HistDesc& hd = a.h[i];
@@ -3403,7 +3423,7 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
   // the overlap-add history of the next pass: the last valid frame's quantizer output
   if (threadIdx.x < 128)
     reinterpret_cast<float4*>(a.qprev + (long)b * 512)[threadIdx.x] =
-        reinterpret_cast<const float4*>(a.qcur + ((long)b * 2 + nv - 1) * 512)[threadIdx.x];
+        reinterpret_cast<const float4*>(a.qcur + ((long)b * NFR_MAX + nv - 1) * 512)[threadIdx.x];
   if (threadIdx.x == 0) a.mpos[b] += 16 * nv;
 }
 
@@ -3503,7 +3523,7 @@ __global__ __launch_bounds__(256) void k_slot_reset(ResetArgs a) {
     a.st[slot] = a.st_src[i];
     a.fpos[slot] = a.fpos_src[i];
     a.mpos[slot] = 0;
-    for (int q = 0; q < 6; ++q)
+    for (int q = 0; q < NHB_MAX; ++q)
       if (a.flags[q]) a.flags[q][slot] = FrameFlags{0, 0};
   }
 }

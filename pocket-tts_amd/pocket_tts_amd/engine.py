@@ -77,13 +77,15 @@ class Engine:
         FlowLM step GEMMs streaming int8 codes. fp8_gemm=True: the large FlowLM step GEMMs run as
         fp8 W8A8 MFMA (accuracy-gated; see ptts_engine_config.fp8_gemm). cfg_yaml: the reference's
         model config (config/b6369a24.yaml), checked against the compiled dimensions.
-        back_frames=2 (pipelined only): two frames per Mimi-decode pass; a step() returns the frame
-        computed three calls earlier (`frame_lag`). back_mfma (ptts_engine_config.back_mfma): how the
+        back_frames=n, 2 or 4 (pipelined only): n frames per Mimi-decode pass; a step() returns the
+        frame computed 2 n - 1 calls earlier (`frame_lag`). back_mfma (ptts_engine_config.back_mfma): how the
         Mimi decode's GEMMs and convs use the matrix cores, BACK_F32 (exact f32 FMA chain), BACK_F32X6
         (f32 products as six bf16 piece products, f32 accuracy) or BACK_BF16 (operands rounded to
         bf16: a variant gated on PCM accuracy); back_bf16=True is BACK_BF16."""
         if back_mfma is None:
             back_mfma = BACK_BF16 if back_bf16 else BACK_F32
+        elif back_bf16 and back_mfma != BACK_BF16:
+            raise ValueError("back_bf16=True contradicts back_mfma=%d (pass one of them)" % back_mfma)
         cfg = EngineConfig(device, max_slots, max_ctx, lsd_decode_steps, seed,
                            weights_path.encode() if weights_path else None,
                            weight_blob or None, int(defer_weights), int(pipeline), int(weight_quant),

@@ -313,11 +313,13 @@ class LoadBoard:
     /dev/shm that every worker of the server maps, and a worker with no free slot answers a request
     on the shared port with 307 (method and body kept) to the private port of the least-loaded peer
     that has one. Requests on a private port are always served (a request is redirected at most
-    once). One int64 triple per rank: (load, private port, pid). Each worker resets its own entry
-    when it maps the board, and a peer is a target only while its pid is alive, so an entry left by
-    a crashed worker, or by an earlier server on the same port, is never redirected to."""
+    once). One int64 quadruple per rank: (load, private port, pid, process start time). Each worker
+    resets its own entry when it maps the board, and a peer is a target only while a process with
+    that pid AND that start time (/proc/<pid>/stat field 22) exists, so an entry left by a crashed
+    worker, or by an earlier server on the same port, is not redirected to even after the pid has
+    been reused by another process."""
 
-    FIELDS = 3
+    FIELDS = 4
 
     def __init__(self, port: int, world: int, rank: int, max_rows: int, path: str | None = None):
         import mmap
@@ -333,7 +335,7 @@ class LoadBoard:
         finally:
             os.close(fd)
         self.v = np.frombuffer(self._mm, np.int64).reshape(world, self.FIELDS)
-        self.v[rank] = (0, 0, os.getpid())  # this worker's entry, whatever an earlier run left
+        self.v[rank] = (0, 0, os.getpid(), self._start_time(os.getpid()))  # whatever an earlier run left
         self.private_port = 0
 
     def publish(self, load: int):
@@ -344,7 +346,23 @@ class LoadBoard:
         self.v[self.rank, 1] = port
 
     @staticmethod
-    def _alive(pid: int) -> bool:
+    def _start_time(pid: int) -> int:
+        """The process's start time in clock ticks since boot (/proc/<pid>/stat field 22); -1 if
+        there is no such process (0 where /proc is not available)."""
+        try:
+            with open(f"/proc/{int(pid)}/stat", "rb") as f:
+                stat = f.read().decode(errors="replace")
+        except FileNotFoundError:
+            return -1
+        except OSError:
+            return 0
+        # the command name (field 2) is parenthesised and may hold spaces: fields after its ')'
+        return int(stat[stat.rindex(")") + 2:].split()[19])
+
+    @classmethod
+    def _alive(cls, pid: int, start: int = 0) -> bool:
+        """True while the worker that published (pid, start) runs: a live process with that pid,
+        owned by this user, started at that time (a reused pid has a later start time)."""
         if pid <= 0:
             return False
         try:
@@ -353,17 +371,17 @@ class LoadBoard:
             return False
         except PermissionError:  # exists, owned by another user: not one of this server's workers
             return False
-        return True
+        return start == 0 or cls._start_time(pid) == start
 
     def redirect_target(self, own_load: int) -> int | None:
         """The private port of the least-loaded live peer with a free slot, if this worker has none."""
         if own_load < self.max_rows:
             return None
-        loads, ports, pids = self.v[:, 0].copy(), self.v[:, 1].copy(), self.v[:, 2].copy()
+        loads, ports, pids, starts = (self.v[:, i].copy() for i in range(self.FIELDS))
         best = None
         for r in range(self.world):
             if (r != self.rank and ports[r] > 0 and loads[r] < self.max_rows and (best is None or loads[r] < loads[best])
-                    and self._alive(pids[r])):
+                    and self._alive(pids[r], starts[r])):
                 best = r
         if best is None:
             return None
@@ -372,7 +390,7 @@ class LoadBoard:
 
     def close(self, unlink: bool = False):
         if self.v is not None:
-            self.v[self.rank] = (0, 0, 0)  # a closed worker is no target
+            self.v[self.rank] = (0, 0, 0, 0)  # a closed worker is no target
         self.v = None
         self._mm.close()
         if unlink:
@@ -734,7 +752,7 @@ def main(argv=None):
     ap.add_argument("--max-ctx", type=int, default=1024)
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
-    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2),
+    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2, 4),
                     help="frames per Mimi decode pass (ptts_engine_config.back_frames): 2, the throughput "
                          "configuration bench.py measures (two more calls of frame lag, ~1.2 ms at B = 32)")
     ap.add_argument("--stand-in-engine", action="store_true",

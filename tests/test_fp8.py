@@ -237,3 +237,36 @@ def test_gpu_fp8_eos_frame_count_agreement():
     # gates set from the measurement
     assert np.abs(f32 - f8).max() <= EOS_ABS
     assert summary["within_1_frame"] >= 0.5, summary  # measured 0.77 (same frame 0.59, EOS |d| <= 0.17)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline,back_frames", [(False, 1), (True, 1), (True, 2)])
+def test_gpu_fp8_matrices_stream_codes_in_every_stepping_mode(pipeline, back_frames):
+    """every fp8 matrix must run W8A8 in every stepping mode. In single-frame pipelined
+    stepping linear2 has no fused feed-forward and no {4, 128} register-resident tile; it used to
+    land on the f32 register-resident GEMM there. The plan's algorithmic bytes state what each
+    launch streams: one byte per weight on the fp8 path, four on an f32 one."""
+    import pocket_tts_amd as pt
+
+    B = 32
+    eng = pt.Engine(device=0, max_slots=B, max_ctx=128, seed=0x5EED, fp8_gemm=True, pipeline=pipeline,
+                    back_frames=back_frames)
+    try:
+        assert eng.fp8_matrices == N_FP8_MATRICES
+        eng.open_many(list(range(B)), [eng.voice_from_prompt(np.zeros((4, 1024), np.float32))] * B,
+                      [np.array([1, 2, 3], np.int32)] * B,
+                      [pt.GenerationParams(temp=0.0, eos_threshold=float("inf"), max_frames=4)] * B)
+        plan = {n: (fl, by) for n, fl, by in eng.plan(B)}
+        weights = {"qkv_gemm": 3072 * 1024, "ff1_gemm": 4096 * 1024, "ff2_gemm": 1024 * 4096, "ffn": 2 * 4096 * 1024}
+        seen = 0
+        for name, (fl, by) in plan.items():
+            kind = name.split(".")[-1]
+            if name.startswith("flow.l") and kind in weights:
+                # codes: 1 B per weight (+ activations and split-K slabs), f32: >= 4 B per weight
+                assert by < 3.0 * weights[kind], (name, by)
+                seen += 1
+        assert plan["head.ada_gemm"][1] < 3.0 * 10240 * 512
+        # per layer: qkv + (ffn | ff1 + ff2)
+        assert seen >= 6 * 2, sorted(plan)
+    finally:
+        eng.close()

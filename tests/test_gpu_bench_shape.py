@@ -1,6 +1,6 @@
 """GPU parity at the benchmark's own shape (BASELINE configs[2]): f32 engine, 32 rows, 125-frame
 voice prompts, 40 text tokens, 132 free-running frames at temperature 0, pipelined stepping with
-frame pairs (the bench's mode: one Mimi decode pass per two frames) and with one frame per pass, and
+frame pairs (the bench's mode: one Mimi decode pass per two frames), four frames and one frame per pass, and
 with frame pairs on the bf16x6 back part (back_mfma = BACK_F32X6: f32 GEMMs as exact bf16 piece
 products) at the same gates. The FlowLM context of every row grows 165 -> 297 positions, so the step attention
 (k_attn_decode_qkv) takes its second 256-key round for the last 40 frames, and the Mimi decoder's
@@ -65,7 +65,7 @@ def _engine_frames(pt, inputs, back_frames, back_mfma=0):
                                      max_frames=FRAMES, seed=1)
         eng.open_many(list(range(B)), voices, [i for _, i in inputs], [params] * B)
         lag, delay = eng.frame_lag()
-        assert (lag, delay) == ((3, 0) if back_frames == 2 else (1, 0))
+        assert (lag, delay) == (2 * back_frames - 1, 0)
         frames = []
         for _ in range(lag + delay):  # pipelined: the first calls return no frame
             assert not eng.step(B).valid.any()
@@ -89,7 +89,7 @@ def test_bench_shape_b32_long_context_matches_reference_and_oracle(oracle):
     with ThreadPoolExecutor(workers) as ex:  # the oracle runs free (temp 0): precompute them
         futs = {b: ex.submit(_oracle_run, oracle, *inputs[b], FRAMES) for b in range(B)}
         runs = {(bf, mf): _engine_frames(pt, inputs, bf, mf)
-                for bf, mf in ((2, pt.BACK_F32), (1, pt.BACK_F32), (2, pt.BACK_F32X6))}
+                for bf, mf in ((2, pt.BACK_F32), (1, pt.BACK_F32), (4, pt.BACK_F32), (2, pt.BACK_F32X6))}
         ref = {b: f.result() for b, f in futs.items()}
 
     worst = {"golden": [0.0, 0.0, 0.0], "oracle": [0.0, 0.0, 0.0]}
@@ -125,7 +125,8 @@ def _oracle_run_noisy(oracle, prompt, ids, n, seed, temp):
     return out
 
 
-def test_bench_exact_input_shared_voice_matches_oracle(oracle):
+@pytest.mark.parametrize("back_frames", [2, 4])
+def test_bench_exact_input_shared_voice_matches_oracle(oracle, back_frames):
     """bench.py's own job, input for input: ONE voice (bench.synth_prompt, 125 frames) admitted
     into all 32 rows in one batched admission, so every row reads the voice's shared KV prefix
     (KvStore::pre) rather than a copy; bench.text_ids(b); temperature 0.7 with bench.slot_seed's
@@ -143,7 +144,7 @@ def test_bench_exact_input_shared_voice_matches_oracle(oracle):
     with ThreadPoolExecutor(workers) as ex:
         futs = [ex.submit(_oracle_run_noisy, oracle, prompt, ids[b], n, seeds[b], temp) for b in range(B)]
         eng = pt.Engine(device=0, max_slots=B, max_ctx=bench.PROMPT_FRAMES + bench.TEXT_TOKENS + n + 8,
-                        lsd_decode_steps=1, seed=0x5EED, pipeline=True, back_frames=2)
+                        lsd_decode_steps=1, seed=0x5EED, pipeline=True, back_frames=back_frames)
         try:
             voice = eng.voice_from_prompt(prompt)
             eng.open_many(list(range(B)), [voice] * B, ids,
@@ -176,4 +177,5 @@ def test_bench_exact_input_shared_voice_matches_oracle(oracle):
             err = [abs(g[0] - e[0]), float(np.abs(g[1] - e[1]).max()), float(np.abs(g[2] - e[2]).max())]
             worst = [max(x, y) for x, y in zip(worst, err)]
             assert err[0] <= LAT_TOL and err[1] <= LAT_TOL and err[2] <= PCM_TOL, (b, i, err)
-    print(f"bench input (shared voice, temp {temp}): worst |d| eos/latent/pcm vs oracle {worst}")
+    print(f"bench input (shared voice, temp {temp}, back_frames {back_frames}): worst |d| eos/latent/pcm vs oracle "
+          f"{worst}")

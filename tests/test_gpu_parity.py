@@ -286,20 +286,25 @@ def test_pipelined_stepping_matches_oracle(oracle):
         eng.close()
 
 
-def test_frame_pairs_continuous_batching_matches_oracle(oracle):
-    """back_frames=2: one Mimi decode pass per two frames, a call returns the frame computed three
-    calls earlier. Rows admitted at an even call, rows admitted at an odd call (they start one call
-    later, so that an utterance's frames pair up from its first), a row whose utterance ends on the
-    first frame of a pair (odd length: the pass commits its codec state through that frame only)
-    and a row re-admitted after it finished must all equal their oracle runs frame for frame."""
+@pytest.mark.parametrize("back_frames", [2, 4])
+def test_frame_pairs_continuous_batching_matches_oracle(oracle, back_frames):
+    """back_frames = n (2 or 4): one Mimi decode pass per n frames, a call returns the frame computed
+    2 n - 1 calls earlier. Rows admitted at a pass boundary, rows admitted inside a pass (they start
+    at the next boundary, so that an utterance's frames group into passes from its first), a row
+    whose utterance ends on the first frame of a pass (5 frames: the pass commits its codec state
+    through that frame only) and a row re-admitted after it finished must all equal their oracle
+    runs frame for frame."""
     import pocket_tts_amd as pt
 
     d = load_golden("e2e_lsd1.safetensors")
     rng = np.random.default_rng(7)
+    n = back_frames
+    lag = 2 * n - 1
     eng = pt.Engine(device=0, max_slots=4, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
-                    back_frames=2)
+                    back_frames=n)
     try:
         orc, lat, got, want = {}, {}, {}, {}
+        calls = [0]
 
         def admit(slots, n_frames):
             ids_l, vs = [], []
@@ -318,6 +323,7 @@ def test_frame_pairs_continuous_batching_matches_oracle(oracle):
 
         def step_check():
             r = eng.step(4)
+            calls[0] += 1
             for b in list(orc):
                 if not r.valid[b]:
                     continue
@@ -331,15 +337,16 @@ def test_frame_pairs_continuous_batching_matches_oracle(oracle):
                 assert pcm_err(r.pcm[b] - o["pcm"]) <= PCM_TOL
             return r
 
-        assert admit([0, 1], 5) == (3, 0)  # call 0 (even); row 0/1 end on the first frame of a pair
-        for _ in range(3):
+        assert admit([0, 1], 5) == (lag, 0)  # call 0 (a pass boundary); 5 frames end on a pass's first
+        for _ in range(lag):
             assert not step_check().valid.any()
-        assert admit([2, 3], 4) == (3, 1)  # before call 3 (odd): rows 2/3 start at call 4
-        for _ in range(6):
+        c = calls[0]  # inside a pass: rows 2/3 start at the next boundary
+        assert admit([2, 3], 4) == (lag, (n - c % n) % n)
+        for _ in range(2 * lag):
             step_check()
-        assert got[0] == 5 and got[1] == 5  # frames 0..4 of rows 0/1 arrived by call 7
-        admit([0], 3)  # re-admission of a finished row (call 9: odd)
-        for _ in range(12):
+        assert got[0] == 5 and got[1] == 5  # frames 0..4 of rows 0/1 arrived
+        admit([0], 3)  # re-admission of a finished row
+        for _ in range(2 * lag + n + 3):
             step_check()
         assert got[0] == 3 and got[2] == 4 and got[3] == 4
         assert not eng.step(4).valid.any()
@@ -347,7 +354,7 @@ def test_frame_pairs_continuous_batching_matches_oracle(oracle):
         eng.close()
 
 
-@pytest.mark.parametrize("back_frames", [1, 2])
+@pytest.mark.parametrize("back_frames", [1, 2, 4])
 def test_varying_rows_per_call_match_oracle(oracle, back_frames):
     """Pipelined stepping with n_rows changing from call to call, so rows pause (outside n_rows)
     and resume with their codec state intact: the overlap-add history, conv histories and Mimi
@@ -396,7 +403,7 @@ def test_varying_rows_per_call_match_oracle(oracle, back_frames):
         eng.close()
 
 
-@pytest.mark.parametrize("back_frames", [1, 2])
+@pytest.mark.parametrize("back_frames", [1, 2, 4])
 def test_flush_calls_drain_and_pause_rows(oracle, back_frames):
     """ptts_flush_async: a pipelined call that starts no frame. Flushes in the middle of a job
     pause every row for the call (their frames resume in order, equal to the oracle's), flushes at
@@ -474,7 +481,7 @@ def test_long_utterance_wraps_mimi_ring(gpu_engine, oracle):
     assert worst <= PCM_TOL, worst
 
 
-@pytest.mark.parametrize("back_frames", [1, 2])
+@pytest.mark.parametrize("back_frames", [1, 2, 4])
 def test_batch_scheduler_matches_oracle(oracle, back_frames):
     """Serving front end (f1) on the real pipelined engine: 6 requests of different lengths through
     3 slots (continuous admission into recycled slots); every request's audio equals its own

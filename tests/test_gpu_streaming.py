@@ -40,7 +40,7 @@ class SentenceTokenizer:
         return 40
 
 
-@pytest.mark.parametrize("pipeline,back_frames", [(False, 1), (True, 1), (True, 2)])
+@pytest.mark.parametrize("pipeline,back_frames", [(False, 1), (True, 1), (True, 2), (True, 4)])
 def test_streaming_matches_batch_over_multiple_chunks(oracle, pipeline, back_frames):
     import pocket_tts_amd as pt
     from pocket_tts_amd.text import prepare_text_prompt

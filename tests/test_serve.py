@@ -331,9 +331,11 @@ def test_configs3_256_streams_over_8_workers(tmp_path):
 
 
 def test_load_board_never_redirects_to_a_dead_or_stale_worker(tmp_path):
-    """ADVICE r4: a board entry left by a crashed worker (or an earlier server on the same port)
-    must not draw 307s. Entries carry the worker's pid; a worker resets its own entry when it maps
-    the board and clears it on close."""
+    """ADVICE r4/r5: a board entry left by a crashed worker (or an earlier server on the same port)
+    must not draw 307s, even once its pid has been reused by another process. Entries carry the
+    worker's pid and process start time; a worker resets its own entry when it maps the board and
+    clears it on close."""
+    import os
     import subprocess
     import sys
 
@@ -345,13 +347,18 @@ def test_load_board_never_redirects_to_a_dead_or_stale_worker(tmp_path):
     # rank 1: an entry of a process that has exited (free slots, a port)
     p = subprocess.Popen([sys.executable, "-c", "pass"])
     p.wait()
-    b0.v[1] = (0, 5001, p.pid)
+    b0.v[1] = (0, 5001, p.pid, 1)
     # rank 2: a stale entry with no pid at all (an earlier board layout / run)
-    b0.v[2] = (0, 5002, 0)
+    b0.v[2] = (0, 5002, 0, 0)
+    assert b0.redirect_target(4) is None
+    # a live pid whose start time differs from the entry's: the pid was reused, not the worker
+    me = os.getpid()
+    assert LoadBoard._start_time(me) > 0
+    b0.v[1] = (0, 5001, me, LoadBoard._start_time(me) + 1)
     assert b0.redirect_target(4) is None
     # a live peer with a free slot is a target; re-mapping as rank 1 resets the stale entry first
     b1 = LoadBoard(port=1, world=3, rank=1, max_rows=4, path=path)
-    assert tuple(b0.v[1]) == (0, 0, b1.v[1, 2])
+    assert tuple(b0.v[1]) == (0, 0, b1.v[1, 2], LoadBoard._start_time(me))
     b1.set_private_port(6001)
     assert b0.redirect_target(4) == 6001
     b1.close()

@@ -3,7 +3,7 @@ temperature 0, pipelined frame pairs): each library runs in its own child proces
 PCM and latents of every row and frame go to an .npz, and the max abs differences are printed. For a
 tile or reduction-order change that has no GPU test of its own build (e.g. a -D variant library).
 
-    python tools/lib_diff.py A.so B.so [frames]
+    python tools/lib_diff.py A.so B.so [frames] [back_frames]
 """
 
 import os
@@ -16,7 +16,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(out, frames):
+def child(out, frames, back_frames=2):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "pocket-tts_amd"))
     import bench
@@ -24,7 +24,7 @@ def child(out, frames):
 
     B = 32
     eng = pt.Engine(device=0, max_slots=B, max_ctx=bench.PROMPT_FRAMES + bench.TEXT_TOKENS + frames + 8,
-                    lsd_decode_steps=1, seed=0x5EED, pipeline=True, back_frames=2)
+                    lsd_decode_steps=1, seed=0x5EED, pipeline=True, back_frames=back_frames)
     try:
         voice = eng.voice_from_prompt(bench.synth_prompt())
         eng.open_many(list(range(B)), [voice] * B, [bench.text_ids(b) for b in range(B)],
@@ -44,16 +44,18 @@ def child(out, frames):
 
 def main():
     if sys.argv[1] == "--child":
-        child(sys.argv[2], int(sys.argv[3]))
+        child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
         return
     a, b = sys.argv[1], sys.argv[2]
     frames = int(sys.argv[3]) if len(sys.argv) > 3 else 60
+    bf = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     res = []
     with tempfile.TemporaryDirectory() as d:
         for i, lib in enumerate((a, b)):
             out = os.path.join(d, f"{i}.npz")
             env = dict(os.environ, PTTS_LIB=os.path.abspath(lib))
-            subprocess.run([sys.executable, __file__, "--child", out, str(frames)], env=env, check=True, timeout=300)
+            subprocess.run([sys.executable, __file__, "--child", out, str(frames), str(bf)], env=env, check=True,
+                           timeout=300)
             res.append(np.load(out))
     dp = np.abs(res[0]["pcm"] - res[1]["pcm"]).max(axis=(1, 2))
     dl = np.abs(res[0]["lat"] - res[1]["lat"]).max(axis=(1, 2))
