@@ -42,9 +42,6 @@ int pick_splits(int M, int N, int K) {
 // PTTS_OVR="name=L[:S],...", read at every plan build.
 static void tile_override(const std::string& name, int& layout, int& ksplit) {
   const char* e = probe_env("PTTS_OVR");
-#ifdef PTTS_OVR_BUILTIN  // A/B variant libraries (tools/ab.sh): the override compiled in
-  if (!e) e = PTTS_OVR_BUILTIN;
-#endif
   if (!e) return;
   const std::string s(e);
   size_t p = 0;
@@ -1250,6 +1247,11 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   const bool big = B >= 16;  // B * 16 >= 256 Mimi rows: the LDS-DMA tiles fill the chip
   auto tile = [&](const std::string& op, int small_splits) {
     BackTile t = big ? back_tile(op, pipeline_) : BackTile{0, small_splits};
+    // four-frame passes: SEANet conv0 and the stage-0 transposed conv have twice a pair pass's rows
+    // (B * 64: 256 / 1,024 64 x 64 tiles at B = 32), enough to fill the chip unsplit, so neither
+    // writes slabs nor needs its reduce launch (steady step 0.5179 -> 0.5137 ms,
+    // profiles/r06/ab_quad_splits.txt; unsplit in pair passes: +2.7 %, profiles/r06/ab1.txt)
+    if (big && nfr >= 4 && (op == "seanet.conv0" || op == "seanet.up0.convtr")) t.splits = 1;
     // back_mfma bf16 / bf16x6: the bf16-operand / split-f32 twin of the ILV tile (kernels.hip
     // PTTS_GLB: layout + 100, PTTS_GLX6: + 200); the register-blocked and non-ILV tiles of the f32
     // table map to the 64 x 64 one
@@ -1416,11 +1418,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   // beat the two conv launches: stage 2 (480 workgroups; 22.5 us against 16.8 + 11.0). Stages
   // 0 and 1 have 96 / 160 workgroups of it and measured slower than their two tuned launches.
   // PTTS_RESBLOCK_STAGES (probe builds): bit mask of the stages that fuse.
-#ifdef PTTS_RESBLOCK_DEFAULT
-  int fused_stages = PTTS_RESBLOCK_DEFAULT;
-#else
   int fused_stages = 4;
-#endif
   if (probe_env("PTTS_RESBLOCK_STAGES")) fused_stages = atoi(probe_env("PTTS_RESBLOCK_STAGES"));
   // (f32 only: its own MFMA loop). A fused stage's (unsplit) transposed conv stores no ELU'd copy:
   // the block ELUs the raw rows as they enter LDS

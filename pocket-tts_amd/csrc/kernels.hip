@@ -1022,10 +1022,6 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
     }
 }
 
-#ifdef PTTS_PROBES
-#include "../probes/gemm_per.inc"  // persistent back-part tiles (layouts 40-42), measurement builds only
-#endif
-
 // ---------------------------------------------------------------------------------------------
 // Register-blocked K-split GEMM: each wave accumulates a (32*TM) x (32*TN) block (TM*TN
 // 32x32 accumulators); one A fragment feeds TN MFMAs and one B fragment TM, so operand bytes per
@@ -1523,39 +1519,9 @@ static void launch_split_tail(K kernel, int TM, int TN, int minb, hipStream_t s,
                      cap_lds(kernel, a.max_wg_per_cu), s, b);
 }
 
-#ifdef PTTS_PROBES
-// Persistent tiles (k_gemm_glds_per; probe builds: measured, not adopted): one
-// workgroup per CU slot the launch may hold (the per-CU cap, else MINB), at most one per unit.
-template <typename K>
-static void launch_persist(K kernel, int TM, int TN, int minb, int grid_z, hipStream_t s, const GemmArgs& a) {
-  GemmArgs b = a;
-  b.tiles_n = (a.N + TN - 1) / TN;
-  b.tiles_m = (a.M + TM - 1) / TM;
-  b.units_z = grid_z;
-  b.xcd_pn = choose_xcd_pn(a, b.tiles_n, b.tiles_m);
-  const int cap = std::max(a.max_wg_per_cu, g_wg_cap);
-  const long units = (long)b.tiles_n * b.tiles_m * grid_z;
-  const int G = (int)std::min<long>(units, (long)NUM_CUS * (cap > 0 ? cap : minb));
-  if (G <= 0) return;
-  b.probe = 0;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)G), dim3(256), cap_lds(kernel, cap), s, b);
-}
-#endif
-
 template <int MODE>
 static void gemm_launch(const GemmArgs& a, int grid_z, hipStream_t s) {
   switch (a.layout) {
-#ifdef PTTS_PROBES
-    case 40:  // persistent 64 x 64, 3 buffers (back part)
-      launch_persist((k_gemm_glds_per<MODE, 3, 2>), 64, 64, 2, grid_z, s, a);
-      return;
-    case 41:  // persistent 64 x 64, 4 buffers
-      launch_persist((k_gemm_glds_per<MODE, 4, 2>), 64, 64, 2, grid_z, s, a);
-      return;
-    case 42:  // persistent 64 x 64, 5 buffers (80 KiB: the LDS one capped workgroup holds anyway)
-      launch_persist((k_gemm_glds_per<MODE, 5, 1>), 64, 64, 1, grid_z, s, a);
-      return;
-#endif
 #define PTTS_GLDS(L, WM_, WN_, BK_, NB_)                                                               \
   case L:                                                                                               \
     launch_tiled((k_gemm_glds<MODE, WM_, WN_, BK_, NB_>),                                              \

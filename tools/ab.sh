@@ -7,7 +7,8 @@
 #
 # An arm is a label and a comma-separated list of environment settings ("-" = none); the pseudo
 # setting BENCH=a+b+c appends the bench.py arguments "a b c" for that arm only. The usual ones:
-#   PTTS_LIB=abl/libbase.so                                  a base library (tools/build_base.sh REV)
+#   PTTS_LIB=gpubin/libbase.so                               a base library (tools/build_base.sh REV)
+#   PTTS_LIB=gpubin/libNAME.so                               a patch variant (tools/build_variant.sh NAME PATCH)
 #   PTTS_LIB=pocket-tts_amd/lib-probes/libpocket_tts_hip.so  the measurement build (make -C pocket-tts_amd probes)
 #   PTTS_BACK_PRIO / PTTS_FRONT_PRIO / PTTS_BACK_WG_CAP / PTTS_OVR=op=layout:splits ...  probe knobs
 # Every bench run is under its own time limit; a failing run ends the script (no retries).
