@@ -416,7 +416,7 @@ def main():
     ap.add_argument("--no-quant-variant", action="store_true",
                     help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM), fp8_gemm and "
                          "back_bf16 engines")
-    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2, 4),
+    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2, 4, 8),
                     help="frames per Mimi-decode pass of pipelined stepping (ptts_engine_config.back_frames; "
                          "2, the throughput configuration: 0.559 vs 0.584 ms per steady step, DESIGN.md section 1)")
     ap.add_argument("--back-mfma", choices=("f32", "f32x6"), default="f32",

@@ -89,7 +89,7 @@ typedef struct ptts_engine_config {
                                naming the key): another variant is a rebuild. Checked, not read
                                for shapes. ptts_config_check() is the same check alone. */
   int back_frames;          /* pipelined engines only: frames per Mimi-decode pass, 1 (default;
-                               0 means 1), 2 or 4. With n > 1, frames n j .. n j + n - 1 of every
+                               0 means 1), 2, 4 or 8. With n > 1, frames n j .. n j + n - 1 of every
                                row are decoded by ONE back pass (the streaming codec state advances
                                as for n passes; PCM identical within float rounding), a call
                                returns the frame computed 2 n - 1 calls earlier, and rows admitted

@@ -91,8 +91,8 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_REQUIRE(cfg.fp8_gemm == 0 || cfg.fp8_gemm == 1, "fp8_gemm must be 0 or 1");
   PTTS_REQUIRE(!(cfg.fp8_gemm && cfg.weight_quant != QUANT_NONE), "fp8_gemm and weight_quant are exclusive");
   fp8_ = cfg.fp8_gemm;
-  PTTS_REQUIRE(cfg.back_frames >= 0 && cfg.back_frames <= NFR_MAX && cfg.back_frames != 3,
-               "back_frames must be 0, 1, 2 or 4");
+  PTTS_REQUIRE(cfg.back_frames >= 0 && cfg.back_frames <= NFR_MAX && !(cfg.back_frames & (cfg.back_frames - 1)),
+               "back_frames must be 0, 1, 2, 4 or 8");
   nfr_ = cfg.pipeline && cfg.back_frames >= 2 ? cfg.back_frames : 1;
   PTTS_REQUIRE(cfg.back_mfma >= PTTS_BACK_F32 && cfg.back_mfma <= PTTS_BACK_F32X6, "unknown back_mfma mode");
   back_mfma_ = cfg.back_mfma;

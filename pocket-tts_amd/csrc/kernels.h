@@ -364,13 +364,13 @@ struct FrontCommitArgs {
 };
 void front_commit(const FrontCommitArgs& a, hipStream_t s);
 
-// Frames per back-part pass (ptts_engine_config.back_frames: 1, 2 or 4) and the front -> back
+// Frames per back-part pass (ptts_engine_config.back_frames: 1, 2, 4 or 8) and the front -> back
 // hand-off buffers of the largest pass (three passes' worth: the front part may run two passes ahead)
-constexpr int NFR_MAX = 4;
+constexpr int NFR_MAX = 8;
 constexpr int NHB_MAX = 3 * NFR_MAX;
 
 // Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0, for
-// nfr (1, 2 or 4) consecutive frames of every row: latent[f] [B][32] -> x [B][16 nfr][512] (frame
+// nfr (1, 2, 4 or 8) consecutive frames of every row: latent[f] [B][32] -> x [B][16 nfr][512] (frame
 // f at rows 16 f..), h = LN(x). The overlap-add history [B][512] is read from qprev_in (frame 0;
 // frame f > 0 overlaps frame f - 1); the quantized rows of the pass go to qprev_out
 // [B][NFR_MAX][512], and the commit copies the last valid frame's into the history (rows without a

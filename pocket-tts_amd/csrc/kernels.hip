@@ -3288,7 +3288,7 @@ __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
     const float* wqf = reinterpret_cast<const float*>(wqr[u]);
     const float* w0 = reinterpret_cast<const float*>(&wur[u][0]);
     const float* w1 = reinterpret_cast<const float*>(&wur[u][1]);
-    float q[NFR_MAX] = {0.f, 0.f, 0.f, 0.f};
+    float q[NFR_MAX] = {};
 #pragma unroll
     for (int g = 0; g < NFR_MAX; ++g)
       if (g < a.nfr) {
@@ -3335,7 +3335,7 @@ __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
 void quant_upsample(const float* const latent[NFR_MAX], const FrameFlags* const fl[NFR_MAX], int nfr, int B, const float* emb_std,
                     const float* emb_mean, const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
                     float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s) {
-  if (nfr != 1 && nfr != 2 && nfr != 4) throw std::runtime_error("quant_upsample: 1, 2 or 4 frames");
+  if (nfr < 1 || nfr > NFR_MAX || (nfr & (nfr - 1))) throw std::runtime_error("quant_upsample: 1, 2, 4 or 8 frames");
   QuantUpArgs a{};
   for (int g = 0; g < NFR_MAX; ++g) {
     a.latent[g] = latent[g < nfr ? g : 0];

@@ -752,7 +752,7 @@ def main(argv=None):
     ap.add_argument("--max-ctx", type=int, default=1024)
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
-    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2, 4),
+    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2, 4, 8),
                     help="frames per Mimi decode pass (ptts_engine_config.back_frames): 2, the throughput "
                          "configuration bench.py measures (two more calls of frame lag, ~1.2 ms at B = 32)")
     ap.add_argument("--stand-in-engine", action="store_true",
