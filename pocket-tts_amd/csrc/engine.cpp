@@ -1570,6 +1570,11 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
   PTTS_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
   // back part of a pipelined step: its launches leave room for the concurrent front part
   set_wg_cap(part == 1 && pipeline_ ? back_cap_ : 0);
+  // the back part's tile waves issue at priority 3 beside the front part's (pair passes: steady step
+  // 0.5533 -> 0.5496 ms, devfn.h back_prio), except in four-frame passes, whose back part has four
+  // steps' time per pass: there the front part's waves keep the default order (0.5134 -> 0.5106
+  // ms, profiles/r06/ab_bf8.txt)
+  set_back_hi(part == 1 && pipeline_ && nfr_ >= 4 ? 0 : 1);
   // per-op cap override for back-part launches: PTTS_OP_CAP="name=cap,..." (tuning)
   const char* opcap = part == 1 && pipeline_ ? probe_env("PTTS_OP_CAP") : nullptr;
   try {
@@ -1619,10 +1624,12 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
 #endif
   } catch (...) {
     set_wg_cap(0);
+    set_back_hi(1);
     (void)hipStreamEndCapture(cs, &g);
     throw;
   }
   set_wg_cap(0);
+  set_back_hi(1);
   PTTS_HIP(hipStreamEndCapture(cs, &g));
   hipGraphExec_t ge = nullptr;
   PTTS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));

@@ -101,6 +101,8 @@ struct GemmArgs {
   int w_nt;
   // 1: a launch of the front part (FlowLM / flow head): its waves take the front issue priority
   int front;
+  // 1: a back-part launch whose waves issue at priority 3 (set by the launcher from set_back_hi)
+  int back_hi;
   // measurement probe, -DPTTS_PROBES builds only (tools/; PTTS_BACK_PROBE: back-part launches of a
   // pipelined step, PTTS_FRONT_PROBE: all other tiled launches; results are wrong): bit 0 skips
   // the MFMAs, bit 1 the operand loads of the K loop. Ignored by product builds.
@@ -319,6 +321,10 @@ struct FlowHeadArgs {
 // Launches issued while a cap > 0 is set reserve dynamic LDS so that at most `cap` workgroups of
 // each kernel share a CU (0 = no cap). Per host thread; the engine sets it around graph capture.
 void set_wg_cap(int cap);
+// Issue priority of the back part's tile waves (k_gemm_glds outside the front part, k_gemm_rb,
+// k_resblock) for the launches made on this host thread from now on: 1 (default) s_setprio 3,
+// 0 none. Set while a back graph is captured (engine.cpp part_graph).
+void set_back_hi(int on);
 #ifdef PTTS_PROBES
 // one {tag, s_memrealtime} record appended to a device ring (tools/stamps.py)
 constexpr unsigned STAMP_CAP = 1u << 16;
@@ -468,6 +474,7 @@ struct ResBlockArgs {
   // E == R (the raw transposed-conv output): the k3 conv's input is elu(R), applied as the rows
   // enter LDS, so the transposed conv stores no ELU'd copy (HE stays ELU'd: the commit ELUs it)
   int e_raw = 0;
+  int back_hi = 1;  // issue priority 3 (set by the launcher from set_back_hi)
 };
 constexpr int RESBLOCK_FIN_TT = 128;  // stage-2 time tile (the side buffer's granularity)
 void resblock(const ResBlockArgs& a, hipStream_t s);

@@ -30,6 +30,8 @@ namespace ptts {
 // Per host thread: engines of one process (serve --gpus N threads) capture graphs concurrently.
 static thread_local int g_wg_cap = 0;
 void set_wg_cap(int cap) { g_wg_cap = cap; }
+static thread_local int g_back_hi = 1;
+void set_back_hi(int on) { g_back_hi = on; }
 #ifdef PTTS_PROBES
 __device__ int g_front_prio = 0;
 void set_front_prio(int prio) {
@@ -663,7 +665,7 @@ template <int MODE, int WM, int WN, int BK, int NBUF, int TMW = 1, int TNW = 1, 
           int PREC = 0>
 __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
   if (a.front) front_prio();
-  else back_prio();
+  else if (a.back_hi) back_prio();
   constexpr bool BF16 = PREC == 1, X6 = PREC == 2;
   constexpr int TM = 32 * WM * TMW, TN = 32 * WN * TNW, ROWS = TM + TN;
   constexpr int CPR = BK / 4;        // 16-byte columns per LDS row
@@ -1031,7 +1033,7 @@ __global__ __launch_bounds__(256, MINB) void k_gemm_glds(GemmArgs a) {
 // ---------------------------------------------------------------------------------------------
 template <int MODE, int TM, int TN>
 __global__ __launch_bounds__(256) void k_gemm_rb(GemmArgs a) {
-  back_prio();
+  if (a.back_hi) back_prio();
   __shared__ float red[4 * 16 * 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1484,6 +1486,7 @@ template <typename K>
 static void launch_tiled(K kernel, dim3 grid, int threads, hipStream_t s, const GemmArgs& a) {
   GemmArgs b = a;
   b.xcd_pn = choose_xcd_pn(a, (int)grid.x, (int)grid.y);
+  b.back_hi = g_back_hi;
 #ifdef PTTS_PROBES
   b.probe = g_wg_cap > 0 ? back_probe() : front_probe();  // the cap is set exactly while the back part is captured
 #endif
@@ -3589,7 +3592,7 @@ void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols
 // =============================================================================================
 template <int C, int H, int TT>
 __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
-  back_prio();
+  if (a.back_hi) back_prio();
   constexpr int LDE = C + 4, LDV = H + 4;
   __shared__ __attribute__((aligned(16))) float sm[(TT + 2) * LDE + TT * LDV];
   float* sE = sm;
@@ -3739,7 +3742,9 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
   }
 }
 
-void resblock(const ResBlockArgs& a, hipStream_t s) {
+void resblock(const ResBlockArgs& ra, hipStream_t s) {
+  ResBlockArgs a = ra;
+  a.back_hi = g_back_hi;
   // time tiles: stage 0 32 rows (96 workgroups), stage 1 96 (160), stage 2 128 (480) at B = 32
   if (a.C == 256 && a.T % 32 == 0)
     hipLaunchKernelGGL((k_resblock<256, 128, 32>), dim3(a.T / 32, a.B), dim3(256),
