@@ -1240,8 +1240,9 @@ static BackTile back_tile(const std::string& op, bool pipeline) {
 
 // BACK part of a step: Mimi decode of the frames the front part left in buffer `hb`; `qp` is the
 // frame's parity for the quantizer history (the previous frame's quantizer output is in qp ^ 1).
-void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
+void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp, int pcm_frames) {
   PTTS_REQUIRE(nfr >= 1 && nfr <= nfr_, "frames per back pass out of range");
+  PTTS_REQUIRE(pcm_frames >= nfr, "pass block smaller than the pass");
   int hbs[NFR_MAX];  // frame f's hand-off buffer (f < nfr)
   for (int f = 0; f < NFR_MAX; ++f) hbs[f] = (hb + std::min(f, nfr - 1)) % nhb_;
   const bool big = B >= 16;  // B * 16 >= 256 Mimi rows: the LDS-DMA tiles fill the chip
@@ -1412,7 +1413,9 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
   }
   const float* cin_buf = a0_;
   int T = 16 * nfr, ch = 512;
-  float* pcm_out = nfr == 1 ? pcm_[hb] : pcmp_[hb / nfr];  // a pass's PCM is [B][nfr][1920]
+  // a pass's PCM is [B][pcm_frames][1920] in its pass block (frames past nfr untouched)
+  float* pcm_out = pcm_frames == 1 ? pcm_[hb] : pcmp_[hb / pcm_frames];
+  const long pcm_ld = (long)pcm_frames * FRAME;
   bool fin_fused = false;  // the final conv ran in the stage-2 residual block's epilogue
   // fused residual blocks (k3 conv + ELU + k1 conv + skip + ELU, the hidden rows in LDS) where they
   // beat the two conv launches: stage 2 (480 workgroups; 22.5 us against 16.8 + 11.0). Stages
@@ -1469,6 +1472,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
         rb.fb = W(L_.dfin_b);
         rb.fH = hist_[7];
         rb.fout = pcm_out;
+        rb.fld = pcm_ld;
         rb.fside = fin_side_;
         fin_fused = true;
         fl += 2.0 * B * T * 3 * 64;
@@ -1488,7 +1492,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
     const float *X = ca_[2], *H = hist_[7], *w = W(L_.dfin_w), *b = W(L_.dfin_b);
     float* Y = pcm_out;
     const int TF = FRAME * nfr;
-    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, TF, 64, 3, w, b, Y, 0, s); },
+    ops.push_back({"seanet.conv_final", [=](hipStream_t s) { conv_cout1(X, H, B, TF, 64, 3, w, b, Y, 0, s, pcm_ld); },
                    2.0 * B * TF * 3 * 64, 4.0 * ((double)B * TF * 64 + B * 2.0 * 64 + B * TF + 3 * 64 + 1)});
   }
   // ---- commit of the back part: conv histories and Mimi positions of rows with a frame
@@ -1509,6 +1513,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
       c.fin_pcm = pcm_out;
       c.fin_side = fin_side_;
       c.fin_T = FRAME * nfr;
+      c.fin_ld = pcm_ld;
     }
     double hb_bytes = 0;  // every history row is read from its activation and stored
     for (int i = 0; i < 8; ++i) hb_bytes += 8.0 * B * hist_P_[i] * hist_C_[i];
@@ -1520,7 +1525,7 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp) {
 std::vector<Op> Engine::build_step(int B) {
   std::vector<Op> ops;
   build_front(ops, B, 0);
-  build_back(ops, B, 0, nfr_, 0);
+  build_back(ops, B, 0, nfr_, 0, nfr_);
   return ops;
 }
 
@@ -1556,14 +1561,14 @@ std::vector<std::string> Engine::plan_names(int B) {
   return v;
 }
 
-hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp) {
-  if (part == 0) qp = 0;  // the front part does not use the quantizer history
-  const int key = ((B * 2 + part) * NHB + hb) * 2 + qp;
+hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp, int nfr) {
+  if (part == 0) qp = nfr = 0;  // the front part does not use the quantizer history
+  const int key = (((B * 2 + part) * NHB + hb) * 2 + qp) * (NFR_MAX + 1) + nfr;
   auto it = graphs_.find(key);
   if (it != graphs_.end()) return it->second;
   std::vector<Op> ops;
   if (part == 0) build_front(ops, B, hb);
-  else build_back(ops, B, hb, nfr_, qp);
+  else build_back(ops, B, hb, nfr, qp, nfr_);
   hipGraph_t g = nullptr;
   // captured on the stream it is launched on (the back part of a pipelined step: stream_be_)
   hipStream_t cs = part == 1 && pipeline_ ? stream_be_ : stream_;
@@ -1679,14 +1684,14 @@ void Engine::call_async(int B, bool run_front) {
   prev_rows_ = out_rows_;
   const int hb = (int)(k_ % nhb_), qp = (int)(k_ & 1);
   // the front part of this call, or (a flush) its hand-off buffer marked frame-less
-  hipGraphExec_t front = B > 0 ? part_graph(0, B, hb, 0) : nullptr;
+  hipGraphExec_t front = B > 0 ? part_graph(0, B, hb, 0, 0) : nullptr;
   auto run_front_part = [&]() {
     if (front && xh_dirty_) refresh_xh();
     if (front) PTTS_HIP(hipGraphLaunch(front, stream_));
     else PTTS_HIP(hipMemsetAsync(flags_[hb], 0, sizeof(FrameFlags) * max_slots_, stream_));
   };
   if (!pipeline_) {
-    hipGraphExec_t back = part_graph(1, B, hb, qp);
+    hipGraphExec_t back = part_graph(1, B, hb, qp, 1);
     run_front_part();
     PTTS_HIP(hipGraphLaunch(back, stream_));
     out_hb_ = hb;
@@ -1717,10 +1722,17 @@ void Engine::call_async(int B, bool run_front) {
     if (kr == nf - 1) PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
     if (kr == 0 && k_ >= nf) {
       const int h0 = (int)((k_ - nf) % nhb_), pq = (int)(((k_ - nf) / nf) & 1);
-      int rows = 0;
-      for (int f = 0; f < nf; ++f) rows = std::max(rows, rows_hb_[(h0 + f) % nhb_]);
+      // rows: the largest row count of the pass's calls (the first: a call inside a pass covers at
+      // most the previous call's rows); nfe: the calls that started frames (the rest were flushes,
+      // e.g. a job's drain), the only frames the pass decodes
+      int rows = 0, nfe = 0;
+      for (int f = 0; f < nf; ++f) {
+        const int r = rows_hb_[(h0 + f) % nhb_];
+        rows = std::max(rows, r);
+        if (r > 0 && nfe == f) nfe = f + 1;
+      }
       if (rows > 0) {  // no pass when every call of the pass was a flush
-        hipGraphExec_t back = part_graph(1, rows, h0, pq);
+        hipGraphExec_t back = part_graph(1, rows, h0, pq, nfe);
         PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[(h0 + nf - 1) % nhb_], 0));
         if (admit_pending_) {
           PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
@@ -1740,7 +1752,7 @@ void Engine::call_async(int B, bool run_front) {
     run_front_part();
     PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
     if (prev_rows > 0) {
-      hipGraphExec_t back = part_graph(1, prev_rows, hb1, qp1);
+      hipGraphExec_t back = part_graph(1, prev_rows, hb1, qp1, 1);
       PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_front_[hb1], 0));
       if (admit_pending_) {  // slot state rewritten since the front part this back part decodes
         PTTS_HIP(hipStreamWaitEvent(stream_be_, ev_admit_, 0));
@@ -2611,7 +2623,7 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
                             hipMemcpyHostToDevice, stream_));
     PTTS_HIP(hipMemcpyAsync(flags_[par] + slot, &on, sizeof on, hipMemcpyHostToDevice, stream_));
     std::vector<Op> ops;
-    build_back(ops, slot + 1, par, 1, par);
+    build_back(ops, slot + 1, par, 1, par, 1);
     size_t j = 0;
     for (; j < ops.size(); ++j) {
       if (ops[j].name == "seanet.conv0" && tr) rows16(tr + (size_t)i * UP * MD, mx_);

@@ -95,9 +95,13 @@ class Engine {
   // hb: front -> back hand-off buffer (frame index mod NHB); qp: parity of the back part's
   // quantizer history (frame index mod 2; the back part reads the previous frame's half)
   void build_front(std::vector<Op>& ops, int B, int hb);
-  // back part over nfr consecutive frames from hand-off buffers hb, hb + 1, .. hb + nfr - 1
-  void build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp);
-  hipGraphExec_t part_graph(int part, int B, int hb, int qp);
+  // back part over nfr consecutive frames from hand-off buffers hb, hb + 1, .. hb + nfr - 1; the
+  // PCM goes to the pass block of hb (pcm_frames frames per row, pcmp_) or, with pcm_frames 1, to
+  // pcm_[hb]
+  void build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp, int pcm_frames);
+  // multi-frame passes: a pass whose later calls were all flushes decodes only the frames its
+  // calls started (nfr in part_graph's key)
+  hipGraphExec_t part_graph(int part, int B, int hb, int qp, int nfr);
   void push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r);
   void flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag);
   void linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M, const float* Wt,

@@ -410,6 +410,7 @@ struct CommitArgs {
   float* fin_pcm = nullptr;
   const float* fin_side = nullptr;
   int fin_T = 0;
+  long fin_ld = 0;  // fin_pcm's row stride (0: fin_T)
 };
 void step_commit(const CommitArgs& a, hipStream_t s);
 
@@ -452,9 +453,10 @@ void embed_gather(const int* ids, int n, const float* table, int dim, float* out
 void copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, hipStream_t s);
 
 // out[m] = sum_k x[m*ldx + k] * w[k] + b  (tiny GEMV column, e.g. the N=1 final conv)
-// Streaming conv with Cout == 1: pcm[b][t] = bias + sum_{j,ci} elu(xin)[...] * w[j][ci].
+// Streaming conv with Cout == 1: pcm[b][t] = bias + sum_{j,ci} elu(xin)[...] * w[j][ci] (Y's row
+// stride ldy, 0: T).
 void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, const float* w, const float* bias,
-                float* Y, int elu_in, hipStream_t s);
+                float* Y, int elu_in, hipStream_t s, long ldy = 0);
 
 // Fused SEANet residual block of one decoder stage (seanet.rs:43-89, kernels [3, 1], true skip):
 // Y = elu(R + b1 + conv_k1(elu(b3 + conv_k3(E)))) over [B][T][C] channels-last rows, E's two rows
@@ -475,6 +477,7 @@ struct ResBlockArgs {
   // enter LDS, so the transposed conv stores no ELU'd copy (HE stays ELU'd: the commit ELUs it)
   int e_raw = 0;
   int back_hi = 1;  // issue priority 3 (set by the launcher from set_back_hi)
+  long fld = 0;     // fout's row stride (0: T; a pass block of more frames than this launch covers)
 };
 constexpr int RESBLOCK_FIN_TT = 128;  // stage-2 time tile (the side buffer's granularity)
 void resblock(const ResBlockArgs& a, hipStream_t s);

@@ -3369,7 +3369,8 @@ __global__ __launch_bounds__(256) void k_commit(CommitArgs a) {
   if (a.fin_side) {  // every row (as the final conv computes every row): tile-boundary shares
     const int nx = a.fin_T / RESBLOCK_FIN_TT;
     for (int e = 2 + threadIdx.x; e < 2 * nx; e += 256)
-      a.fin_pcm[(long)b * a.fin_T + (e >> 1) * RESBLOCK_FIN_TT + (e & 1)] += a.fin_side[(long)b * 2 * nx + e];
+      a.fin_pcm[(long)b * (a.fin_ld ? a.fin_ld : a.fin_T) + (e >> 1) * RESBLOCK_FIN_TT + (e & 1)] +=
+          a.fin_side[(long)b * 2 * nx + e];
   }
   int nv = 0;  // valid frames: a prefix
   while (nv < a.nfr && a.flags[nv][b].valid) ++nv;
@@ -3732,7 +3733,7 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
       const float d0 = sD[r], d1 = sD[(TT + 2) + r + 1], d2 = sD[2 * (TT + 2) + r + 2];
       // rows 0, 1 of a later tile: the terms from this tile's rows only (the rest via the side buffer)
       const float v = r >= 2 || t0 == 0 ? ((d0 + d1) + d2) + fb : (r == 0 ? d2 : d1 + d2) + fb;
-      a.fout[(long)b * a.T + t0 + r] = v;
+      a.fout[(long)b * (a.fld ? a.fld : a.T) + t0 + r] = v;
     } else if (tid < TT + 2 && x + 1 < nx) {  // this tile's share of the next tile's rows 0, 1
       const int k = tid - TT;
       const float v = k == 0 ? sD[TT] + sD[(TT + 2) + TT + 1]  // d0[TT-2] + d1[TT-1]
@@ -3761,7 +3762,8 @@ void resblock(const ResBlockArgs& ra, hipStream_t s) {
 
 template <int KT>
 __global__ __launch_bounds__(256) void k_conv_cout1(const float* X, const float* H, int B, int T, int cin,
-                                                    const float* w, const float* bias, float* Y, int elu_in) {
+                                                    const float* w, const float* bias, float* Y, int elu_in,
+                                                    long ldy) {
   constexpr int P = KT - 1, ROWS = 64 + P;
   __shared__ float tile[4][ROWS][65];
   __shared__ float sw[KT * 64];
@@ -3787,15 +3789,15 @@ __global__ __launch_bounds__(256) void k_conv_cout1(const float* X, const float*
   for (int c = 0; c < 64; ++c)
 #pragma unroll
     for (int j = 0; j < KT; ++j) acc += sw[j * 64 + c] * tile[wave][lane + j][c];
-  if (live && t0 + lane < T) Y[(long)b * T + t0 + lane] = acc + bias[0];
+  if (live && t0 + lane < T) Y[(long)b * ldy + t0 + lane] = acc + bias[0];
 }
 
 void conv_cout1(const float* X, const float* H, int B, int T, int cin, int k, const float* w, const float* bias,
-                float* Y, int elu_in, hipStream_t s) {
+                float* Y, int elu_in, hipStream_t s, long ldy) {
   const long waves = (long)B * ((T + 63) / 64);  // one lane per input channel: cin == 64, k == 3
   (void)k;
   hipLaunchKernelGGL(k_conv_cout1<3>, dim3((unsigned)((waves + 3) / 4)), dim3(256), cap_lds(k_conv_cout1<3>, g_wg_cap), s, X, H, B, T, cin, w, bias,
-                     Y, elu_in);
+                     Y, elu_in, ldy > 0 ? ldy : (long)T);
 }
 
 // Encoder first conv (1 -> cout, k taps, zero history of k-1 samples): one thread per output.

@@ -87,6 +87,10 @@ def main():
     ap.add_argument("--port", type=int, default=8765)
     ap.add_argument("--out", default="")
     ap.add_argument("--workdir", default=os.path.join(HERE, "..", "gpurun_out"))
+    ap.add_argument("--back-frames", type=int, default=2, help="the server's frames per Mimi decode pass")
+    ap.add_argument("--trace", action="store_true",
+                    help="run the server with PTTS_SERVE_TRACE=1 and report the medians of its per-request "
+                         "submit -> admission and submit -> first frame times")
     args = ap.parse_args()
 
     import httpx
@@ -95,9 +99,13 @@ def main():
     prompt_path = os.path.join(args.workdir, "serve_load_prompt.npy")
     np.save(prompt_path, (0.11 * np.random.default_rng(1).standard_normal((125, 1024))).astype(np.float32))
     env = dict(os.environ, PYTHONPATH=os.path.abspath(PKG) + os.pathsep + os.environ.get("PYTHONPATH", ""))
-    log = open(os.path.join(args.workdir, "serve_load_server.log"), "w")
+    if args.trace:
+        env["PTTS_SERVE_TRACE"] = "1"
+    log_path = os.path.join(args.workdir, "serve_load_server.log")
+    log = open(log_path, "w")
     server = subprocess.Popen([sys.executable, "-m", "pocket_tts_amd.serve", "--voice", f"synth={prompt_path}",
-                               "--slots", "32", "--max-ctx", "480", "--port", str(args.port)],
+                               "--slots", "32", "--max-ctx", "480", "--port", str(args.port),
+                               "--back-frames", str(args.back_frames)],
                               env=env, stdout=log, stderr=subprocess.STDOUT)
     try:
         base = f"http://127.0.0.1:{args.port}"
@@ -110,7 +118,7 @@ def main():
             except httpx.HTTPError:
                 time.sleep(0.1)
         result = {"clients": args.clients, "procs": args.procs, "route": "/stream", "seconds_per_round": args.seconds,
-                  "rounds": []}
+                  "back_frames": args.back_frames, "rounds": []}
         per = [args.clients // args.procs + (1 if p < args.clients % args.procs else 0) for p in range(args.procs)]
         for rnd in range(args.rounds):
             procs, first = [], 0
@@ -156,7 +164,18 @@ def main():
         med = lambda k: float(np.median([r[k] for r in result["rounds"] if r[k] is not None]))
         result["median"] = {k: round(med(k), 2) for k in ("audio_sec_per_wall_sec", "ttfc_burst_p50_ms",
                                                           "ttfc_steady_p50_ms", "ttfc_steady_p90_ms")}
-        print(json.dumps({"median": result["median"]}), flush=True)
+        if args.trace:  # the server's own per-request stamps (serve.py BatchScheduler._deliver)
+            log.flush()
+            tr = {"admit_wait_ms": [], "first_ms": [], "first_to_chunk0_ms": []}
+            for line in open(log_path):
+                if line.startswith("ptts-serve slot"):
+                    w = line.split()
+                    for k in tr:
+                        if k in w:
+                            tr[k].append(float(w[w.index(k) + 1]))
+            result["server_trace_median"] = {k: round(float(np.median(v)), 3) for k, v in tr.items() if v}
+            result["server_trace_median"]["requests"] = len(tr["first_ms"])
+        print(json.dumps({"median": result["median"], "trace": result.get("server_trace_median")}), flush=True)
         r = httpx.post(base + "/v1/audio/speech", json={"token_ids": ids(0), "words": 20, "response_format": "wav"}, timeout=120)
         r.raise_for_status()
         result["openai_wav_bytes"] = len(r.content)
