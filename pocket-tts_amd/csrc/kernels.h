@@ -376,7 +376,7 @@ constexpr int NFR_MAX = 8;
 constexpr int NHB_MAX = 3 * NFR_MAX;
 
 // Denorm + 1x1 quantizer conv + depthwise ConvTrUpsample1d (k32 s16) + LN of Mimi layer 0, for
-// nfr (1, 2, 4 or 8) consecutive frames of every row: latent[f] [B][32] -> x [B][16 nfr][512] (frame
+// nfr (1 .. NFR_MAX; a partial pass may cover 3) consecutive frames of every row: latent[f] [B][32] -> x [B][16 nfr][512] (frame
 // f at rows 16 f..), h = LN(x). The overlap-add history [B][512] is read from qprev_in (frame 0;
 // frame f > 0 overlaps frame f - 1); the quantized rows of the pass go to qprev_out
 // [B][NFR_MAX][512], and the commit copies the last valid frame's into the history (rows without a

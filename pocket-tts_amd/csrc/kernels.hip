@@ -3338,7 +3338,7 @@ __global__ __launch_bounds__(256) void k_quant_upsample(QuantUpArgs a) {
 void quant_upsample(const float* const latent[NFR_MAX], const FrameFlags* const fl[NFR_MAX], int nfr, int B, const float* emb_std,
                     const float* emb_mean, const float* wq, const float* wup, const float* qprev_in, float* qprev_out,
                     float* x, float* h, const float* ln_w, const float* ln_b, hipStream_t s) {
-  if (nfr < 1 || nfr > NFR_MAX || (nfr & (nfr - 1))) throw std::runtime_error("quant_upsample: 1, 2, 4 or 8 frames");
+  if (nfr < 1 || nfr > NFR_MAX) throw std::runtime_error("quant_upsample: 1 to NFR_MAX frames");
   QuantUpArgs a{};
   for (int g = 0; g < NFR_MAX; ++g) {
     a.latent[g] = latent[g < nfr ? g : 0];
