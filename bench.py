@@ -416,9 +416,10 @@ def main():
     ap.add_argument("--no-quant-variant", action="store_true",
                     help="skip the extra jobs on the int8-weight (weight_quant = QUANT_FLOW_LM), fp8_gemm and "
                          "back_bf16 engines")
-    ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2, 4, 8),
+    ap.add_argument("--back-frames", type=int, default=4, choices=(1, 2, 4, 8),
                     help="frames per Mimi-decode pass of pipelined stepping (ptts_engine_config.back_frames; "
-                         "2, the throughput configuration: 0.559 vs 0.584 ms per steady step, DESIGN.md section 1)")
+                         "4, the throughput configuration: 0.505 ms per steady step against 0.522 with 2, 0.529 "
+                         "with 8 and 0.62 with 1, DESIGN.md section 14)")
     ap.add_argument("--back-mfma", choices=("f32", "f32x6"), default="f32",
                     help="the back part's f32 GEMMs: f32 MFMA, or f32 products from exact three-piece bf16 "
                          "splits (ptts_engine_config.back_mfma PTTS_BACK_F32X6, f32 accuracy)")

@@ -1,6 +1,6 @@
 """GPU parity at the benchmark's own shape (BASELINE configs[2]): f32 engine, 32 rows, 125-frame
 voice prompts, 40 text tokens, 132 free-running frames at temperature 0, pipelined stepping with
-frame pairs (the bench's mode: one Mimi decode pass per two frames), four frames and one frame per pass, and
+four frames per Mimi decode pass (the bench's mode since round 6), frame pairs and one frame per pass, and
 with frame pairs on the bf16x6 back part (back_mfma = BACK_F32X6: f32 GEMMs as exact bf16 piece
 products) at the same gates. The FlowLM context of every row grows 165 -> 297 positions, so the step attention
 (k_attn_decode_qkv) takes its second 256-key round for the last 40 frames, and the Mimi decoder's

@@ -24,7 +24,7 @@ python tools/prof_ops.py piped "$OUT/prof/run_kernel_trace.csv" "$OUT/bench_ops.
 for C in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   T=$(echo "$C" | cut -d' ' -f1)
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace -d "$OUT/pmc_$T" -o run --output-format csv \
-      -- python "$ROOT/bench.py" --profile-frames 6 --warmup 2 $NOVAR --no-op-times > "$OUT/pmc_$T.log" 2>&1) \
+      -- python "$ROOT/bench.py" --profile-frames ${PMC_FRAMES:-12} --warmup 2 $NOVAR --no-op-times > "$OUT/pmc_$T.log" 2>&1) \
     || { echo "pmc $C failed"; tail -n 5 "$OUT/pmc_$T.log"; exit 1; }
   for c in $C; do
     python tools/prof_ops.py counters "$OUT/pmc_$T/run_counter_collection.csv" "$OUT/bench_ops.json" $c \
