@@ -1421,7 +1421,10 @@ void Engine::build_back(std::vector<Op>& ops, int B, int hb, int nfr, int qp, in
   // beat the two conv launches: stage 2 (480 workgroups; 22.5 us against 16.8 + 11.0). Stages
   // 0 and 1 have 96 / 160 workgroups of it and measured slower than their two tuned launches.
   // PTTS_RESBLOCK_STAGES (probe builds): bit mask of the stages that fuse.
-  int fused_stages = 4;
+  // Four-frame passes give stages 0 and 1 four times their single-frame workgroups (384 / 640 at
+  // B = 32), and there the fused block of every stage pays: 0.5049 -> 0.5008 ms
+  // (profiles/r06/ab_resblock.txt; stage 1 fused in pair passes: +0.8 %, round 5)
+  int fused_stages = nfr >= 4 ? 7 : 4;
   if (probe_env("PTTS_RESBLOCK_STAGES")) fused_stages = atoi(probe_env("PTTS_RESBLOCK_STAGES"));
   // (f32 only: its own MFMA loop). A fused stage's (unsplit) transposed conv stores no ELU'd copy:
   // the block ELUs the raw rows as they enter LDS

@@ -3602,14 +3602,25 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int b = blockIdx.y, t0 = blockIdx.x * TT;
-  // ---- E rows t0-2 .. t0+TT-1 (history rows for t < 0) into LDS
-  constexpr int C4 = C / 4;
-  for (int e = tid; e < (TT + 2) * C4; e += 256) {
+  // ---- E rows t0-2 .. t0+TT-1 (history rows for t < 0) into LDS: every load of the thread is
+  // issued before the first LDS store (one memory round trip, not one per 256-thread sweep)
+  constexpr int C4 = C / 4, NE = ((TT + 2) * C4 + 255) / 256;
+  float4 ev[NE];
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int e = min(tid + 256 * i, (TT + 2) * C4 - 1);  // a clamped duplicate, never stored
     const int row = e / C4, c4 = e - row * C4;
     const int t = t0 - 2 + row;
     const float* src = t >= 0 ? a.E + ((long)b * a.T + t) * C : a.HE + ((long)b * 2 + (t + 2)) * C;
-    float4 v = *reinterpret_cast<const float4*>(src + 4 * c4);
-    if (a.e_raw && t >= 0) v = make_float4(elu1(v.x), elu1(v.y), elu1(v.z), elu1(v.w));
+    ev[i] = *reinterpret_cast<const float4*>(src + 4 * c4);
+  }
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int e = tid + 256 * i;
+    if (e >= (TT + 2) * C4) break;
+    const int row = e / C4, c4 = e - row * C4;
+    float4 v = ev[i];
+    if (a.e_raw && t0 - 2 + row >= 0) v = make_float4(elu1(v.x), elu1(v.y), elu1(v.z), elu1(v.w));
     *reinterpret_cast<float4*>(sE + row * LDE + 4 * c4) = v;
   }
   __syncthreads();
@@ -3667,6 +3678,11 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
   for (int blk = wave; blk < MB * NB2; blk += 4) {
     const int mi = blk / NB2, ni = blk - mi * NB2;
     const float* wrow = a.W1 + (long)(32 * ni + r) * H + 16 * h;
+    const int col = 32 * ni + r;
+    const long base = ((long)b * a.T + t0) * C + col;
+    float rv[16];  // the skip rows, requested ahead of the MFMAs that they do not depend on
+#pragma unroll
+    for (int g = 0; g < 16; ++g) rv[g] = a.R[base + (long)(32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h) * C];
     floatx16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
@@ -3684,12 +3700,7 @@ __global__ __launch_bounds__(256) void k_resblock(ResBlockArgs a) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[j], bf[j], acc, 0, 0, 0);
     }
-    const int col = 32 * ni + r;
     const float bias = a.b1[col];
-    const long base = ((long)b * a.T + t0) * C + col;
-    float rv[16];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) rv[g] = a.R[base + (long)(32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h) * C];
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int row = 32 * mi + (g & 3) + 8 * (g >> 2) + 4 * h;
