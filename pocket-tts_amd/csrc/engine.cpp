@@ -179,6 +179,9 @@ Engine::Engine(const ptts_engine_config& cfg) {
   tickets_ = (int*)dalloc(TICKETS);  // zero; every split-tail launch leaves them zero
   ids_dev_ = (int*)dalloc(PREFILL);
   rowtab_dev_ = (int*)dalloc(PREFILL);
+  ctab_dev_ = (int*)dalloc(PREFILL);
+  qrow_dev_ = (int*)dalloc(PREFILL);
+  orow_dev_ = (int*)dalloc(PREFILL);
   admit_slots_ = (int*)dalloc(B);
   admit_st_ = (SlotState*)dalloc((sizeof(SlotState) * B + 3) / 4);
   admit_fpos_ = (int*)dalloc(B);
@@ -253,7 +256,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_HIP(hipHostMalloc((void**)&h_st_, sizeof(SlotState) * B, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_fp_, sizeof(int) * B, hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_ids_, sizeof(int) * PREFILL, hipHostMallocDefault));
-  PTTS_HIP(hipHostMalloc((void**)&h_tab_, sizeof(int) * PREFILL, hipHostMallocDefault));
+  PTTS_HIP(hipHostMalloc((void**)&h_tab_, sizeof(int) * 4 * PREFILL, hipHostMallocDefault));  // ptab | ctab | qrow | orow
   PTTS_HIP(hipHostMalloc((void**)&h_vpre_, sizeof(float*) * (B + 1), hipHostMallocDefault));
   PTTS_HIP(hipHostMalloc((void**)&h_vlen_, sizeof(int) * (B + 1), hipHostMallocDefault));
   memset(h_vpre_, 0, sizeof(float*) * (B + 1));
@@ -897,7 +900,13 @@ void Engine::flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool o
       }
       const float* Q = q_;
       float* O = o_;
-      ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, M, NH, map, kv, 0, qg, O, s); }});
+      RowMap am = map;  // compact admission: the attention runs on the padded 16-row groups
+      int Ma = M;
+      if (map.ptab) {
+        am.tab = map.ptab;
+        Ma = map.mpad;
+      }
+      ops.push_back({p + ".attention", [=](hipStream_t s) { attention(Q, Ma, NH, am, kv, 0, qg, O, s); }});
     }
     auto rr = [&](const std::string& name, int S2, int N, int act, bool resid, float* Y, const float* lnw,
                   const float* lnb, bool ln, float* Hout, float* Hfrag = nullptr) {
@@ -2463,29 +2472,53 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     }
     off += n_ids[i];
   }
+  // The GEMMs, reduces and RoPE run on the tokens only (Tc compact rows: 40 tokens are 40 rows, not
+  // 48); the attention keeps the slot-aligned 16-row groups (RowMap::ptab / qrow / orow)
   for (size_t c0 = 0; c0 < tab.size(); c0 += PREFILL) {
     const int T = (int)std::min<size_t>(PREFILL, tab.size() - c0);  // PREFILL % 16 == 0
     if (c0 > 0) PTTS_HIP(hipStreamSynchronize(stream_));  // ids / row table / staging reused by this pass
-    memcpy(h_ids_, rid.data() + c0, sizeof(int) * T);
-    memcpy(h_tab_, tab.data() + c0, sizeof(int) * T);
-    PTTS_HIP(hipMemcpyAsync(ids_dev_, h_ids_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
-    PTTS_HIP(hipMemcpyAsync(rowtab_dev_, h_tab_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    int* h_ptab = h_tab_;
+    int* h_ctab = h_tab_ + PREFILL;
+    int* h_qrow = h_tab_ + 2 * PREFILL;
+    int* h_orow = h_tab_ + 3 * PREFILL;
+    int Tc = 0;
+    for (int r = 0; r < T; ++r) {
+      const int v = tab[c0 + r];
+      h_ptab[r] = v;
+      h_orow[r] = v < 0 ? -1 : Tc;
+      if (v >= 0) {
+        h_ctab[Tc] = v;
+        h_qrow[Tc] = r;
+        h_ids_[Tc] = rid[c0 + r];
+        ++Tc;
+      }
+    }
+    if (Tc == 0) continue;
+    PTTS_HIP(hipMemcpyAsync(ids_dev_, h_ids_, sizeof(int) * Tc, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(rowtab_dev_, h_ptab, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(ctab_dev_, h_ctab, sizeof(int) * Tc, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(qrow_dev_, h_qrow, sizeof(int) * Tc, hipMemcpyHostToDevice, stream_));
+    PTTS_HIP(hipMemcpyAsync(orow_dev_, h_orow, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
     std::vector<Op> ops;
     {
       const int* idp = ids_dev_;
       const float* tb = W(L_.embed);
       float* x = x_;
-      ops.push_back({"prefill.embed", [=](hipStream_t s) { embed_gather(idp, T, tb, D, x, s); }});
+      ops.push_back({"prefill.embed", [=](hipStream_t s) { embed_gather(idp, Tc, tb, D, x, s); }});
     }
     {
       float* x = x_;
       float* h = h_;
       const float* w = W(L_.fl[0].n1w);
       const float* b = W(L_.fl[0].n1b);
-      ops.push_back({"prefill.ln1", [=](hipStream_t s) { layernorm(x, D, h, D, T, D, w, b, 1e-5f, s); }});
+      ops.push_back({"prefill.ln1", [=](hipStream_t s) { layernorm(x, D, h, D, Tc, D, w, b, 1e-5f, s); }});
     }
-    RowMap map{0, 1, 0, nullptr, rowtab_dev_};
-    flow_layers(ops, T, map, 16, false, "prefill");
+    RowMap map{0, 1, 0, nullptr, ctab_dev_};
+    map.ptab = rowtab_dev_;
+    map.mpad = T;
+    map.qrow = qrow_dev_;
+    map.orow = orow_dev_;
+    flow_layers(ops, Tc, map, 16, false, "prefill");
     run_ops(ops);
   }
   // the slot state the back part owns (Mimi ring position, conv and overlap-add histories, frame

@@ -188,7 +188,8 @@ class Engine {
   float* tslab_ = nullptr;
   int* tickets_ = nullptr;
   int* ids_dev_ = nullptr;
-  int* rowtab_dev_ = nullptr;   // [PREFILL] slot << 16 | pos, -1 = padding row
+  int* rowtab_dev_ = nullptr;   // [PREFILL] slot << 16 | pos, -1 = padding row (16-row groups)
+  int *ctab_dev_ = nullptr, *qrow_dev_ = nullptr, *orow_dev_ = nullptr;  // compact admission rows (RowMap)
   int* admit_slots_ = nullptr;  // [max_slots] staged admission list
   SlotState* admit_st_ = nullptr;
   int* admit_fpos_ = nullptr;

@@ -228,6 +228,14 @@ struct RowMap {
   int slot0, rps, p0;
   const int* pos_arr;
   const int* tab;
+  // compact batched admission (slots_open): the GEMM / reduce rows are the tokens only (tab), while
+  // the 16-query attention runs on slot-aligned 16-row groups with padding (ptab, mpad rows): qkv
+  // rope writes query row r at padded row qrow[r], the attention writes padded row p's output at
+  // row orow[p] (-1: padding, not written)
+  const int* ptab = nullptr;
+  int mpad = 0;
+  const int* qrow = nullptr;
+  const int* orow = nullptr;
 };
 // Shared voice prefixes (FlowLM cache): when `pre` is set, positions < pre_len[slot] of slot
 // `slot` live in the voice's own cache pre[slot] ([NL][2][nh][F][64], F = pre_len[slot]; layer

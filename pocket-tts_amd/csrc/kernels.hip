@@ -2569,8 +2569,9 @@ __global__ __launch_bounds__(256) void k_qkv_rope(const float* P, int S, const f
   const float freq = expf((float)i * (-logf(10000.0f) * 2.0f / 64.0f));
   const float ang = (float)pos * freq;
   const float cs = cosf(ang), sn = sinf(ang);
-  Q[(long)row * d + c] = q0 * cs - q1 * sn;
-  Q[(long)row * d + c + 1] = q0 * sn + q1 * cs;
+  const long qr = mp.qrow ? mp.qrow[row] : row;  // compact admission: the query's padded row
+  Q[qr * d + c] = q0 * cs - q1 * sn;
+  Q[qr * d + c + 1] = q0 * sn + q1 * cs;
   if (slot < 0) return;  // padding row of a batched admission
   float* kb = kv.base + (long)slot * kv.slot_stride + ((long)hh * kv.cap + (pos % kv.cap)) * 64 + 2 * i;
   float* vb = kv.base + (long)slot * kv.slot_stride + ((long)(nh + hh) * kv.cap + (pos % kv.cap)) * 64 + 2 * i;
@@ -2944,7 +2945,8 @@ __global__ __launch_bounds__(64 * A16_WAVES) void k_attn16(const float* __restri
       num += s_o[w][qi][dd] * ew;
       den += s_l[w][qi] * ew;
     }
-    O[(long)(row0 + qi) * d + head * 64 + dd] = num / den;
+    const int orow = mp.orow ? mp.orow[row0 + qi] : row0 + qi;  // compact admission: the token's row
+    if (orow >= 0) O[(long)orow * d + head * 64 + dd] = num / den;
   }
 }
 
