@@ -253,6 +253,19 @@ int ptts_frame_lag(const ptts_engine* e, int* admit_delay);
  * GPU always has the next step queued while the host hands out frames. calls_back <= 1. */
 int ptts_fetch_prev(ptts_engine* e, int calls_back, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
                     float* eos_logits, float* latents);
+/* First-frame previews (pipelined engines; no reference counterpart: the reference decodes each
+ * frame right after its FlowLM step, tts_model.rs:1040-1047, and does not pipeline). With
+ * max_rows > 0 (at most 8), the first frame of up to max_rows rows that start in one call is also
+ * decoded right after that call's FlowLM step, alone, from the fresh Mimi state every utterance
+ * starts from, so the first chunk of a new stream does not wait ptts_frame_lag() calls. The rows'
+ * regular first frame still arrives through ptts_fetch (within float rounding of the preview); a
+ * caller delivers whichever comes first. 0 disables. PTTS_ERR_INVALID on a sequential engine. */
+int ptts_preview_enable(ptts_engine* e, int max_rows);
+/* Completed previews, oldest first: *n_out frames, slot slots[i] and pcm [i][1920] (at most
+ * max_n; a preview's rows are returned together). wait = 0: only those already complete (never
+ * blocks); 1: blocks until the launched previews complete (as many as fit in max_n). A slot
+ * re-admitted or closed before its preview is fetched drops that preview. */
+int ptts_preview_fetch(ptts_engine* e, int wait, int max_n, int* slots, float* pcm, int* n_out);
 /* Test hook (teacher forcing): overwrite the backbone input latent of `slot`. */
 int ptts_slot_set_latent(ptts_engine* e, int slot, const float* latent32);
 /* MimiModel::decode_from_latent (mimi.rs:143-157) after the denorm + DummyQuantizer of

@@ -259,6 +259,16 @@ int ptts_fetch_prev(ptts_engine* e, int calls_back, int n_rows, float* pcm, uint
   return guard([&] { eng(e).fetch(n_rows, pcm, frame_valid, last, eos_logits, latents, calls_back); });
 }
 
+int ptts_preview_enable(ptts_engine* e, int max_rows) { return guard([&] { eng(e).preview_enable(max_rows); }); }
+
+int ptts_preview_fetch(ptts_engine* e, int wait, int max_n, int* slots, float* pcm, int* n_out) {
+  return guard([&] {
+    if (!n_out) throw ptts::Error(PTTS_ERR_INVALID, "null argument");
+    *n_out = 0;
+    *n_out = eng(e).preview_fetch(wait, max_n, slots, pcm);
+  });
+}
+
 int ptts_frame_lag(const ptts_engine* e, int* admit_delay) {
   if (!e || !e->impl) return -1;
   const ptts::Engine& E = *e->impl;

@@ -188,6 +188,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   vpre_ = (const float**)dalloc((sizeof(float*) * (B + 1) + 3) / 4);  // zero: no slot has a prefix
   vlen_ = (int*)dalloc(B + 1);
   slot_voice_.assign(B, nullptr);
+  drained_.assign(B, 1);
   share_voice_ = probe_env("PTTS_NO_SHARED_VOICE") == nullptr;
 #ifdef PTTS_PROBES
   if (probe_env("PTTS_STAMPS")) {
@@ -290,6 +291,7 @@ Engine::~Engine() {
   (void)hipSetDevice(dev_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (stream_be_) (void)hipStreamSynchronize(stream_be_);
+  if (stream_pv_) (void)hipStreamSynchronize(stream_pv_);
 #ifdef PTTS_PROBES
   if (stamp_ring_) {  // tag (part << 8 | buffer << 1 | end), then the 100-MHz realtime count
     unsigned n = 0;
@@ -307,6 +309,17 @@ Engine::~Engine() {
   for (int s = 0; s < (int)slot_voice_.size(); ++s) voice_release(s, true);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : graph_defs_) (void)hipGraphDestroy(kv.second);
+  for (auto& kv : pv_graphs_) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : pv_graph_defs_) (void)hipGraphDestroy(kv.second);
+  for (PvEntry& q : pv_q_) {
+    if (q.ev) (void)hipEventDestroy(q.ev);
+    if (q.h_pcm) (void)hipHostFree(q.h_pcm);
+    if (q.h_idx) (void)hipHostFree(q.h_idx);
+  }
+  for (int q = 0; q < NHB; ++q)
+    if (ev_pv_read_[q]) (void)hipEventDestroy(ev_pv_read_[q]);
+  if (ev_pv_front_) (void)hipEventDestroy(ev_pv_front_);
+  if (stream_pv_) (void)hipStreamDestroy(stream_pv_);
   for (int q = 0; q < NHB; ++q) {
     if (ev_front_[q]) (void)hipEventDestroy(ev_front_[q]);
     if (ev_back_[q]) (void)hipEventDestroy(ev_back_[q]);
@@ -1698,6 +1711,10 @@ void Engine::call_async(int B, bool run_front) {
   // the front part of this call, or (a flush) its hand-off buffer marked frame-less
   hipGraphExec_t front = B > 0 ? part_graph(0, B, hb, 0, 0) : nullptr;
   auto run_front_part = [&]() {
+    if (pv_read_pending_[hb]) {  // a preview still gathers from this hand-off buffer
+      PTTS_HIP(hipStreamWaitEvent(stream_, ev_pv_read_[hb], 0));
+      pv_read_pending_[hb] = false;
+    }
     if (front && xh_dirty_) refresh_xh();
     if (front) PTTS_HIP(hipGraphLaunch(front, stream_));
     else PTTS_HIP(hipMemsetAsync(flags_[hb], 0, sizeof(FrameFlags) * max_slots_, stream_));
@@ -1730,6 +1747,7 @@ void Engine::call_async(int B, bool run_front) {
     // stamps, profiles/r04/graph_boundary_ab.txt).
     if (kr == 0) PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
     run_front_part();
+    launch_previews(B, hb);
     // only the pass's last front part is waited for (by the pass, below)
     if (kr == nf - 1) PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
     if (kr == 0 && k_ >= nf) {
@@ -1762,6 +1780,7 @@ void Engine::call_async(int B, bool run_front) {
     const int hb1 = (hb + nhb_ - 1) % nhb_, qp1 = qp ^ 1;  // frame k-1
     PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
     run_front_part();
+    launch_previews(B, hb);
     PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
     if (prev_rows > 0) {
       hipGraphExec_t back = part_graph(1, prev_rows, hb1, qp1, 1);
@@ -1784,6 +1803,7 @@ void Engine::sync() {
   PTTS_HIP(hipSetDevice(dev_));
   PTTS_HIP(hipStreamSynchronize(stream_));
   PTTS_HIP(hipStreamSynchronize(stream_be_));
+  if (stream_pv_) PTTS_HIP(hipStreamSynchronize(stream_pv_));
 }
 
 // Outputs of the last call's frame (see step_async); rows past the rows that frame covered
@@ -1819,6 +1839,7 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
   };
   for (int b = 0; b < B; ++b) {
     const bool ok = b < n && hf[b].valid;
+    if (ok && hf[b].last) drained_[b] = 1;  // its last frame's pass has completed (waited above)
     if (valid) valid[b] = ok;
     if (last) last[b] = ok && hf[b].last;
     if (pcm) {
@@ -2525,8 +2546,17 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
   // flags) is reset only after the back parts already queued, which may still decode the slot's
   // previous utterance; the voice-KV copy and the text prefill above touch front-owned state
   // only, so they run ahead of that wait, beside those back parts
-  PTTS_HIP(hipEventRecord(ev_be_tail_, stream_be_));
-  PTTS_HIP(hipStreamWaitEvent(stream_, ev_be_tail_, 0));
+  // That wait is needed only while an admitted slot may still have a frame in flight: a slot whose
+  // utterance is drained (never admitted, closed, or its last frame fetched) is written by no
+  // queued back part (the commit and the histories touch rows with a frame only), so the front
+  // stream does not stall behind the queued back passes at such an admission (the server's case)
+  bool drained = true;
+  for (int i = 0; i < n; ++i) drained = drained && drained_[slots[i]];
+  if (!drained) {
+    PTTS_HIP(hipEventRecord(ev_be_tail_, stream_be_));
+    PTTS_HIP(hipStreamWaitEvent(stream_, ev_be_tail_, 0));
+  }
+  for (int i = 0; i < n; ++i) drained_[slots[i]] = 0;
   // fresh Mimi decoder state (init_states(1, 1000) per segment, tts_model.rs:941) + slot states
   std::vector<SlotState> st(n);
   std::vector<int> fp(n);
@@ -2558,6 +2588,11 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
       act_slots_.push_back(slots[i]);
       st[i].active = 0;
     }
+  // first-frame previews: each admitted row's first front part runs at call k_ + admit_delay_ (a
+  // re-admitted slot's unfetched preview belonged to its previous utterance)
+  for (int i = 0; i < n; ++i) pv_forget(slots[i]);
+  if (pv_max_ > 0)
+    for (int i = 0; i < n; ++i) pv_pending_.push_back({slots[i], k_ + admit_delay_});
   memcpy(h_slots_, slots, sizeof(int) * n);
   memcpy(h_st_, st.data(), sizeof(SlotState) * n);
   memcpy(h_fp_, fp.data(), sizeof(int) * n);
@@ -2678,6 +2713,8 @@ void Engine::decode_latents(int slot, const float* lat, int n, float* pcm, float
     PTTS_HIP(hipStreamSynchronize(stream_));
   }
   mark_admission();
+  drained_[slot] = 1;
+  pv_forget(slot);
 }
 
 void Engine::slot_close(int slot) {
@@ -2698,6 +2735,8 @@ void Engine::slot_close(int slot) {
   }
   mark_admission();
   PTTS_HIP(hipStreamSynchronize(stream_));
+  drained_[slot] = 1;
+  pv_forget(slot);
   voice_release(slot, true);
 }
 
@@ -2736,6 +2775,210 @@ void Engine::set_latent(int slot, const float* lat) {
   PTTS_HIP(hipMemcpyAsync(lat_in_ + (size_t)slot * LDIM, lat, sizeof(float) * LDIM, hipMemcpyHostToDevice, stream_));
   mark_admission();
   PTTS_HIP(hipStreamSynchronize(stream_));
+}
+
+// ---- first-frame previews --------------------------------------------------------------------
+// The pipelined engine returns a row's frame k frame_lag() calls after the call that computed its
+// latent (2 n - 1 with n-frame passes): the back passes decode every row's frames together, so the
+// first frame of a new utterance waits for a pass over frames of all rows. A preview decodes the
+// first frame of each newly started row right after its front part, alone: a single-frame back
+// pass over those rows (their latents gathered from the call's hand-off buffer into a compact
+// batch of P = 1, 2, 4 or 8 rows) on its own high-priority stream, from the fresh Mimi decoder
+// state every utterance starts from (tts_model.rs:941 init_states; zero conv and overlap-add
+// histories, empty attention ring). That is exactly the state the row's regular pass decodes its
+// frame 0 from, so the preview is that frame up to float rounding of the other tile shapes; the
+// regular pass still decodes it (it advances the row's own state), and the caller delivers the
+// first of the two to arrive (serve.py BatchScheduler).
+void Engine::swap_back(BackBufs& b) {
+  std::swap(ring_, b.ring);
+  std::swap(qprev_, b.qprev);
+  std::swap(qcur_, b.qcur);
+  std::swap(mx_, b.mx);
+  std::swap(mh_, b.mh);
+  std::swap(mq_, b.mq);
+  std::swap(mo_, b.mo);
+  std::swap(mqkv_, b.mqkv);
+  std::swap(mu_, b.mu);
+  std::swap(a0_, b.a0);
+  std::swap(mpartial_, b.mpartial);
+  std::swap(mpcap_, b.mpcap);
+  std::swap(fin_side_, b.fin_side);
+  for (int i = 0; i < 3; ++i) {
+    std::swap(cb_[i], b.cb[i]);
+    std::swap(cv_[i], b.cv[i]);
+    std::swap(ca_[i], b.ca[i]);
+    std::swap(ce_[i], b.ce[i]);
+  }
+  for (int i = 0; i < 8; ++i) std::swap(hist_[i], b.hist[i]);
+  std::swap(lat_out_[0], b.lat);
+  std::swap(flags_[0], b.flags);
+  std::swap(pcm_[0], b.pcm);
+  std::swap(mpos_, b.mpos);
+}
+
+void Engine::preview_enable(int max_rows) {
+  PTTS_REQUIRE(max_rows >= 0 && max_rows <= PV_MAX, "preview rows must be in [0, 8]");
+  PTTS_REQUIRE(max_rows == 0 || pipeline_, "first-frame previews: pipelined engines only");
+  PTTS_HIP(hipSetDevice(dev_));
+  if (max_rows > 0 && !stream_pv_) {
+    const size_t P = PV_MAX;
+    BackBufs& b = pv_;
+    b.ring = dalloc((size_t)ring_slot_ * P);
+    b.mpos = (int*)dalloc(P);
+    b.qprev = dalloc((size_t)(1 + NFR_MAX) * P * MD);
+    b.qcur = b.qprev + P * MD;
+    b.mx = dalloc(P * UP * MD);
+    b.mh = dalloc(P * UP * MD);
+    b.mq = dalloc(P * UP * MD);
+    b.mo = dalloc(P * UP * MD);
+    b.mqkv = dalloc(P * UP * 3 * MD);
+    b.mu = dalloc(P * UP * MFF);
+    b.a0 = dalloc(P * 16 * 512);
+    int T = 16, ch = 512;
+    for (int i = 0; i < 3; ++i) {
+      T *= RATIOS[i];
+      ch /= 2;
+      b.cb[i] = dalloc(P * T * ch);
+      b.ce[i] = dalloc(P * T * ch);
+      b.cv[i] = dalloc(P * T * (ch / 2));
+      b.ca[i] = dalloc(P * T * ch);
+    }
+    b.mpcap = std::max({(size_t)8 * P * UP * MD, (size_t)4 * P * UP * RATIOS[0] * (MD / 2)});
+    b.mpartial = dalloc(b.mpcap);
+    for (int i = 0; i < 8; ++i) b.hist[i] = dalloc(P * hist_P_[i] * hist_C_[i]);
+    b.fin_side = dalloc(P * (FRAME / RESBLOCK_FIN_TT) * 2);
+    b.lat = dalloc(P * LDIM);
+    b.flags = (FrameFlags*)dalloc(P * 2);
+    b.pcm = dalloc(P * FRAME);
+    for (PvEntry& q : pv_q_) {
+      PTTS_HIP(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
+      PTTS_HIP(hipHostMalloc((void**)&q.h_pcm, sizeof(float) * P * FRAME, hipHostMallocDefault));
+      PTTS_HIP(hipHostMalloc((void**)&q.h_idx, sizeof(int) * P, hipHostMallocDefault));
+      q.d_idx = (int*)dalloc(P);
+    }
+    for (int q = 0; q < NHB; ++q) PTTS_HIP(hipEventCreateWithFlags(&ev_pv_read_[q], hipEventDisableTiming));
+    PTTS_HIP(hipEventCreateWithFlags(&ev_pv_front_, hipEventDisableTiming));
+    int lo = 0, hi = 0;  // the preview is the one latency-bound part: the highest stream priority
+    PTTS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    PTTS_HIP(hipStreamCreateWithPriority(&stream_pv_, hipStreamNonBlocking, hi));
+  }
+  pv_max_ = max_rows;
+  if (!max_rows) pv_pending_.clear();
+  for (int P = 1; P < 2 * max_rows; P *= 2) pv_graph(P);  // instantiated now, not at a first chunk
+}
+
+void Engine::pv_forget(int slot) {
+  pv_pending_.erase(std::remove_if(pv_pending_.begin(), pv_pending_.end(),
+                                   [slot](const std::pair<int, long long>& p) { return p.first == slot; }),
+                    pv_pending_.end());
+  for (int i = 0; i < pv_count_; ++i) {
+    PvEntry& e = pv_q_[(pv_head_ + i) % PV_Q];
+    for (int j = 0; j < e.n; ++j)
+      if (e.slots[j] == slot) e.slots[j] = -1;
+  }
+}
+
+// the preview pass over P compact rows (built once per P, captured on stream_pv_)
+hipGraphExec_t Engine::pv_graph(int P) {
+  auto it = pv_graphs_.find(P);
+  if (it != pv_graphs_.end()) return it->second;
+  std::vector<Op> ops;
+  swap_back(pv_);  // build_back over the preview buffers (its lambdas capture the pointers)
+  try {
+    build_back(ops, P, 0, 1, 0, 1);
+  } catch (...) {
+    swap_back(pv_);
+    throw;
+  }
+  swap_back(pv_);
+  hipGraph_t g = nullptr;
+  PTTS_HIP(hipStreamBeginCapture(stream_pv_, hipStreamCaptureModeThreadLocal));
+  try {
+    // fresh decoder state: conv histories, overlap-add history, ring position 0
+    for (int i = 0; i < 8; ++i)
+      PTTS_HIP(hipMemsetAsync(pv_.hist[i], 0, sizeof(float) * P * hist_P_[i] * hist_C_[i], stream_pv_));
+    PTTS_HIP(hipMemsetAsync(pv_.qprev, 0, sizeof(float) * P * MD, stream_pv_));
+    PTTS_HIP(hipMemsetAsync(pv_.mpos, 0, sizeof(int) * P, stream_pv_));
+    set_wg_cap(0);
+    set_back_hi(1);
+    for (const Op& op : ops) op.fn(stream_pv_);
+  } catch (...) {
+    (void)hipStreamEndCapture(stream_pv_, &g);
+    throw;
+  }
+  PTTS_HIP(hipStreamEndCapture(stream_pv_, &g));
+  hipGraphExec_t ge = nullptr;
+  PTTS_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  pv_graph_defs_[P] = g;
+  pv_graphs_[P] = ge;
+  return ge;
+}
+
+// After the front part of call k_ (buffer hb, rows [0, B)) is queued on stream_: the previews of
+// the rows whose first front part that is (rows past B, or past pv_max_ rows, or with the FIFO
+// full, take the regular path only)
+void Engine::launch_previews(int B, int hb) {
+  if (pv_max_ <= 0 || pv_pending_.empty()) return;
+  std::vector<int> rows;
+  std::vector<std::pair<int, long long>> keep;
+  for (const auto& p : pv_pending_) {
+    if (p.second > k_) keep.push_back(p);
+    else if (p.second == k_ && p.first < B && (int)rows.size() < pv_max_) rows.push_back(p.first);
+  }
+  pv_pending_.swap(keep);
+  if (rows.empty() || pv_count_ == PV_Q) return;
+  const int n = (int)rows.size();
+  int P = 1;
+  while (P < n) P *= 2;
+  hipGraphExec_t graph = pv_graph(P);
+  PvEntry& e = pv_q_[(pv_head_ + pv_count_) % PV_Q];  // free: fetched (its copies done) or never used
+  e.n = n;
+  for (int i = 0; i < n; ++i) e.slots[i] = e.h_idx[i] = rows[i];
+  PTTS_HIP(hipEventRecord(ev_pv_front_, stream_));
+  PTTS_HIP(hipStreamWaitEvent(stream_pv_, ev_pv_front_, 0));
+  PTTS_HIP(hipMemcpyAsync(e.d_idx, e.h_idx, sizeof(int) * n, hipMemcpyHostToDevice, stream_pv_));
+  gather_rows(lat_out_[hb], LDIM, e.d_idx, n, P, pv_.lat, stream_pv_);
+  gather_rows(reinterpret_cast<const float*>(flags_[hb]), 2, e.d_idx, n, P, reinterpret_cast<float*>(pv_.flags),
+              stream_pv_);
+  PTTS_HIP(hipGetLastError());
+  PTTS_HIP(hipEventRecord(ev_pv_read_[hb], stream_pv_));  // front(k + nhb_) rewrites buffer hb
+  pv_read_pending_[hb] = true;
+  PTTS_HIP(hipGraphLaunch(graph, stream_pv_));
+  PTTS_HIP(hipMemcpyAsync(e.h_pcm, pv_.pcm, sizeof(float) * n * FRAME, hipMemcpyDeviceToHost, stream_pv_));
+  PTTS_HIP(hipEventRecord(e.ev, stream_pv_));
+  ++pv_count_;
+}
+
+// Completed previews in launch order, whole previews only, at most max_n frames: slots[i] and
+// pcm[i * 1920 ..]. wait: block until the launched previews complete (as many as fit).
+int Engine::preview_fetch(int wait, int max_n, int* slots, float* pcm) {
+  PTTS_REQUIRE(max_n >= 0 && (max_n == 0 || (slots && pcm)), "preview_fetch: null outputs");
+  int got = 0;
+  while (pv_count_ > 0) {
+    PvEntry& e = pv_q_[pv_head_];
+    int live = 0;
+    for (int j = 0; j < e.n; ++j) live += e.slots[j] >= 0;
+    if (got + live > max_n) break;
+    if (wait) {
+      PTTS_HIP(hipEventSynchronize(e.ev));
+    } else {
+      const hipError_t r = hipEventQuery(e.ev);
+      if (r == hipErrorNotReady) {
+        (void)hipGetLastError();  // not an error: clear it for the next PTTS_HIP(hipGetLastError())
+        break;
+      }
+      PTTS_HIP(r);
+    }
+    for (int j = 0; j < e.n; ++j)
+      if (e.slots[j] >= 0) {
+        slots[got] = e.slots[j];
+        memcpy(pcm + (size_t)got * FRAME, e.h_pcm + (size_t)j * FRAME, sizeof(float) * FRAME);
+        ++got;
+      }
+    pv_head_ = (pv_head_ + 1) % PV_Q;
+    --pv_count_;
+  }
+  return got;
 }
 
 }  // namespace ptts

@@ -75,6 +75,15 @@ class Engine {
   // the frame of the call calls_back (0 or 1) calls before the latest
   void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat, int calls_back = 0);
 
+  // First-frame previews (ptts_preview_enable / ptts_preview_fetch): the first frame of up to
+  // max_rows rows that start in one call is also decoded right after that call's front part, by a
+  // single-frame back pass over those rows alone on a third stream, from a fresh Mimi state (the
+  // state every utterance starts from), so a new stream's first chunk does not wait the
+  // pipeline's frame lag. The rows' regular frame 0 is still decoded (it advances their state);
+  // the caller delivers whichever arrives first.
+  void preview_enable(int max_rows);
+  int preview_fetch(int wait, int max_n, int* slots, float* pcm);
+
   double time_op(int B, const std::string& name, int reps);
   // GEMM-core test hook (ptts_test_gemm): Y = X W^T on tile `layout` (host buffers)
   void test_gemm(int layout, int M, int N, int K, int splits, int tail_S, const float* X, const float* Wt, float* Y);
@@ -289,6 +298,47 @@ class Engine {
 
   std::map<int, hipGraphExec_t> graphs_;
   std::map<int, hipGraph_t> graph_defs_;
+
+  // slots whose utterance has no frame left in flight (never admitted, closed, or its last frame
+  // fetched): their admission need not wait for the back parts already queued (ev_be_tail_)
+  std::vector<char> drained_;
+
+  // ---- first-frame previews (preview_enable)
+  static constexpr int PV_MAX = 8;  // rows per preview pass (the small-tile back path: < 16 rows)
+  static constexpr int PV_Q = 8;    // previews in flight / not yet fetched
+  // the buffers build_back reads and writes, swapped in while the preview graphs are built
+  struct BackBufs {
+    float *ring = nullptr, *qprev = nullptr, *qcur = nullptr, *mx = nullptr, *mh = nullptr, *mq = nullptr,
+          *mo = nullptr, *mqkv = nullptr, *mu = nullptr, *a0 = nullptr, *mpartial = nullptr, *fin_side = nullptr;
+    float *cb[3] = {}, *cv[3] = {}, *ca[3] = {}, *ce[3] = {}, *hist[8] = {};
+    float *lat = nullptr, *pcm = nullptr;
+    FrameFlags* flags = nullptr;
+    int* mpos = nullptr;
+    size_t mpcap = 0;
+  };
+  void swap_back(BackBufs& b);
+  struct PvEntry {
+    int n = 0;
+    int slots[PV_MAX] = {};
+    hipEvent_t ev = nullptr;
+    float* h_pcm = nullptr;  // pinned [PV_MAX][1920]
+    int* h_idx = nullptr;    // pinned [PV_MAX]
+    int* d_idx = nullptr;
+  };
+  int pv_max_ = 0;
+  hipStream_t stream_pv_ = nullptr;
+  BackBufs pv_{};
+  PvEntry pv_q_[PV_Q];
+  int pv_head_ = 0, pv_count_ = 0;  // FIFO of launched, unfetched previews
+  std::vector<std::pair<int, long long>> pv_pending_;  // (slot, call of its first front part)
+  hipEvent_t ev_pv_front_ = nullptr;
+  hipEvent_t ev_pv_read_[NHB] = {};  // a preview's gather of hand-off buffer q (front(q + nhb) waits)
+  bool pv_read_pending_[NHB] = {};
+  std::map<int, hipGraphExec_t> pv_graphs_;
+  std::map<int, hipGraph_t> pv_graph_defs_;
+  void launch_previews(int B, int hb);
+  hipGraphExec_t pv_graph(int P);
+  void pv_forget(int slot);  // drop the slot's pending / unfetched previews (re-admitted or closed)
 };
 
 }  // namespace ptts

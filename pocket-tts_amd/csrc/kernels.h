@@ -442,6 +442,9 @@ struct ResetArgs {
   int* mpos;
 };
 void slot_reset(const ResetArgs& a, hipStream_t s);
+// dst[i] = src[idx[i]] (rows of ld floats) for i < n, zero rows for n <= i < P: the
+// first-frame preview pass's latents and frame flags gathered from a hand-off buffer
+void gather_rows(const float* src, int ld, const int* idx, int n, int P, float* dst, hipStream_t s);
 
 // TimestepEmbedder pair + RMSNorm + average (mlp.rs:76-133,296-319): out [n][512].
 // tmp: scratch [2][n][512].

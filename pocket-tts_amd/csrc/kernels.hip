@@ -3504,6 +3504,17 @@ void slot_reset(const ResetArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_slot_reset, dim3(a.n, a.nb + 1), dim3(256), 0, s, a);
 }
 
+__global__ __launch_bounds__(64) void k_gather_rows(const float* src, int ld, const int* idx, int n, float* dst) {
+  const int i = blockIdx.x;
+  const float* r = i < n ? src + (long)idx[i] * ld : nullptr;
+  for (int e = threadIdx.x; e < ld; e += 64) dst[(long)i * ld + e] = r ? r[e] : 0.f;
+}
+
+void gather_rows(const float* src, int ld, const int* idx, int n, int P, float* dst, hipStream_t s) {
+  if (n < 0 || n > P || P < 1) throw std::runtime_error("gather_rows: 0 <= n <= P, P >= 1");
+  hipLaunchKernelGGL(k_gather_rows, dim3(P), dim3(64), 0, s, src, ld, idx, n, dst);
+}
+
 // =============================================================================================
 // Time embeddings (once per engine / lsd_decode_steps): grid (step, embedder).
 // =============================================================================================

@@ -285,6 +285,23 @@ class Engine:
         r.last = r.last.astype(bool)
         return r
 
+    def enable_preview(self, max_rows: int = 8):
+        """First-frame previews (ptts_preview_enable, pipelined engines): the first frame of up to
+        max_rows rows starting in one call is decoded right after their first FlowLM step, alone,
+        so it does not wait frame_lag() calls; fetch_previews() returns them. 0 disables."""
+        check(lib().ptts_preview_enable(self.handle, int(max_rows)))
+        self._pv_slots = np.zeros(64, np.int32)
+        self._pv_pcm = np.zeros((64, FRAME), np.float32)
+
+    def fetch_previews(self, wait: bool = False) -> list[tuple[int, np.ndarray]]:
+        """Completed first-frame previews, oldest first: (slot, pcm [1920]) pairs (fresh arrays).
+        wait=False never blocks."""
+        n = C.c_int(0)
+        check(lib().ptts_preview_fetch(self.handle, int(wait), len(self._pv_slots),
+                                       self._pv_slots.ctypes.data_as(C.POINTER(C.c_int)), fptr(self._pv_pcm),
+                                       C.byref(n)))
+        return [(int(self._pv_slots[i]), self._pv_pcm[i].copy()) for i in range(n.value)]
+
     def generate(self, slot: int, voice: Voice, ids, params: GenerationParams) -> np.ndarray:
         a = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1))
         cap = params.max_frames * FRAME

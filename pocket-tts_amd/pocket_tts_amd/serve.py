@@ -111,6 +111,9 @@ class Request:
     frames: int = 0
     waker: Callable[[], None] | None = None  # set by an async consumer (HTTP /stream)
     times: dict = field(default_factory=dict)  # submit / admit / first / last (time.time())
+    # first-frame preview: 1 = the preview was delivered as frame 0 and the regular frame 0 is still
+    # to come (it is dropped), 2 = that frame came
+    preview: int = 0
 
     def put(self, item):
         """Driver side: hand over a frame (np.ndarray), the end marker (None) or an error."""
@@ -158,11 +161,22 @@ class Request:
 
 
 class BatchScheduler:
-    """Continuous batching over one engine's slots (one GPU)."""
+    """Continuous batching over one engine's slots (one GPU).
 
-    def __init__(self, engine, max_rows: int | None = None):
+    On a pipelined engine a new row's first frame would trail its first step by the pipeline's
+    frame lag (three calls with frame-pair passes). With `preview_rows` > 0 the engine also decodes
+    each new row's first frame on its own right after that step (ptts_preview_enable); the
+    scheduler delivers that preview as the request's frame 0 and drops the regular frame 0 when it
+    comes (the two agree within float rounding: the regular pass decodes it from the same fresh
+    state), or, if the regular frame comes first, drops the preview."""
+
+    def __init__(self, engine, max_rows: int | None = None, preview_rows: int = 8):
         self.engine = engine
         self.max_rows = min(max_rows or engine.max_slots, engine.max_slots)
+        self.preview = bool(preview_rows) and getattr(engine, "pipeline", False) and hasattr(engine, "enable_preview")
+        if self.preview:
+            engine.enable_preview(preview_rows)
+        self.previews = 0  # first frames delivered from a preview
         self.waiting: deque[Request] = deque()
         self.active: dict[int, Request] = {}
         self.cv = threading.Condition()
@@ -222,15 +236,32 @@ class BatchScheduler:
         for r in batch:
             r.times["admit"] = now
 
+    def _deliver_previews(self):
+        if not self.preview:
+            return
+        for slot, pcm in self.engine.fetch_previews():
+            req = self.active.get(slot)
+            if req is None or req.frames or req.preview:  # the regular frame 0 came first
+                continue
+            req.preview = 1
+            req.frames = 1
+            self.row_frames += 1
+            self.previews += 1
+            req.times["first"] = time.time()
+            req.put(pcm)
+
     def _deliver(self, res, rows) -> list[int]:
         done = []
         for slot, req in list(self.active.items()):
             if slot < rows and res.valid[slot]:
-                req.frames += 1
-                self.row_frames += 1
-                if req.frames == 1:
-                    req.times["first"] = time.time()
-                req.put(res.pcm[slot])  # a view: fetch() returns fresh arrays every step
+                if req.preview == 1:  # frame 0, already delivered from the preview
+                    req.preview = 2
+                else:
+                    req.frames += 1
+                    self.row_frames += 1
+                    if req.frames == 1:
+                        req.times["first"] = time.time()
+                    req.put(res.pcm[slot])  # a view: fetch() returns fresh arrays every step
                 if res.last[slot]:
                     req.times["last"] = time.time()
                     if self.trace:
@@ -267,8 +298,10 @@ class BatchScheduler:
                     self.engine.step_async(rows)
                     issued.append(rows)
                     self.steps += 1
+                self._deliver_previews()
                 if len(issued) == 2 or (issued and not rows):
                     res = self.engine.fetch(issued[0], calls_back=len(issued) - 1)
+                    self._deliver_previews()  # those that completed while fetch() waited: ahead of it
                     done = self._deliver(res, issued.popleft())
                     if done:
                         with self.cv:

@@ -98,6 +98,53 @@ def test_scheduler_continuous_batching(pipeline):
         sch.close()
 
 
+class PreviewFakeEngine(FakeEngine):
+    """Pipelined stand-in with first-frame previews (ptts_preview_enable / _fetch): a row's frame 0
+    is also published as a preview `delay` fetch_previews() calls after the step that computed it
+    (delay large: the regular frame 0 arrives first and the preview must be dropped)."""
+
+    def __init__(self, max_slots=4, delay=0):
+        super().__init__(max_slots=max_slots, pipeline=True)
+        self.delay, self.pv, self.pv_rows = delay, [], 0
+
+    def enable_preview(self, n):
+        self.pv_rows = n
+
+    def open_many(self, slots, *a):  # a re-admitted slot's unfetched preview is dropped (pv_forget)
+        self.pv = [e for e in self.pv if e[1] not in slots]
+        super().open_many(slots, *a)
+
+    def _compute(self, n):
+        starting = [s for s, st in self.rows.items() if s < n and st["k"] == 0][: self.pv_rows]
+        out = super()._compute(n)
+        for s in starting:
+            self.pv.append([self.delay, s, out["pcm"][s].copy()])
+        return out
+
+    def fetch_previews(self, wait=False):
+        ready = [(s, p) for d, s, p in self.pv if d <= 0]
+        self.pv = [[d - 1, s, p] for d, s, p in self.pv if d > 0]
+        return ready
+
+
+@pytest.mark.parametrize("delay", [0, 50])
+def test_scheduler_first_frame_previews(delay):
+    """The preview is delivered as frame 0 and the regular frame 0 dropped (delay 0), or the regular
+    frame 0 comes first and the late preview is dropped (delay 50): every stream gets each frame
+    exactly once, in order."""
+    eng = PreviewFakeEngine(max_slots=3, delay=delay)
+    sch = BatchScheduler(eng, preview_rows=2)
+    try:
+        lens = [4, 1, 3, 6, 2, 5, 1]
+        reqs = [sch.submit([u + 1, 7], VOICE, params(n)) for u, n in enumerate(lens)]
+        for u, (req, n) in enumerate(zip(reqs, lens)):
+            assert [int(f[0]) for f in req.stream(timeout=10)] == [(u + 1) * 1000 + k for k in range(n)]
+        assert (sch.previews > 0) == (delay == 0)
+        assert sch.row_frames == sum(lens)
+    finally:
+        sch.close()
+
+
 def test_multi_gpu_scheduler_spreads_requests():
     scheds = [BatchScheduler(FakeEngine(max_slots=2)) for _ in range(3)]
     multi = MultiGpuScheduler(scheds)
