@@ -253,6 +253,10 @@ int ptts_frame_lag(const ptts_engine* e, int* admit_delay);
  * GPU always has the next step queued while the host hands out frames. calls_back <= 1. */
 int ptts_fetch_prev(ptts_engine* e, int calls_back, int n_rows, float* pcm, uint8_t* frame_valid, uint8_t* last,
                     float* eos_logits, float* latents);
+/* *ready = 1 if ptts_fetch_prev(e, calls_back, ..) would return without waiting (the call's frame
+ * is complete), else 0; never blocks. A driver that also serves previews polls this and
+ * ptts_preview_fetch instead of blocking in the fetch. */
+int ptts_fetch_ready(ptts_engine* e, int calls_back, int* ready);
 /* First-frame previews (pipelined engines; no reference counterpart: the reference decodes each
  * frame right after its FlowLM step, tts_model.rs:1040-1047, and does not pipeline). With
  * max_rows > 0 (at most 8), the first frame of up to max_rows rows that start in one call is also

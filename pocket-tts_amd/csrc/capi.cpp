@@ -259,6 +259,13 @@ int ptts_fetch_prev(ptts_engine* e, int calls_back, int n_rows, float* pcm, uint
   return guard([&] { eng(e).fetch(n_rows, pcm, frame_valid, last, eos_logits, latents, calls_back); });
 }
 
+int ptts_fetch_ready(ptts_engine* e, int calls_back, int* ready) {
+  return guard([&] {
+    if (!ready) throw ptts::Error(PTTS_ERR_INVALID, "null argument");
+    *ready = eng(e).fetch_ready(calls_back) ? 1 : 0;
+  });
+}
+
 int ptts_preview_enable(ptts_engine* e, int max_rows) { return guard([&] { eng(e).preview_enable(max_rows); }); }
 
 int ptts_preview_fetch(ptts_engine* e, int wait, int max_n, int* slots, float* pcm, int* n_out) {

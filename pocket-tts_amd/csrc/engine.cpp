@@ -1854,6 +1854,23 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
   }
 }
 
+bool Engine::fetch_ready(int calls_back) {
+  PTTS_REQUIRE(calls_back == 0 || calls_back == 1, "calls_back must be 0 or 1");
+  const int q = calls_back ? prev_hb_ : out_hb_;
+  hipError_t r;
+  if (pipeline_) {
+    r = hipEventQuery(ev_back_[q - q % nfr_]);
+  } else {
+    r = hipStreamQuery(stream_);
+  }
+  if (r == hipErrorNotReady) {
+    (void)hipGetLastError();
+    return false;
+  }
+  PTTS_HIP(r);
+  return true;
+}
+
 // GEMM-core test hook: one dense GEMM (mode 0) on the given tile layout, split-K slabs (splits > 1:
 // Y receives the [splits][M][N] partial slabs) or the split tail (tail_S > 0, layouts 34 / 35),
 // from host operands; the tests compare it with an fp64 product (every shipped layout, shapes the

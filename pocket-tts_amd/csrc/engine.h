@@ -74,6 +74,8 @@ class Engine {
   void sync();
   // the frame of the call calls_back (0 or 1) calls before the latest
   void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat, int calls_back = 0);
+  // fetch() of that call would not block (its frame's back pass has completed)
+  bool fetch_ready(int calls_back);
 
   // First-frame previews (ptts_preview_enable / ptts_preview_fetch): the first frame of up to
   // max_rows rows that start in one call is also decoded right after that call's front part, by a

@@ -285,6 +285,12 @@ class Engine:
         r.last = r.last.astype(bool)
         return r
 
+    def fetch_ready(self, calls_back: int = 0) -> bool:
+        """fetch(calls_back=...) would not block (ptts_fetch_ready)."""
+        r = C.c_int(0)
+        check(lib().ptts_fetch_ready(self.handle, calls_back, C.byref(r)))
+        return bool(r.value)
+
     def enable_preview(self, max_rows: int = 8):
         """First-frame previews (ptts_preview_enable, pipelined engines): the first frame of up to
         max_rows rows starting in one call is decoded right after their first FlowLM step, alone,

@@ -114,6 +114,7 @@ class Request:
     # first-frame preview: 1 = the preview was delivered as frame 0 and the regular frame 0 is still
     # to come (it is dropped), 2 = that frame came
     preview: int = 0
+    start_step: int = 0  # the scheduler's step that starts the row (trace)
 
     def put(self, item):
         """Driver side: hand over a frame (np.ndarray), the end marker (None) or an error."""
@@ -177,6 +178,7 @@ class BatchScheduler:
         if self.preview:
             engine.enable_preview(preview_rows)
         self.previews = 0  # first frames delivered from a preview
+        self.poll_s = 50e-6
         self.waiting: deque[Request] = deque()
         self.active: dict[int, Request] = {}
         self.cv = threading.Condition()
@@ -184,6 +186,7 @@ class BatchScheduler:
         self.steps = 0
         self.row_frames = 0  # frames delivered (valid rows summed over steps)
         self.trace = bool(os.environ.get("PTTS_SERVE_TRACE"))
+        self._issue_t: dict[int, float] = {}  # trace: wall time each step was issued
         # called (under self.cv) with the new load whenever it changes: the multi-process server
         # publishes it on its LoadBoard for the overflow redirect
         self.on_load: Callable[[int], None] | None = None
@@ -233,8 +236,11 @@ class BatchScheduler:
         self.engine.open_many([r.slot for r in batch], [r.voice for r in batch], [r.ids for r in batch],
                               [r.params for r in batch])
         now = time.time()
+        # the rows start at the step issued admit_delay calls after the next one (ptts_frame_lag)
+        delay = self.engine.frame_lag()[1] if hasattr(self.engine, "frame_lag") else 0
         for r in batch:
             r.times["admit"] = now
+            r.start_step = self.steps + delay
 
     def _deliver_previews(self):
         if not self.preview:
@@ -267,7 +273,10 @@ class BatchScheduler:
                     if self.trace:
                         t = req.times
                         t0 = t.get("route", t["submit"])
+                        ts = self._issue_t.get(req.start_step, t["submit"])
                         print(f"ptts-serve slot {slot} route_to_submit_ms {1e3 * (t['submit'] - t0):.1f} "
+                              f"start_ms {1e3 * (ts - t['submit']):.2f} "
+                              f"first_after_start_ms {1e3 * (t['first'] - ts):.2f} "
                               f"first_to_chunk0_ms {1e3 * (t.get('chunk0', t['first']) - t['first']):.1f} "
                               f"frames {req.frames} admit_wait_ms "
                               f"{1e3 * (t['admit'] - t['submit']):.1f} first_ms {1e3 * (t['first'] - t['submit']):.1f} "
@@ -297,10 +306,21 @@ class BatchScheduler:
                 if rows:
                     self.engine.step_async(rows)
                     issued.append(rows)
+                    if self.trace:
+                        self._issue_t[self.steps] = time.time()
+                        self._issue_t.pop(self.steps - 256, None)
                     self.steps += 1
                 self._deliver_previews()
                 if len(issued) == 2 or (issued and not rows):
-                    res = self.engine.fetch(issued[0], calls_back=len(issued) - 1)
+                    cb = len(issued) - 1
+                    # while a stream waits for its first frame, poll the call's frame and the
+                    # previews (~50 us apart) instead of blocking in fetch(): a preview completes
+                    # while the call's back pass still runs, and is handed out as soon as it does
+                    if self.preview and any(r.frames == 0 for r in self.active.values()):
+                        while not self.engine.fetch_ready(cb):
+                            self._deliver_previews()
+                            time.sleep(self.poll_s)
+                    res = self.engine.fetch(issued[0], calls_back=cb)
                     self._deliver_previews()  # those that completed while fetch() waited: ahead of it
                     done = self._deliver(res, issued.popleft())
                     if done:
@@ -788,6 +808,8 @@ def main(argv=None):
     ap.add_argument("--back-frames", type=int, default=2, choices=(1, 2, 4, 8),
                     help="frames per Mimi decode pass (ptts_engine_config.back_frames): 2, the throughput "
                          "configuration bench.py measures (two more calls of frame lag, ~1.2 ms at B = 32)")
+    ap.add_argument("--preview-rows", type=int, default=8,
+                    help="first-frame previews: rows per call whose first frame is decoded at once (0: off)")
     ap.add_argument("--stand-in-engine", action="store_true",
                     help="CPU self-test of the launcher and routing: a stand-in engine that computes nothing")
     ap.add_argument("--stand-in-step-ms", type=float, default=0.0, help="--stand-in-engine: time per step")
@@ -833,7 +855,7 @@ def main(argv=None):
             voices[name] = engine.voice_from_audio(audio[0], sr)
     if not voices:
         raise SystemExit("at least one --voice NAME=path is required")
-    scheduler = BatchScheduler(engine)
+    scheduler = BatchScheduler(engine, preview_rows=args.preview_rows)
     service = TTSService(scheduler, voices, default_voice=next(iter(voices)),
                          tokenizer=load_tokenizer(args.tokenizer) if args.tokenizer else None)
     service.worker = {"rank": rank, "world": world, "pid": os.getpid(), "weights_checksum": checksum}

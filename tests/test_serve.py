@@ -121,6 +121,9 @@ class PreviewFakeEngine(FakeEngine):
             self.pv.append([self.delay, s, out["pcm"][s].copy()])
         return out
 
+    def fetch_ready(self, calls_back=0):
+        return True
+
     def fetch_previews(self, wait=False):
         ready = [(s, p) for d, s, p in self.pv if d <= 0]
         self.pv = [[d - 1, s, p] for d, s, p in self.pv if d > 0]

@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--workdir", default=os.path.join(HERE, "..", "gpurun_out"))
     ap.add_argument("--back-frames", type=int, default=2, help="the server's frames per Mimi decode pass")
+    ap.add_argument("--preview-rows", type=int, default=8, help="the server's first-frame preview rows (0: off)")
     ap.add_argument("--trace", action="store_true",
                     help="run the server with PTTS_SERVE_TRACE=1 and report the medians of its per-request "
                          "submit -> admission and submit -> first frame times")
@@ -105,7 +106,7 @@ def main():
     log = open(log_path, "w")
     server = subprocess.Popen([sys.executable, "-m", "pocket_tts_amd.serve", "--voice", f"synth={prompt_path}",
                                "--slots", "32", "--max-ctx", "480", "--port", str(args.port),
-                               "--back-frames", str(args.back_frames)],
+                               "--back-frames", str(args.back_frames), "--preview-rows", str(args.preview_rows)],
                               env=env, stdout=log, stderr=subprocess.STDOUT)
     try:
         base = f"http://127.0.0.1:{args.port}"
@@ -118,7 +119,7 @@ def main():
             except httpx.HTTPError:
                 time.sleep(0.1)
         result = {"clients": args.clients, "procs": args.procs, "route": "/stream", "seconds_per_round": args.seconds,
-                  "back_frames": args.back_frames, "rounds": []}
+                  "back_frames": args.back_frames, "preview_rows": args.preview_rows, "rounds": []}
         per = [args.clients // args.procs + (1 if p < args.clients % args.procs else 0) for p in range(args.procs)]
         for rnd in range(args.rounds):
             procs, first = [], 0
@@ -166,7 +167,7 @@ def main():
                                                           "ttfc_steady_p50_ms", "ttfc_steady_p90_ms")}
         if args.trace:  # the server's own per-request stamps (serve.py BatchScheduler._deliver)
             log.flush()
-            tr = {"admit_wait_ms": [], "first_ms": [], "first_to_chunk0_ms": []}
+            tr = {"admit_wait_ms": [], "start_ms": [], "first_after_start_ms": [], "first_ms": [], "first_to_chunk0_ms": []}
             for line in open(log_path):
                 if line.startswith("ptts-serve slot"):
                     w = line.split()
