@@ -314,7 +314,6 @@ Engine::~Engine() {
   for (PvEntry& q : pv_q_) {
     if (q.ev) (void)hipEventDestroy(q.ev);
     if (q.h_pcm) (void)hipHostFree(q.h_pcm);
-    if (q.h_idx) (void)hipHostFree(q.h_idx);
   }
   for (int q = 0; q < NHB; ++q)
     if (ev_pv_read_[q]) (void)hipEventDestroy(ev_pv_read_[q]);
@@ -2834,6 +2833,7 @@ void Engine::swap_back(BackBufs& b) {
 }
 
 void Engine::preview_enable(int max_rows) {
+  static_assert(PV_MAX <= GATHER_MAX, "preview rows travel in the gather's arguments");
   PTTS_REQUIRE(max_rows >= 0 && max_rows <= PV_MAX, "preview rows must be in [0, 8]");
   PTTS_REQUIRE(max_rows == 0 || pipeline_, "first-frame previews: pipelined engines only");
   PTTS_HIP(hipSetDevice(dev_));
@@ -2870,8 +2870,6 @@ void Engine::preview_enable(int max_rows) {
     for (PvEntry& q : pv_q_) {
       PTTS_HIP(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
       PTTS_HIP(hipHostMalloc((void**)&q.h_pcm, sizeof(float) * P * FRAME, hipHostMallocDefault));
-      PTTS_HIP(hipHostMalloc((void**)&q.h_idx, sizeof(int) * P, hipHostMallocDefault));
-      q.d_idx = (int*)dalloc(P);
     }
     for (int q = 0; q < NHB; ++q) PTTS_HIP(hipEventCreateWithFlags(&ev_pv_read_[q], hipEventDisableTiming));
     PTTS_HIP(hipEventCreateWithFlags(&ev_pv_front_, hipEventDisableTiming));
@@ -2908,14 +2906,16 @@ hipGraphExec_t Engine::pv_graph(int P) {
     throw;
   }
   swap_back(pv_);
+  // The preview state must stay the fresh one (zero conv and overlap-add histories, Mimi position
+  // 0): the pass's closing commit, the only op that writes it, is left out, so the buffers keep
+  // the zeros dalloc gave them and no reset runs per preview. (The attention ring is rewritten at
+  // positions 0..15 by each preview before it reads them. The small-row path has no fused final
+  // conv, whose tile-boundary shares the commit would otherwise add.)
+  PTTS_REQUIRE(P < 16 && !ops.empty() && ops.back().name == "commit", "preview pass: unexpected plan");
+  ops.pop_back();
   hipGraph_t g = nullptr;
   PTTS_HIP(hipStreamBeginCapture(stream_pv_, hipStreamCaptureModeThreadLocal));
   try {
-    // fresh decoder state: conv histories, overlap-add history, ring position 0
-    for (int i = 0; i < 8; ++i)
-      PTTS_HIP(hipMemsetAsync(pv_.hist[i], 0, sizeof(float) * P * hist_P_[i] * hist_C_[i], stream_pv_));
-    PTTS_HIP(hipMemsetAsync(pv_.qprev, 0, sizeof(float) * P * MD, stream_pv_));
-    PTTS_HIP(hipMemsetAsync(pv_.mpos, 0, sizeof(int) * P, stream_pv_));
     set_wg_cap(0);
     set_back_hi(1);
     for (const Op& op : ops) op.fn(stream_pv_);
@@ -2950,13 +2950,10 @@ void Engine::launch_previews(int B, int hb) {
   hipGraphExec_t graph = pv_graph(P);
   PvEntry& e = pv_q_[(pv_head_ + pv_count_) % PV_Q];  // free: fetched (its copies done) or never used
   e.n = n;
-  for (int i = 0; i < n; ++i) e.slots[i] = e.h_idx[i] = rows[i];
+  for (int i = 0; i < n; ++i) e.slots[i] = rows[i];
   PTTS_HIP(hipEventRecord(ev_pv_front_, stream_));
   PTTS_HIP(hipStreamWaitEvent(stream_pv_, ev_pv_front_, 0));
-  PTTS_HIP(hipMemcpyAsync(e.d_idx, e.h_idx, sizeof(int) * n, hipMemcpyHostToDevice, stream_pv_));
-  gather_rows(lat_out_[hb], LDIM, e.d_idx, n, P, pv_.lat, stream_pv_);
-  gather_rows(reinterpret_cast<const float*>(flags_[hb]), 2, e.d_idx, n, P, reinterpret_cast<float*>(pv_.flags),
-              stream_pv_);
+  gather_preview(lat_out_[hb], flags_[hb], rows.data(), n, P, pv_.lat, pv_.flags, stream_pv_);
   PTTS_HIP(hipGetLastError());
   PTTS_HIP(hipEventRecord(ev_pv_read_[hb], stream_pv_));  // front(k + nhb_) rewrites buffer hb
   pv_read_pending_[hb] = true;

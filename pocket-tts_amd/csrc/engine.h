@@ -324,8 +324,6 @@ class Engine {
     int slots[PV_MAX] = {};
     hipEvent_t ev = nullptr;
     float* h_pcm = nullptr;  // pinned [PV_MAX][1920]
-    int* h_idx = nullptr;    // pinned [PV_MAX]
-    int* d_idx = nullptr;
   };
   int pv_max_ = 0;
   hipStream_t stream_pv_ = nullptr;

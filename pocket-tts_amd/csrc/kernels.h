@@ -442,9 +442,12 @@ struct ResetArgs {
   int* mpos;
 };
 void slot_reset(const ResetArgs& a, hipStream_t s);
-// dst[i] = src[idx[i]] (rows of ld floats) for i < n, zero rows for n <= i < P: the
-// first-frame preview pass's latents and frame flags gathered from a hand-off buffer
-void gather_rows(const float* src, int ld, const int* idx, int n, int P, float* dst, hipStream_t s);
+// The first-frame preview pass's inputs, one launch: row i < n gets the latent and frame flags of
+// row idx[i] of a hand-off buffer, rows n <= i < P zeros (no frame). idx travels in the kernel
+// arguments (no host-to-device copy ahead of it).
+constexpr int GATHER_MAX = 8;
+void gather_preview(const float* lat, const FrameFlags* flags, const int* idx, int n, int P, float* lat_out,
+                    FrameFlags* flags_out, hipStream_t s);
 
 // TimestepEmbedder pair + RMSNorm + average (mlp.rs:76-133,296-319): out [n][512].
 // tmp: scratch [2][n][512].

@@ -3504,15 +3504,29 @@ void slot_reset(const ResetArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_slot_reset, dim3(a.n, a.nb + 1), dim3(256), 0, s, a);
 }
 
-__global__ __launch_bounds__(64) void k_gather_rows(const float* src, int ld, const int* idx, int n, float* dst) {
-  const int i = blockIdx.x;
-  const float* r = i < n ? src + (long)idx[i] * ld : nullptr;
-  for (int e = threadIdx.x; e < ld; e += 64) dst[(long)i * ld + e] = r ? r[e] : 0.f;
+struct GatherArgs {
+  const float* lat;
+  const FrameFlags* flags;
+  float* lat_out;
+  FrameFlags* flags_out;
+  int n;
+  int idx[GATHER_MAX];
+};
+
+__global__ __launch_bounds__(64) void k_gather_preview(GatherArgs a) {
+  const int i = blockIdx.x, t = threadIdx.x;
+  const bool on = i < a.n;
+  const int r = on ? a.idx[i] : 0;
+  if (t < 32) a.lat_out[i * 32 + t] = on ? a.lat[(long)r * 32 + t] : 0.f;
+  if (t == 32) a.flags_out[i] = on ? a.flags[r] : FrameFlags{0, 0};
 }
 
-void gather_rows(const float* src, int ld, const int* idx, int n, int P, float* dst, hipStream_t s) {
-  if (n < 0 || n > P || P < 1) throw std::runtime_error("gather_rows: 0 <= n <= P, P >= 1");
-  hipLaunchKernelGGL(k_gather_rows, dim3(P), dim3(64), 0, s, src, ld, idx, n, dst);
+void gather_preview(const float* lat, const FrameFlags* flags, const int* idx, int n, int P, float* lat_out,
+                    FrameFlags* flags_out, hipStream_t s) {
+  if (n < 0 || n > P || P < 1 || P > GATHER_MAX) throw std::runtime_error("gather_preview: 0 <= n <= P <= 8");
+  GatherArgs a{lat, flags, lat_out, flags_out, n, {}};
+  for (int i = 0; i < n; ++i) a.idx[i] = idx[i];
+  hipLaunchKernelGGL(k_gather_preview, dim3(P), dim3(64), 0, s, a);
 }
 
 // =============================================================================================

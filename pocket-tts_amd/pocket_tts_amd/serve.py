@@ -186,7 +186,6 @@ class BatchScheduler:
         self.steps = 0
         self.row_frames = 0  # frames delivered (valid rows summed over steps)
         self.trace = bool(os.environ.get("PTTS_SERVE_TRACE"))
-        self._issue_t: dict[int, float] = {}  # trace: wall time each step was issued
         # called (under self.cv) with the new load whenever it changes: the multi-process server
         # publishes it on its LoadBoard for the overflow redirect
         self.on_load: Callable[[int], None] | None = None
@@ -273,7 +272,7 @@ class BatchScheduler:
                     if self.trace:
                         t = req.times
                         t0 = t.get("route", t["submit"])
-                        ts = self._issue_t.get(req.start_step, t["submit"])
+                        ts = t.get("start", t["submit"])
                         print(f"ptts-serve slot {slot} route_to_submit_ms {1e3 * (t['submit'] - t0):.1f} "
                               f"start_ms {1e3 * (ts - t['submit']):.2f} "
                               f"first_after_start_ms {1e3 * (t['first'] - ts):.2f} "
@@ -307,8 +306,10 @@ class BatchScheduler:
                     self.engine.step_async(rows)
                     issued.append(rows)
                     if self.trace:
-                        self._issue_t[self.steps] = time.time()
-                        self._issue_t.pop(self.steps - 256, None)
+                        now = time.time()
+                        for r in self.active.values():
+                            if r.start_step == self.steps:
+                                r.times["start"] = now
                     self.steps += 1
                 self._deliver_previews()
                 if len(issued) == 2 or (issued and not rows):
