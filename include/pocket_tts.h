@@ -257,6 +257,12 @@ int ptts_fetch_prev(ptts_engine* e, int calls_back, int n_rows, float* pcm, uint
  * is complete), else 0; never blocks. A driver that also serves previews polls this and
  * ptts_preview_fetch instead of blocking in the fetch. */
 int ptts_fetch_ready(ptts_engine* e, int calls_back, int* ready);
+/* *done = 1 once the FlowLM step (front part) of the call calls_back (0..3) calls before the latest
+ * has run on the GPU; wait = 1 blocks until it has. Pipelined engines let the host run calls ahead
+ * of the GPU; a driver that admits new rows waits here (calls_back = 1) before its next call, so an
+ * admission queues behind one FlowLM step at most (first-chunk latency), while the GPU still has
+ * the next step queued. */
+int ptts_front_done(ptts_engine* e, int calls_back, int wait, int* done);
 /* First-frame previews (pipelined engines; no reference counterpart: the reference decodes each
  * frame right after its FlowLM step, tts_model.rs:1040-1047, and does not pipeline). With
  * max_rows > 0 (at most 8), the first frame of up to max_rows rows that start in one call is also

@@ -266,6 +266,13 @@ int ptts_fetch_ready(ptts_engine* e, int calls_back, int* ready) {
   });
 }
 
+int ptts_front_done(ptts_engine* e, int calls_back, int wait, int* done) {
+  return guard([&] {
+    if (!done) throw ptts::Error(PTTS_ERR_INVALID, "null argument");
+    *done = eng(e).front_done(calls_back, wait != 0) ? 1 : 0;
+  });
+}
+
 int ptts_preview_enable(ptts_engine* e, int max_rows) { return guard([&] { eng(e).preview_enable(max_rows); }); }
 
 int ptts_preview_fetch(ptts_engine* e, int wait, int max_n, int* slots, float* pcm, int* n_out) {

@@ -272,6 +272,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   PTTS_HIP(hipEventCreateWithFlags(&ev_admit_, hipEventDisableTiming));
   PTTS_HIP(hipEventCreateWithFlags(&ev_be_tail_, hipEventDisableTiming));
   PTTS_HIP(hipEventCreateWithFlags(&ev_act_, hipEventDisableTiming));
+  for (hipEvent_t& e : ev_call_) PTTS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   PTTS_HIP(hipEventRecord(ev_act_, stream_));
   PTTS_HIP(hipEventRecord(ev_admit_, stream_));
   pipeline_ = cfg.pipeline != 0;
@@ -326,6 +327,8 @@ Engine::~Engine() {
   if (ev_admit_) (void)hipEventDestroy(ev_admit_);
   if (ev_be_tail_) (void)hipEventDestroy(ev_be_tail_);
   if (ev_act_) (void)hipEventDestroy(ev_act_);
+  for (hipEvent_t e : ev_call_)
+    if (e) (void)hipEventDestroy(e);
   if (stream_be_) (void)hipStreamDestroy(stream_be_);
   for (void* p : allocs_) (void)hipFree(p);
   for (int q = 0; q < NHB; ++q) {
@@ -1717,6 +1720,7 @@ void Engine::call_async(int B, bool run_front) {
     if (front && xh_dirty_) refresh_xh();
     if (front) PTTS_HIP(hipGraphLaunch(front, stream_));
     else PTTS_HIP(hipMemsetAsync(flags_[hb], 0, sizeof(FrameFlags) * max_slots_, stream_));
+    PTTS_HIP(hipEventRecord(ev_call_[k_ % 4], stream_));
   };
   if (!pipeline_) {
     hipGraphExec_t back = part_graph(1, B, hb, qp, 1);
@@ -1851,6 +1855,24 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
       else memset(lat + (size_t)b * LDIM, 0, sizeof(float) * LDIM);
     }
   }
+}
+
+bool Engine::front_done(int calls_back, bool wait) {
+  PTTS_REQUIRE(calls_back >= 0 && calls_back <= 3, "calls_back must be in [0, 3]");
+  const long long k = k_ - 1 - calls_back;
+  if (k < 0) return true;
+  hipEvent_t e = ev_call_[k % 4];
+  if (wait) {
+    PTTS_HIP(hipEventSynchronize(e));
+    return true;
+  }
+  const hipError_t r = hipEventQuery(e);
+  if (r == hipErrorNotReady) {
+    (void)hipGetLastError();
+    return false;
+  }
+  PTTS_HIP(r);
+  return true;
 }
 
 bool Engine::fetch_ready(int calls_back) {

@@ -76,6 +76,9 @@ class Engine {
   void fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos, float* lat, int calls_back = 0);
   // fetch() of that call would not block (its frame's back pass has completed)
   bool fetch_ready(int calls_back);
+  // the front part of the call calls_back (0..3) calls before the latest has completed (wait:
+  // block until it has); true for calls before the first
+  bool front_done(int calls_back, bool wait);
 
   // First-frame previews (ptts_preview_enable / ptts_preview_fetch): the first frame of up to
   // max_rows rows that start in one call is also decoded right after that call's front part, by a
@@ -332,6 +335,7 @@ class Engine {
   int pv_head_ = 0, pv_count_ = 0;  // FIFO of launched, unfetched previews
   std::vector<std::pair<int, long long>> pv_pending_;  // (slot, call of its first front part)
   hipEvent_t ev_pv_front_ = nullptr;
+  hipEvent_t ev_call_[4] = {};  // after the front part (or flush) of call k: ev_call_[k % 4]
   hipEvent_t ev_pv_read_[NHB] = {};  // a preview's gather of hand-off buffer q (front(q + nhb) waits)
   bool pv_read_pending_[NHB] = {};
   std::map<int, hipGraphExec_t> pv_graphs_;

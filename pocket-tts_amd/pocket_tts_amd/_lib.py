@@ -98,6 +98,7 @@ SIGNATURES = [
     ("ptts_fetch_prev", C.c_int, [C.c_void_p, C.c_int, C.c_int, F32P, U8P, U8P, F32P, F32P]),
     ("ptts_preview_enable", C.c_int, [C.c_void_p, C.c_int]),
     ("ptts_fetch_ready", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
+    ("ptts_front_done", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int)]),
     ("ptts_preview_fetch", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int), F32P, C.POINTER(C.c_int)]),
     ("ptts_slot_set_latent", C.c_int, [C.c_void_p, C.c_int, F32P]),
     ("ptts_decode_latents", C.c_int, [C.c_void_p, C.c_int, F32P, C.c_int, F32P, F32P, F32P, F32P]),

@@ -291,6 +291,13 @@ class Engine:
         check(lib().ptts_fetch_ready(self.handle, calls_back, C.byref(r)))
         return bool(r.value)
 
+    def front_done(self, calls_back: int = 1, wait: bool = False) -> bool:
+        """The FlowLM step of the call calls_back calls before the latest has run (ptts_front_done);
+        wait=True blocks until it has."""
+        r = C.c_int(0)
+        check(lib().ptts_front_done(self.handle, calls_back, int(wait), C.byref(r)))
+        return bool(r.value)
+
     def enable_preview(self, max_rows: int = 8):
         """First-frame previews (ptts_preview_enable, pipelined engines): the first frame of up to
         max_rows rows starting in one call is decoded right after their first FlowLM step, alone,

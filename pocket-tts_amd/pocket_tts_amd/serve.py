@@ -179,6 +179,7 @@ class BatchScheduler:
             engine.enable_preview(preview_rows)
         self.previews = 0  # first frames delivered from a preview
         self.poll_s = 50e-6
+        self.shallow = getattr(engine, "pipeline", False) and hasattr(engine, "front_done")
         self.waiting: deque[Request] = deque()
         self.active: dict[int, Request] = {}
         self.cv = threading.Condition()
@@ -300,6 +301,13 @@ class BatchScheduler:
                         break
                     batch = self._take()
                     rows = max(self.active) + 1 if self.active else 0
+                # A pipelined engine lets the host run calls ahead of the GPU (the fetch below waits
+                # for a frame several calls old), and an admission queues behind every FlowLM step
+                # already issued: keep one step queued behind the running one, no more, so a new
+                # row's prefill and first step wait for one step at most (first-chunk latency; the
+                # GPU still always has the next step queued)
+                if self.shallow and issued:
+                    self.engine.front_done(1, wait=True)
                 if batch:
                     self._admit(batch)
                 if rows:

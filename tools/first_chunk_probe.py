@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--admissions", type=int, default=60)
     ap.add_argument("--poll-us", type=float, default=0.0, help="sleep between polls (0: spin)")
     ap.add_argument("--idle-only", action="store_true", help="only the one-row engine (for a kernel trace)")
+    ap.add_argument("--shallow", type=int, default=1, help="wait for the previous call's FlowLM step before a call")
     args = ap.parse_args()
     import pocket_tts_amd as pt
 
@@ -35,7 +36,7 @@ def main():
     rng = np.random.default_rng(5)
     prompt = (0.11 * rng.standard_normal((125, 1024))).astype(np.float32)
     ids = [(k * 97 + 13) % 4000 for k in range(40)]
-    out = {"back_frames": args.back_frames, "preview_rows": args.preview_rows}
+    out = {"back_frames": args.back_frames, "preview_rows": args.preview_rows, "shallow": args.shallow}
 
     def params(n, seed):
         return pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), max_frames=n, seed=seed)
@@ -61,6 +62,8 @@ def main():
                     t["first"], t["how"] = time.perf_counter(), "preview"
 
         def step():
+            if issued and args.shallow:
+                eng.front_done(1, wait=True)  # as the scheduler: one FlowLM step queued at most
             eng.step_async(rows)
             issued.append(rows)
             if "start_k" in t and t["start_k"] == 0 and "start" not in t:
