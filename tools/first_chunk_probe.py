@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--admissions", type=int, default=60)
     ap.add_argument("--poll-us", type=float, default=0.0, help="sleep between polls (0: spin)")
     ap.add_argument("--idle-only", action="store_true", help="only the one-row engine (for a kernel trace)")
+    ap.add_argument("--stamps", default="", help="write every admission's host stamps (monotonic ns) here")
     ap.add_argument("--shallow", type=int, default=1, help="wait for the previous call's FlowLM step before a call")
     args = ap.parse_args()
     import pocket_tts_amd as pt
@@ -59,7 +60,7 @@ def main():
         def poll():
             for slot, _ in eng.fetch_previews() if args.preview_rows else []:
                 if slot == rows_long and "first" not in t:
-                    t["first"], t["how"] = time.perf_counter(), "preview"
+                    t["first"], t["how"] = time.monotonic_ns() * 1e-9, "preview"
 
         def step():
             if issued and args.shallow:
@@ -67,7 +68,7 @@ def main():
             eng.step_async(rows)
             issued.append(rows)
             if "start_k" in t and t["start_k"] == 0 and "start" not in t:
-                t["start"] = time.perf_counter()
+                t["start"] = time.monotonic_ns() * 1e-9
             if "start_k" in t:
                 t["start_k"] -= 1
             poll()
@@ -81,7 +82,7 @@ def main():
                 issued.pop(0)
                 poll()
                 if r.valid[rows_long] and "first" not in t:
-                    t["first"], t["how"] = time.perf_counter(), "regular"
+                    t["first"], t["how"] = time.monotonic_ns() * 1e-9, "regular"
                 if r.last[rows_long]:
                     state["busy"] = False
 
@@ -93,9 +94,9 @@ def main():
                 if t:
                     rec.append(dict(t))
                 t.clear()
-                t["t0"] = time.perf_counter()
+                t["t0"] = time.monotonic_ns() * 1e-9
                 eng.open_many([rows_long], [v], [ids], [params(SHORT, 1000 + n)])
-                t["t1"] = time.perf_counter()
+                t["t1"] = time.monotonic_ns() * 1e-9
                 t["start_k"] = eng.frame_lag()[1]
                 state["busy"] = True
                 n += 1
@@ -104,6 +105,9 @@ def main():
             step()
         rec.append(dict(t))
         eng.close()
+        if args.stamps:
+            with open(args.stamps + (".loaded" if rows_long else ".idle"), "w") as f:
+                json.dump(rec, f)
         rec = [r for r in rec[5:] if "first" in r and "start" in r]
         ms = lambda a, b: float(np.median([1e3 * (r[b] - r[a]) for r in rec]))
         return {"admissions": len(rec), "open_many_ms": round(ms("t0", "t1"), 3),
