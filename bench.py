@@ -40,6 +40,10 @@ from pathlib import Path
 
 import numpy as np
 
+# the HIP runtime reads this at its initialization, which torch.distributed's RCCL setup (N > 1)
+# does before the engine library is loaded (the library sets the same default at load: capi.cpp)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "pocket-tts_amd"))
 sys.path.insert(0, str(ROOT / "tests"))

@@ -1,4 +1,5 @@
 // extern "C" boundary (include/pocket_tts.h): exceptions -> status codes + thread-local message.
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -34,6 +35,13 @@ ptts::Engine& eng(ptts_engine* e) {
   if (!e || !e->impl) throw ptts::Error(PTTS_ERR_INVALID, "null engine");
   return *e->impl;
 }
+
+// HIP runtime setting read when the runtime initializes (the process's first HIP call, normally
+// after this library is loaded): graphs launched as their kernel nodes instead of pre-captured AQL
+// packets. The step graphs run 0.7 % faster that way (steady step 0.5027 -> 0.4991 ms, same-box
+// A/B medians of 4, profiles/r06/ab_env2.txt). A value the caller set is kept; a process that
+// initialized HIP before loading this library keeps the runtime's default.
+__attribute__((constructor)) void ptts_runtime_env() { setenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0", 0); }
 }  // namespace
 
 extern "C" {

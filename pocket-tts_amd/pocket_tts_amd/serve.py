@@ -803,6 +803,10 @@ def main(argv=None):
     once and broadcast over RCCL at load time."""
     import argparse
 
+    # before any HIP initialization (a torchrun worker's RCCL setup comes before the engine library
+    # loads, which sets the same default): graph kernel nodes instead of captured packets (capi.cpp)
+    os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--voice", action="append", default=[], help="NAME=path (.npy prompt [F,1024] or .wav)")
     ap.add_argument("--tokenizer", default=None)
