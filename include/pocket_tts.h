@@ -201,6 +201,23 @@ int ptts_voice_from_audio(ptts_engine* e, const float* samples, int n_samples, i
  * rates divided by their gcd. */
 int ptts_resample_len(int n_samples, int sr_from, int sr_to);
 int ptts_resample(ptts_engine* e, const float* x, int n_samples, int sr_from, int sr_to, float* y);
+/* Resampler choice of the _ex entry points below. PTTS_RESAMPLE_POLY is the rule above (the
+ * default everywhere). PTTS_RESAMPLE_RUBATO_SEPTIC is the Rust driver's own resample()
+ * (audio.rs:197-255): rubato 0.14.1 FastFixedIn, PolynomialDegree::Septic, ratio sr_to / sr_from,
+ * one process() call over the whole input, output kept as rubato returns it (no delay
+ * compensation, no trim). Its source is not in the reference: the restated algorithm (kernels.h
+ * septic_schedule, oracle/ptts_oracle.c orc_resample_septic) is parity-unpinned. Equal rates
+ * return the input unchanged for both, as audio.rs:198-200 does. */
+#define PTTS_RESAMPLE_POLY 0
+#define PTTS_RESAMPLE_RUBATO_SEPTIC 1
+/* Output length of the chosen resampler (0 if the arguments are invalid); for the rubato rule the
+ * count of its position walk, about (n - 5) * sr_to / sr_from. */
+int ptts_resample_len_ex(int n_samples, int sr_from, int sr_to, int resampler);
+int ptts_resample_ex(ptts_engine* e, const float* x, int n_samples, int sr_from, int sr_to, int resampler, float* y);
+/* ptts_voice_from_audio with the resampler chosen; ptts_voice_from_audio(...) ==
+ * ptts_voice_from_audio_ex(..., PTTS_RESAMPLE_POLY, out). */
+int ptts_voice_from_audio_ex(ptts_engine* e, const float* samples, int n_samples, int sample_rate, int chunk_frames,
+                             int resampler, ptts_voice** out);
 /* Conditioning rows the voice holds (frames). */
 int ptts_voice_len(const ptts_voice* v);
 /* The [n_frames x 1024] conditioning a PCM voice was built from (host copy); for tests. */

@@ -869,6 +869,65 @@ int orc_resample(const float* x, int n, int sr_from, int sr_to, float* y) {
   return n_out;
 }
 
+/* rubato 0.14.1 FastFixedIn with PolynomialDegree::Septic, as the Rust driver calls it
+ * (audio.rs:216-225: FastFixedIn::new(to/from, 1.0, Septic, n, channels), then one process()):
+ * rubato keeps an 8-point polynomial window (POLYNOMIAL_LEN = 8) behind a zero history of 2 x 8
+ * samples; its read position starts at last_index = -(8 / 2), and each output first advances it
+ * by t_ratio = 1 / ratio (the ratio is fixed, so the ramp dt_ratio is 0) in f64, then evaluates
+ * the septic through the samples at floor(idx) - 3 .. floor(idx) + 4 at frac = idx - floor(idx)
+ * (coerced to f32); outputs continue while the position before the step is below
+ * chunk - (8 + 1). The septic is the Lagrange polynomial of nodes -3..4 (rubato writes it in power
+ * form: the same polynomial, f32 rounding apart), evaluated here as prefix x suffix products of
+ * (frac - node) times 1 / prod_{m != j} (j - m), summed in tap order; the HIP kernel
+ * (kernels.hip k_resample_septic) performs the same f32 operations in the same order. */
+static long septic_walk(long n, int sr_from, int sr_to, int* start, float* frac) {
+  const double ratio = (double)sr_to / (double)sr_from, t = 1.0 / ratio, end = (double)(n - 9);
+  double idx = -4.0;
+  long cnt = 0;
+  while (idx < end) {
+    idx += t;
+    const double fl = floor(idx);
+    if (start) start[cnt] = (int)fl;
+    if (frac) frac[cnt] = (float)(idx - fl);
+    ++cnt;
+  }
+  return cnt;
+}
+int orc_resample_septic_len(int n, int sr_from, int sr_to) {
+  if (n <= 0 || sr_from <= 0 || sr_to <= 0) return 0;
+  if (sr_from == sr_to) return n;
+  return (int)septic_walk(n, sr_from, sr_to, NULL, NULL);
+}
+int orc_resample_septic(const float* x, int n, int sr_from, int sr_to, float* y) {
+  const int n_out = orc_resample_septic_len(n, sr_from, sr_to);
+  if (n_out <= 0) return 0;
+  if (sr_from == sr_to) { memcpy(y, x, sizeof(float) * (size_t)n); return n; }
+  int* st = (int*)malloc(sizeof(int) * (size_t)n_out);
+  float* fr = (float*)malloc(sizeof(float) * (size_t)n_out);
+  septic_walk(n, sr_from, sr_to, st, fr);
+  static const float inv_den[8] = {-1.f / 5040.f, 1.f / 720.f, -1.f / 240.f, 1.f / 144.f,
+                                   -1.f / 144.f,  1.f / 240.f, -1.f / 720.f, 1.f / 5040.f};
+  for (int o = 0; o < n_out; ++o) {
+    const float f = fr[o];
+    float d[8], pre[8], suf[8];
+    for (int m = 0; m < 8; ++m) d[m] = f - (float)(m - 3);
+    pre[0] = 1.f;
+    for (int m = 1; m < 8; ++m) pre[m] = pre[m - 1] * d[m - 1];
+    suf[7] = 1.f;
+    for (int m = 6; m >= 0; --m) suf[m] = suf[m + 1] * d[m + 1];
+    float acc = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      const int i = st[o] - 3 + j;
+      const float v = (i >= 0 && i < n) ? x[i] : 0.f;
+      acc = acc + v * ((pre[j] * suf[j]) * inv_den[j]);
+    }
+    y[o] = acc;
+  }
+  free(st);
+  free(fr);
+  return n_out;
+}
+
 /* ---------------- CPU baseline driver ---------------- */
 double orc_bench(const orc_model* m, int n_utt, int F, int S, int n_frames, int threads) {
   orc_state** st = (orc_state**)malloc(sizeof(orc_state*) * (size_t)n_utt);

@@ -73,6 +73,11 @@ void orc_encode_ex(const orc_model* m, const float* pcm, int n, int chunk_frames
  * (returns its length). */
 int orc_resample_len(int n, int sr_from, int sr_to);
 int orc_resample(const float* x, int n, int sr_from, int sr_to, float* y);
+/* The Rust driver's resampler instead (audio.rs:197-255: rubato 0.14.1 FastFixedIn, Septic, one
+ * process() call over the whole input), restated from rubato's published algorithm (its source is
+ * not in the reference: parity unpinned). Equal rates copy. Returns the output length. */
+int orc_resample_septic_len(int n, int sr_from, int sr_to);
+int orc_resample_septic(const float* x, int n, int sr_from, int sr_to, float* y);
 
 /* Time-embedding table for lsd_steps (mlp.rs:296-319): out [lsd_steps x 512]. */
 void orc_time_embeddings(const orc_model* m, int lsd_steps, float* out);

@@ -192,6 +192,26 @@ int ptts_resample(ptts_engine* e, const float* x, int n_samples, int sr_from, in
   return guard([&] { eng(e).resample_host(x, n_samples, sr_from, sr_to, y); });
 }
 
+int ptts_resample_len_ex(int n_samples, int sr_from, int sr_to, int resampler) {
+  if (resampler == PTTS_RESAMPLE_POLY) return ptts_resample_len(n_samples, sr_from, sr_to);
+  if (resampler != PTTS_RESAMPLE_RUBATO_SEPTIC || n_samples <= 0 || sr_from <= 0 || sr_to <= 0) return 0;
+  if (sr_from == sr_to) return n_samples;
+  const long n = ptts::septic_schedule(n_samples, sr_from, sr_to, nullptr, nullptr);
+  return n < (1L << 30) ? (int)n : 0;
+}
+
+int ptts_resample_ex(ptts_engine* e, const float* x, int n_samples, int sr_from, int sr_to, int resampler, float* y) {
+  return guard([&] { eng(e).resample_host(x, n_samples, sr_from, sr_to, y, resampler); });
+}
+
+int ptts_voice_from_audio_ex(ptts_engine* e, const float* samples, int n_samples, int sample_rate, int chunk_frames,
+                             int resampler, ptts_voice** out) {
+  return guard([&] {
+    if (!out) throw ptts::Error(PTTS_ERR_INVALID, "null out");
+    *out = eng(e).voice_from_audio(samples, n_samples, sample_rate, chunk_frames, resampler);
+  });
+}
+
 int ptts_test_gemm(ptts_engine* e, int layout, int m, int n, int k, int splits, int tail_slices, const float* x,
                    const float* w, float* y) {
   return guard([&] { eng(e).test_gemm(layout, m, n, k, splits, tail_slices, x, w, y); });

@@ -2312,32 +2312,51 @@ int voice_chunk_frames(int F, int override_frames) {
 }
 }  // namespace
 
-// The GPU resampler on its own (test hook of the voice front end).
-void Engine::resample_host(const float* x, int n, int sr_from, int sr_to, float* y) {
+// The GPU resampler on its own (test hook of the voice front end): the resample_poly rule, or the
+// Rust driver's rubato FastFixedIn / Septic (kernels.h septic_schedule). Equal rates copy the input,
+// as audio.rs:198-200 returns the tensor unchanged.
+void Engine::resample_host(const float* x, int n, int sr_from, int sr_to, float* y, int resampler) {
   PTTS_REQUIRE(x && y && n >= 1, "empty input");
   PTTS_REQUIRE(sr_from > 0 && sr_to > 0, "sample rates must be positive");
+  PTTS_REQUIRE(resampler == PTTS_RESAMPLE_POLY || resampler == PTTS_RESAMPLE_RUBATO_SEPTIC, "unknown resampler");
+  const bool septic = resampler == PTTS_RESAMPLE_RUBATO_SEPTIC && sr_from != sr_to;
   const ResamplePlan rp = resample_plan(sr_from, sr_to);
-  const long n_out = rp.out_len(n);
+  std::vector<int> st;
+  std::vector<float> fr;
+  const long n_out = septic ? septic_schedule(n, sr_from, sr_to, &st, &fr) : sr_from == sr_to ? n : rp.out_len(n);
+  PTTS_REQUIRE(n_out >= 1, "input too short for the resampler (no output samples)");
   PTTS_REQUIRE(rp.L <= (1 << 22) && n_out < (1L << 30), "resampling ratio or length too large");
   sync();
-  const std::vector<float> taps = resample_taps(rp);
-  float *dx = nullptr, *dh = nullptr, *dy = nullptr;
+  std::vector<float> taps;
+  if (!septic && sr_from != sr_to) taps = resample_taps(rp);
+  void *dx = nullptr, *dh = nullptr, *dy = nullptr, *ds = nullptr;
   try {
     PTTS_HIP(hipMalloc(&dx, sizeof(float) * n));
-    PTTS_HIP(hipMalloc(&dh, sizeof(float) * taps.size()));
     PTTS_HIP(hipMalloc(&dy, sizeof(float) * n_out));
     PTTS_HIP(hipMemcpyAsync(dx, x, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
-    PTTS_HIP(hipMemcpyAsync(dh, taps.data(), sizeof(float) * taps.size(), hipMemcpyHostToDevice, stream_));
-    resample(dx, n, dh, rp, (int)n_out, (int)n_out, dy, stream_);
+    if (sr_from == sr_to) {
+      PTTS_HIP(hipMemcpyAsync(dy, dx, sizeof(float) * n, hipMemcpyDeviceToDevice, stream_));
+    } else if (septic) {
+      PTTS_HIP(hipMalloc(&ds, sizeof(int) * n_out));
+      PTTS_HIP(hipMalloc(&dh, sizeof(float) * n_out));
+      PTTS_HIP(hipMemcpyAsync(ds, st.data(), sizeof(int) * n_out, hipMemcpyHostToDevice, stream_));
+      PTTS_HIP(hipMemcpyAsync(dh, fr.data(), sizeof(float) * n_out, hipMemcpyHostToDevice, stream_));
+      resample_septic((const float*)dx, n, (const int*)ds, (const float*)dh, (int)n_out, (int)n_out, (float*)dy,
+                      stream_);
+    } else {
+      PTTS_HIP(hipMalloc(&dh, sizeof(float) * taps.size()));
+      PTTS_HIP(hipMemcpyAsync(dh, taps.data(), sizeof(float) * taps.size(), hipMemcpyHostToDevice, stream_));
+      resample((const float*)dx, n, (const float*)dh, rp, (int)n_out, (int)n_out, (float*)dy, stream_);
+    }
     PTTS_HIP(hipGetLastError());
     PTTS_HIP(hipMemcpyAsync(y, dy, sizeof(float) * n_out, hipMemcpyDeviceToHost, stream_));
     PTTS_HIP(hipStreamSynchronize(stream_));
   } catch (...) {
     (void)hipStreamSynchronize(stream_);
-    (void)hipFree(dx), (void)hipFree(dh), (void)hipFree(dy);
+    (void)hipFree(dx), (void)hipFree(dh), (void)hipFree(dy), (void)hipFree(ds);
     throw;
   }
-  (void)hipFree(dx), (void)hipFree(dh), (void)hipFree(dy);
+  (void)hipFree(dx), (void)hipFree(dh), (void)hipFree(dy), (void)hipFree(ds);
 }
 
 // Voice cloning (tts_model.rs:428-577): samples at `sr` -> resampled to 24 kHz on the GPU
@@ -2347,12 +2366,17 @@ void Engine::resample_host(const float* x, int n, int sr_from, int sr_to, float*
 // chunk: the streaming convs and the encoder transformer carry their state, which equals the
 // single pass below, but ConvDownsample1d re-applies its replicate padding at each chunk's first
 // frame (conv.rs:116-123); the downsample conv is therefore run per chunk.
-ptts_voice* Engine::voice_from_audio(const float* pcm_in, int n_in, int sr, int chunk_frames) {
+ptts_voice* Engine::voice_from_audio(const float* pcm_in, int n_in, int sr, int chunk_frames, int resampler) {
   PTTS_REQUIRE(ready_, "engine weights not finalized");
   PTTS_REQUIRE(pcm_in != nullptr && n_in >= 1, "empty PCM");
   PTTS_REQUIRE(sr > 0, "sample rate must be positive");
+  PTTS_REQUIRE(resampler == PTTS_RESAMPLE_POLY || resampler == PTTS_RESAMPLE_RUBATO_SEPTIC, "unknown resampler");
   const ResamplePlan rp = resample_plan(sr, PTTS_SAMPLE_RATE);
-  const long n_long = rp.identity() ? n_in : rp.out_len(n_in);
+  const bool septic = resampler == PTTS_RESAMPLE_RUBATO_SEPTIC && !rp.identity();
+  std::vector<int> sst;  // rubato position schedule (host copies outlive the async uploads)
+  std::vector<float> sfr;
+  const long n_long = rp.identity() ? n_in : septic ? septic_schedule(n_in, sr, PTTS_SAMPLE_RATE, &sst, &sfr)
+                                                    : rp.out_len(n_in);
   PTTS_REQUIRE(n_long >= 1 && n_long < (1L << 28) && rp.L <= (1 << 22), "voice prompt length or rate out of range");
   const int n = (int)n_long;
   sync();
@@ -2379,6 +2403,15 @@ ptts_voice* Engine::voice_from_audio(const float* pcm_in, int n_in, int sr, int 
     if (rp.identity()) {
       PTTS_HIP(hipMemsetAsync(dpcm, 0, sizeof(float) * Np, stream_));
       PTTS_HIP(hipMemcpyAsync(dpcm, pcm_in, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+    } else if (septic) {  // the Rust driver's resampler, straight into the frame-padded input
+      float* dx = talloc(n_in);
+      int* ds = (int*)talloc(n);
+      float* df = talloc(n);
+      PTTS_HIP(hipMemcpyAsync(dx, pcm_in, sizeof(float) * n_in, hipMemcpyHostToDevice, stream_));
+      PTTS_HIP(hipMemcpyAsync(ds, sst.data(), sizeof(int) * n, hipMemcpyHostToDevice, stream_));
+      PTTS_HIP(hipMemcpyAsync(df, sfr.data(), sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+      resample_septic(dx, n_in, ds, df, n, Np, dpcm, stream_);
+      PTTS_HIP(hipGetLastError());
     } else {  // resample straight into the frame-padded encoder input (zeros past n)
       taps = resample_taps(rp);
       float* dx = talloc(n_in);

@@ -57,8 +57,10 @@ class Engine {
 
   ptts_voice* voice_from_prompt(const float* prompt, int F);
   ptts_voice* voice_from_pcm(const float* pcm, int n) { return voice_from_audio(pcm, n, PTTS_SAMPLE_RATE, 0); }
-  ptts_voice* voice_from_audio(const float* x, int n, int sample_rate, int chunk_frames);
-  void resample_host(const float* x, int n, int sr_from, int sr_to, float* y);
+  // resampler: PTTS_RESAMPLE_POLY (resample_poly rule) or PTTS_RESAMPLE_RUBATO_SEPTIC (the Rust driver's)
+  ptts_voice* voice_from_audio(const float* x, int n, int sample_rate, int chunk_frames,
+                               int resampler = PTTS_RESAMPLE_POLY);
+  void resample_host(const float* x, int n, int sr_from, int sr_to, float* y, int resampler = PTTS_RESAMPLE_POLY);
   void slot_open(int slot, const ptts_voice* v, const int32_t* ids, int n, const ptts_gen_params& p);
   void slots_open(int n, const int* slots, const ptts_voice* const* voices, const int32_t* ids, const int* n_ids,
                   const ptts_gen_params* params);

@@ -516,4 +516,17 @@ std::vector<float> resample_taps(const ResamplePlan& p);  // host FIR design (f3
 void resample(const float* x, int n_in, const float* taps, const ResamplePlan& p, int n_out, int n_pad, float* y,
               hipStream_t s);
 
+// The Rust driver's resampler instead (audio.rs:197-255): rubato 0.14.1 FastFixedIn with
+// PolynomialDegree::Septic, one process() call over the whole input (chunk = n). Its source is not
+// in the reference; the published algorithm restated here: a read position idx starts at -4
+// (half the 8-point window), advances by t = sr_from / sr_to in f64 before each output, and
+// outputs continue while the position before the step is < n - 9; output m is the degree-7
+// Lagrange polynomial through x[s-3 .. s+4] (zeros outside the input), s = floor(idx), at
+// frac = (f32)(idx - s). septic_schedule() replays the f64 position walk on the host (count, and
+// per output s and frac when the vectors are given); resample_septic() evaluates the outputs, one
+// lane each, in a fixed f32 operation order (no contraction), zeros for n_out <= m < n_pad.
+long septic_schedule(long n, int sr_from, int sr_to, std::vector<int>* start, std::vector<float>* frac);
+void resample_septic(const float* x, int n_in, const int* start, const float* frac, int n_out, int n_pad, float* y,
+                     hipStream_t s);
+
 }  // namespace ptts

@@ -3942,6 +3942,71 @@ void resample(const float* x, int n_in, const float* taps, const ResamplePlan& p
                      p.down, p.half, n_out, n_pad, use_lds, y);
 }
 
+// ---------------------------------------------------------------------------------------------
+// rubato FastFixedIn / Septic (see kernels.h): the Lagrange weights of nodes -3..4 at frac as
+// prefix x suffix products of (frac - node), each times 1 / prod_{m != j} (j - m) =
+// (-1)^(7-j) / (j! (7-j)!); the sum over the 8 taps in tap order. The oracle's orc_resample_septic
+// performs the same f32 operations in the same order (contraction off on both sides), so the two
+// agree bit for bit; lanes of a wave read overlapping 8-sample windows (L1/L2 hits).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float septic_eval(const float* __restrict__ x, int n_in, int s, float f) {
+#pragma clang fp contract(off)
+  constexpr float inv_den[8] = {-1.f / 5040.f, 1.f / 720.f, -1.f / 240.f, 1.f / 144.f,
+                                -1.f / 144.f,  1.f / 240.f, -1.f / 720.f, 1.f / 5040.f};
+  float d[8], pre[8], suf[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) d[m] = f - (float)(m - 3);
+  pre[0] = 1.f;
+#pragma unroll
+  for (int m = 1; m < 8; ++m) pre[m] = pre[m - 1] * d[m - 1];
+  suf[7] = 1.f;
+#pragma unroll
+  for (int m = 6; m >= 0; --m) suf[m] = suf[m + 1] * d[m + 1];
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int i = s - 3 + j;
+    const float v = (i >= 0 && i < n_in) ? x[i] : 0.f;
+    acc = acc + v * ((pre[j] * suf[j]) * inv_den[j]);
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void k_resample_septic(const float* __restrict__ x, int n_in,
+                                                         const int* __restrict__ start,
+                                                         const float* __restrict__ frac, int n_out, int n_pad,
+                                                         float* __restrict__ y) {
+  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n_pad) return;
+  y[m] = m < n_out ? septic_eval(x, n_in, start[m], frac[m]) : 0.f;
+}
+
+long septic_schedule(long n, int sr_from, int sr_to, std::vector<int>* start, std::vector<float>* frac) {
+  if (n <= 0 || sr_from <= 0 || sr_to <= 0) return 0;
+  const double ratio = (double)sr_to / (double)sr_from;  // audio.rs:213
+  const double t = 1.0 / ratio;                          // dt_ratio is 0 at a fixed ratio
+  const double end = (double)(n - 9);                    // chunk_size - (POLYNOMIAL_LEN + 1)
+  double idx = -4.0;                                     // last_index = -(POLYNOMIAL_LEN / 2)
+  long cnt = 0;
+  if (start) start->clear();
+  if (frac) frac->clear();
+  while (idx < end) {
+    idx += t;
+    const double fl = std::floor(idx);
+    if (start) start->push_back((int)fl);
+    if (frac) frac->push_back((float)(idx - fl));
+    ++cnt;
+  }
+  return cnt;
+}
+
+void resample_septic(const float* x, int n_in, const int* start, const float* frac, int n_out, int n_pad, float* y,
+                     hipStream_t s) {
+  if (n_pad <= 0) return;
+  hipLaunchKernelGGL(k_resample_septic, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), 0, s, x, n_in, start, frac,
+                     n_out, n_pad, y);
+}
+
 // =============================================================================================
 // Flow-head chain in ONE persistent launch (mlp.rs:146-213, 370-383; flow_lm.rs:7-22): for every
 // lsd Euler step, input projection -> 6 ResBlocks -> FinalLayer -> x += v / N. As separate

@@ -80,6 +80,10 @@ SIGNATURES = [
     ("ptts_voice_from_audio", C.c_int, [C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     ("ptts_resample_len", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("ptts_resample", C.c_int, [C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, F32P]),
+    ("ptts_resample_len_ex", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int]),
+    ("ptts_resample_ex", C.c_int, [C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, C.c_int, F32P]),
+    ("ptts_voice_from_audio_ex", C.c_int, [C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.POINTER(C.c_void_p)]),
     ("ptts_flush_async", C.c_int, [C.c_void_p, C.c_int]),
     ("ptts_test_gemm", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, F32P, F32P, F32P]),
     ("ptts_voice_len", C.c_int, [C.c_void_p]),

@@ -65,6 +65,15 @@ class StepResult:
     latents: np.ndarray  # [n_rows, 32]
 
 
+RESAMPLERS = {"poly": 0, "rubato": 1}  # PTTS_RESAMPLE_POLY, PTTS_RESAMPLE_RUBATO_SEPTIC
+
+
+def resampler_code(name: str) -> int:
+    if name not in RESAMPLERS:
+        raise ValueError(f"resampler must be one of {sorted(RESAMPLERS)}, got {name!r}")
+    return RESAMPLERS[name]
+
+
 class Engine:
     def __init__(self, device: int = 0, max_slots: int = 1, max_ctx: int = 1024, lsd_decode_steps: int = 1,
                  seed: int = 0x5EED, weights_path: str | None = None, weight_blob: int | None = None,
@@ -198,21 +207,26 @@ class Engine:
         check(lib().ptts_voice_from_pcm(self.handle, fptr(x), x.size, C.byref(h)))
         return Voice(self, h.value)
 
-    def voice_from_audio(self, samples: np.ndarray, sample_rate: int, chunk_frames: int = 0) -> Voice:
+    def voice_from_audio(self, samples: np.ndarray, sample_rate: int, chunk_frames: int = 0,
+                         resampler: str = "poly") -> Voice:
         """Mono samples at any rate -> GPU resample to 24 kHz -> chunked Mimi encode -> voice.
-        chunk_frames: 0 = the reference's adaptive rule, > 0 = that many frames, < 0 = one pass."""
+        chunk_frames: 0 = the reference's adaptive rule, > 0 = that many frames, < 0 = one pass.
+        resampler: "poly" (resample_poly, the rule the reference's ref.wav fixture pair was made
+        with) or "rubato" (the Rust driver's FastFixedIn / Septic, audio.rs:197-255)."""
         x = np.ascontiguousarray(samples, np.float32).reshape(-1)
         h = C.c_void_p()
-        check(lib().ptts_voice_from_audio(self.handle, fptr(x), x.size, int(sample_rate), int(chunk_frames),
-                                          C.byref(h)))
+        check(lib().ptts_voice_from_audio_ex(self.handle, fptr(x), x.size, int(sample_rate), int(chunk_frames),
+                                             resampler_code(resampler), C.byref(h)))
         return Voice(self, h.value)
 
-    def resample(self, x: np.ndarray, sr_from: int, sr_to: int = 24000) -> np.ndarray:
-        """The GPU resampler on its own (ptts_resample)."""
+    def resample(self, x: np.ndarray, sr_from: int, sr_to: int = 24000, resampler: str = "poly") -> np.ndarray:
+        """The GPU resampler on its own (ptts_resample_ex)."""
         x = np.ascontiguousarray(x, np.float32).reshape(-1)
-        y = np.zeros(max(lib().ptts_resample_len(x.size, sr_from, sr_to), 1), np.float32)
-        check(lib().ptts_resample(self.handle, fptr(x), x.size, int(sr_from), int(sr_to), fptr(y)))
-        return y[:lib().ptts_resample_len(x.size, sr_from, sr_to)]
+        code = resampler_code(resampler)
+        n = lib().ptts_resample_len_ex(x.size, int(sr_from), int(sr_to), code)
+        y = np.zeros(max(n, 1), np.float32)
+        check(lib().ptts_resample_ex(self.handle, fptr(x), x.size, int(sr_from), int(sr_to), code, fptr(y)))
+        return y[:n]
 
     # -- slots
     def open(self, slot: int, voice: Voice, ids, params: GenerationParams):

@@ -53,6 +53,10 @@ class TTSModel:
         self.sample_rate = SAMPLE_RATE
         self.tokenizer = tokenizer
         self.voice_prompt_chunk_frames: int | None = None  # tts_model.rs:417 (None = adaptive rule)
+        # voice-prompt resampler for rates other than 24 kHz: "poly" (resample_poly, the rule of the
+        # reference's ref.wav fixture pair) or "rubato" (the Rust driver's FastFixedIn / Septic,
+        # audio.rs:197-255; restated, parity unpinned)
+        self.voice_resampler: str = "poly"
         self._seed = 0
 
     @classmethod
@@ -103,7 +107,7 @@ class TTSModel:
     def get_voice_state_from_tensor(self, audio: np.ndarray, sample_rate: int = SAMPLE_RATE) -> Voice:
         """tts_model.rs:504-577 (24 kHz mono PCM); other rates are resampled on the GPU first."""
         return self.engine.voice_from_audio(np.asarray(audio, np.float32).reshape(-1), sample_rate,
-                                            self.voice_prompt_chunk_frames or 0)
+                                            self.voice_prompt_chunk_frames or 0, self.voice_resampler)
 
     def get_voice_state_from_bytes(self, data: bytes) -> Voice:
         """tts_model.rs:428-444: WAV bytes -> (GPU) resample -> encode -> prompt prefill."""

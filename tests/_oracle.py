@@ -42,6 +42,8 @@ def lib(name: str = ORACLE) -> C.CDLL:
         L.orc_encode_ex.argtypes = [C.c_void_p, F32P, C.c_int, C.c_int, F32P, F32P, F32P, F32P]
         L.orc_resample_len.argtypes = [C.c_int, C.c_int, C.c_int]
         L.orc_resample.argtypes = [F32P, C.c_int, C.c_int, C.c_int, F32P]
+        L.orc_resample_septic_len.argtypes = [C.c_int, C.c_int, C.c_int]
+        L.orc_resample_septic.argtypes = [F32P, C.c_int, C.c_int, C.c_int, F32P]
         L.orc_time_embeddings.argtypes = [C.c_void_p, C.c_int, F32P]
         L.orc_bench.restype = C.c_double
         L.orc_bench.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
@@ -118,6 +120,15 @@ def resample(x: np.ndarray, sr_from: int, sr_to: int = 24000) -> np.ndarray:
     x = np.ascontiguousarray(x, np.float32).reshape(-1)
     y = np.zeros(max(L.orc_resample_len(x.size, sr_from, sr_to), 1), np.float32)
     n = L.orc_resample(fp(x), x.size, sr_from, sr_to, fp(y))
+    return y[:n]
+
+
+def resample_septic(x: np.ndarray, sr_from: int, sr_to: int = 24000) -> np.ndarray:
+    """The oracle's restatement of the Rust driver's resampler (rubato FastFixedIn / Septic)."""
+    L = lib()
+    x = np.ascontiguousarray(x, np.float32).reshape(-1)
+    y = np.zeros(max(L.orc_resample_septic_len(x.size, sr_from, sr_to), 1), np.float32)
+    n = L.orc_resample_septic(fp(x), x.size, sr_from, sr_to, fp(y))
     return y[:n]
 
 

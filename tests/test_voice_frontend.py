@@ -9,7 +9,13 @@ Pinning:
   * chunked encode: the reference's Python streaming modules driven the way the Rust driver
     chunks (gen_golden.py:run_encoder_chunked).
 Tolerances: resampler 1e-6 abs (f64 accumulation here vs scipy's f32 upfirdn); encoder
-conditioning 1e-5 abs (fp32, reduction order only)."""
+conditioning 1e-5 abs (fp32, reduction order only).
+
+The Rust driver's own resampler (rubato 0.14.1 FastFixedIn / Septic, audio.rs:197-255) is an
+option ("rubato"): its source is not in the reference and no fixture of it exists, so its parity
+is UNPINNED. The oracle's restatement is checked against properties of the published algorithm
+(the f64 position walk and its output count, exact reproduction of degree-7 polynomials, a band-
+limited tone at the walk's positions), and the GPU kernel against the oracle bit for bit."""
 
 import struct
 from pathlib import Path
@@ -144,6 +150,77 @@ def test_oracle_resample_matches_reference_ref_wav_pair():
         assert m.size == (y.size + 1919) // 1920 * 1920
 
 
+def _septic_positions(n, sr_from, sr_to=24000):
+    """rubato FastFixedIn's read positions, restated in numpy: from -4, + sr_from / sr_to per
+    output (f64, left to right: np.cumsum adds sequentially), while the position before the step
+    is < n - 9."""
+    t = 1.0 / (sr_to / sr_from)
+    m = int((n - 9 + 4) / t) + 3
+    walk = np.cumsum(np.concatenate([[-4.0], np.full(m, t)]))
+    cnt = int(np.argmax(walk >= n - 9)) if (walk >= n - 9).any() else m
+    return walk[1:cnt + 1]
+
+
+@pytest.mark.parametrize("sr", RATES + (96000, 24000))
+def test_oracle_septic_resampler_walk_and_length(sr):
+    from _oracle import resample_septic
+
+    for n in (10, 11, 37, 4000, 48001):
+        y = resample_septic(np.zeros(n, np.float32), sr)
+        if sr == 24000:
+            assert y.size == n  # equal rates: the input unchanged (audio.rs:198-200)
+            continue
+        assert y.size == _septic_positions(n, sr).size, (sr, n)
+        assert abs(y.size - (n - 5) * 24000 / sr) <= 1.0 + 24000 / sr
+
+
+@pytest.mark.parametrize("sr", RATES)
+def test_oracle_septic_resampler_reproduces_polynomials(sr):
+    """An 8-point septic reproduces every polynomial of degree <= 7 at the read positions whose
+    window lies inside the input (f32 rounding apart)."""
+    from _oracle import resample_septic
+
+    n = 3000
+    rng = np.random.default_rng(sr)
+    c = rng.uniform(-1, 1, 8)
+    p = lambda u: sum(c[i] * ((u - n / 2) / n) ** i for i in range(8))  # noqa: E731
+    y = resample_septic(p(np.arange(n, dtype=np.float64)).astype(np.float32), sr)
+    pos = _septic_positions(n, sr)
+    inner = (np.floor(pos) >= 3) & (np.floor(pos) + 4 < n)
+    assert inner.sum() > 0.9 * y.size
+    assert np.abs(y[inner] - p(pos[inner])).max() <= 2e-5
+
+
+@pytest.mark.parametrize("sr", RATES)
+def test_oracle_septic_resampler_tone_at_walk_positions(sr):
+    """A 300-Hz tone comes out as the tone sampled at the walk's positions (rubato's output is not
+    delay-compensated: output m is the input at -4 + (m + 1) sr / 24000 samples)."""
+    from _oracle import resample_septic
+
+    n = 4000
+    x = np.sin(2 * np.pi * 300 * np.arange(n) / sr).astype(np.float32)
+    y = resample_septic(x, sr)
+    pos = _septic_positions(n, sr)
+    inner = (pos > 4) & (pos < n - 5)
+    assert np.abs(y[inner] - np.sin(2 * np.pi * 300 * pos[inner] / sr)).max() <= 1e-6
+
+
+def test_resampler_choice_over_the_boundary():
+    """ptts_resample_len_ex (host-only: no GPU call) agrees with the oracle for both rules."""
+    from _oracle import lib as olib
+
+    from pocket_tts_amd import engine
+    from pocket_tts_amd._lib import lib
+
+    for sr in RATES + (24000,):
+        for n in (1, 50, 331708):
+            assert lib().ptts_resample_len_ex(n, sr, 24000, 0) == olib().orc_resample_len(n, sr, 24000), (sr, n)
+            assert lib().ptts_resample_len_ex(n, sr, 24000, 1) == olib().orc_resample_septic_len(n, sr, 24000), (sr, n)
+    assert lib().ptts_resample_len_ex(100, 48000, 24000, 7) == 0
+    with pytest.raises(ValueError):
+        engine.resampler_code("sinc")
+
+
 def test_oracle_chunked_encoder_matches_reference():
     from _oracle import Oracle
 
@@ -176,6 +253,47 @@ def test_gpu_resampler_matches_oracle_and_reference(gpu_engine):
     x = (0.3 * np.sin(np.arange(441000) * 0.01)).astype(np.float32)
     y = gpu_engine.resample(x, 44100)
     assert y.size == 240000 and np.abs(y - resample(x, 44100)).max() <= 1e-7
+
+
+@pytest.mark.gpu
+def test_gpu_rubato_resampler_matches_oracle(gpu_engine):
+    """The Rust driver's resampler option on the GPU against the oracle's restatement: bit for bit
+    (same f32 operations in the same order, same host position walk); parity with rubato itself is
+    unpinned (no fixture)."""
+    from _oracle import resample_septic
+
+    g = load_golden("resample.safetensors")
+    for sr in RATES:
+        x = g[f"x_{sr}"]
+        r = resample_septic(x, sr)
+        if r.size == 0:  # x_8000 is one sample: rubato's walk yields nothing, the engine rejects it
+            with pytest.raises(Exception):
+                gpu_engine.resample(x, sr, resampler="rubato")
+            continue
+        y = gpu_engine.resample(x, sr, resampler="rubato")
+        assert y.shape == r.shape, sr
+        np.testing.assert_array_equal(y, r)
+    x = (0.3 * np.sin(np.arange(441000) * 0.01)).astype(np.float32)  # 10 s at 44.1 kHz
+    np.testing.assert_array_equal(gpu_engine.resample(x, 44100, resampler="rubato"), resample_septic(x, 44100))
+    np.testing.assert_array_equal(gpu_engine.resample(x[:1000], 24000, resampler="rubato"), x[:1000])
+    with pytest.raises(Exception):
+        gpu_engine.resample(x[:4], 48000, resampler="rubato")  # the walk yields no sample: rejected
+
+
+@pytest.mark.gpu
+def test_gpu_rubato_voice_path_matches_oracle_resample(gpu_engine):
+    """voice_from_audio with the rubato rule == the oracle's rubato output encoded at 24 kHz."""
+    from _oracle import resample_septic
+
+    x = (0.2 * np.random.default_rng(3).standard_normal(48000 * 2)).astype(np.float32)
+    v = gpu_engine.voice_from_audio(x, 48000, -1, resampler="rubato")
+    w = gpu_engine.voice_from_audio(resample_septic(x, 48000), 24000, -1)
+    assert v.n_frames == w.n_frames
+    np.testing.assert_array_equal(v.conditioning(), w.conditioning())
+    p = gpu_engine.voice_from_audio(x, 48000, -1)  # the default rule differs (a different resampler)
+    assert np.abs(p.conditioning() - v.conditioning()).max() > 1e-4
+    for a in (v, w, p):
+        a.close()
 
 
 @pytest.mark.gpu
