@@ -1220,6 +1220,9 @@ void Engine::build_front(std::vector<Op>& ops, int B, int hb) {
     c.lnb = W(L_.fl[0].n1b);
     c.x = x_;
     c.h = h_;
+    c.err_dev = herr_;
+    c.err_host = h_err_;
+    c.n_zero = nfr_ > 1 ? max_slots_ - B : 0;
     ops.push_back({"front_commit", [c](hipStream_t s) { front_commit(c, s); }, 2.0 * B * D * LDIM,
                    (double)B * (sizeof(SlotState) * 2 + 4.0 * (1 + 3 * LDIM + 1 + 2 + 2 + 2 * D)) +
                        4.0 * ((double)D * LDIM + 2 * D)});
@@ -1637,12 +1640,9 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp, int nfr) {
       }
       op.fn(cs);
     }
-    if (part == 0) {  // the hand-off timeout word, read by fetch() without a device round trip
-      PTTS_HIP(hipMemcpyAsync(h_err_, herr_, sizeof(int), hipMemcpyDeviceToHost, cs));
-      // multi-frame passes: a pass covers the largest row count of its frames, so this frame's
-      // rows past B carry no frame
-      if (nfr_ > 1 && B < max_slots_)
-        PTTS_HIP(hipMemsetAsync(flags_[hb] + B, 0, sizeof(FrameFlags) * (max_slots_ - B), cs));
+    // part 0: the hand-off timeout word (read by fetch() without a device round trip) and the
+    // flags of rows past B are front_commit's side jobs, not copy / fill nodes of the graph
+    if (part == 0) {
     } else if (nfr_ > 1) {  // every frame of the pass (PCM and meta) leaves HBM in one copy
       const size_t n = (size_t)max_slots_ * nfr_ * FRAME + nfr_ * ((meta_floats_ + 31) / 32 * 32);
       PTTS_HIP(hipMemcpyAsync(h_pcmp_[hb / nfr_], pcmp_[hb / nfr_], sizeof(float) * n, hipMemcpyDeviceToHost, cs));

@@ -375,6 +375,13 @@ struct FrontCommitArgs {
   // updated lat_in (Wt = input_linear transposed [32][1024])
   const float *Wt, *lnw, *lnb;
   float *x, *h;
+  // side jobs of workgroup 0 (they used to be copy / fill nodes at the end of the front graph, a
+  // blit launch on the step's critical chain): the hand-off timeout word err_dev -> err_host
+  // (pinned host memory, a system-scope store) and zero flags for the rows B .. B + n_zero - 1
+  // (multi-frame passes: a pass covers the largest row count of its frames)
+  const int* err_dev;
+  int* err_host;
+  int n_zero;
 };
 void front_commit(const FrontCommitArgs& a, hipStream_t s);
 

@@ -3461,7 +3461,12 @@ __global__ __launch_bounds__(256) void k_front_commit(FrontCommitArgs a) {
     }
     a.flags[b] = f;
     a.eos_out[b] = e;
+    if (b == 0 && a.err_host)
+      __hip_atomic_store(a.err_host, __hip_atomic_load(a.err_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  if (b == 0)
+    for (int r = t; r < a.n_zero; r += 256) a.flags[a.B + r] = FrameFlags{0, 0};
   if (t < 32) {
     a.lat_out[b * 32 + t] = cv;
     if (valid) a.lat_in[b * 32 + t] = cv;
