@@ -278,7 +278,10 @@ int ptts_fetch_ready(ptts_engine* e, int calls_back, int* ready);
  * has run on the GPU; wait = 1 blocks until it has. Pipelined engines let the host run calls ahead
  * of the GPU; a driver that admits new rows waits here (calls_back = 1) before its next call, so an
  * admission queues behind one FlowLM step at most (first-chunk latency), while the GPU still has
- * the next step queued. */
+ * the next step queued. Calls are tracked from an engine's first ptts_front_done on (each later
+ * call records an event after its front part; a driver that never asks pays no marker per call):
+ * a call issued before that is answered from the front stream as a whole (done once everything
+ * queued on it has run), which can only be later, never earlier, than its own front part. */
 int ptts_front_done(ptts_engine* e, int calls_back, int wait, int* done);
 /* First-frame previews (pipelined engines; no reference counterpart: the reference decodes each
  * frame right after its FlowLM step, tts_model.rs:1040-1047, and does not pipeline). With

@@ -1591,6 +1591,17 @@ std::vector<std::string> Engine::plan_names(int B) {
   return v;
 }
 
+// A stream wait costs the front stream a few us at the graph boundary even on a completed event
+// (profiles/r04/graph_boundary_ab.txt): the hand-off buffer waits are enqueued only when the host
+// sees the event still pending (the pass that last read the buffer is three passes old, so it has
+// normally completed by the time the call is issued).
+void Engine::wait_unless_done(hipStream_t s, hipEvent_t e) {
+  const hipError_t r = hipEventQuery(e);
+  if (r == hipSuccess) return;
+  (void)hipGetLastError();
+  PTTS_HIP(hipStreamWaitEvent(s, e, 0));
+}
+
 hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp, int nfr) {
   if (part == 0) qp = nfr = 0;  // the front part does not use the quantizer history
   const int key = (((B * 2 + part) * NHB + hb) * 2 + qp) * (NFR_MAX + 1) + nfr;
@@ -1720,7 +1731,7 @@ void Engine::call_async(int B, bool run_front) {
     if (front && xh_dirty_) refresh_xh();
     if (front) PTTS_HIP(hipGraphLaunch(front, stream_));
     else PTTS_HIP(hipMemsetAsync(flags_[hb], 0, sizeof(FrameFlags) * max_slots_, stream_));
-    PTTS_HIP(hipEventRecord(ev_call_[k_ % 4], stream_));
+    if (call_ev_from_ >= 0) PTTS_HIP(hipEventRecord(ev_call_[k_ % 4], stream_));
   };
   if (!pipeline_) {
     hipGraphExec_t back = part_graph(1, B, hb, qp, 1);
@@ -1748,7 +1759,7 @@ void Engine::call_async(int B, bool run_front) {
     // the pass's other calls, so they need no wait of their own (stream order). A stream wait
     // costs the front stream ≈ 5 us at the graph boundary even on a completed event (graph
     // stamps, profiles/r04/graph_boundary_ab.txt).
-    if (kr == 0) PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
+    if (kr == 0) wait_unless_done(stream_, ev_back_[hb]);
     run_front_part();
     launch_previews(B, hb);
     // only the pass's last front part is waited for (by the pass, below)
@@ -1781,7 +1792,7 @@ void Engine::call_async(int B, bool run_front) {
   } else {
     const int prev_rows = k_ > 0 ? front_rows_ : B;  // 0: the previous call was a flush
     const int hb1 = (hb + nhb_ - 1) % nhb_, qp1 = qp ^ 1;  // frame k-1
-    PTTS_HIP(hipStreamWaitEvent(stream_, ev_back_[hb], 0));
+    wait_unless_done(stream_, ev_back_[hb]);
     run_front_part();
     launch_previews(B, hb);
     PTTS_HIP(hipEventRecord(ev_front_[hb], stream_));
@@ -1860,7 +1871,21 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
 bool Engine::front_done(int calls_back, bool wait) {
   PTTS_REQUIRE(calls_back >= 0 && calls_back <= 3, "calls_back must be in [0, 3]");
   const long long k = k_ - 1 - calls_back;
+  if (call_ev_from_ < 0) call_ev_from_ = k_;  // the calls issued from now on record their event
   if (k < 0) return true;
+  if (k < call_ev_from_) {  // issued before the first query: no event of its own, the stream's state
+    if (wait) {
+      PTTS_HIP(hipStreamSynchronize(stream_));
+      return true;
+    }
+    const hipError_t r = hipStreamQuery(stream_);
+    if (r == hipErrorNotReady) {
+      (void)hipGetLastError();
+      return false;
+    }
+    PTTS_HIP(r);
+    return true;
+  }
   hipEvent_t e = ev_call_[k % 4];
   if (wait) {
     PTTS_HIP(hipEventSynchronize(e));

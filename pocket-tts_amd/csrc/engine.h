@@ -118,6 +118,7 @@ class Engine {
   // multi-frame passes: a pass whose later calls were all flushes decodes only the frames its
   // calls started (nfr in part_graph's key)
   hipGraphExec_t part_graph(int part, int B, int hb, int qp, int nfr);
+  void wait_unless_done(hipStream_t s, hipEvent_t e);
   void push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r);
   void flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag);
   void linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M, const float* Wt,
@@ -338,6 +339,9 @@ class Engine {
   std::vector<std::pair<int, long long>> pv_pending_;  // (slot, call of its first front part)
   hipEvent_t ev_pv_front_ = nullptr;
   hipEvent_t ev_call_[4] = {};  // after the front part (or flush) of call k: ev_call_[k % 4]
+  // calls from this one on record ev_call_ (set by the first front_done(): a caller that never
+  // asks puts no event marker on the front stream per call); -1 = none yet
+  long long call_ev_from_ = -1;
   hipEvent_t ev_pv_read_[NHB] = {};  // a preview's gather of hand-off buffer q (front(q + nhb) waits)
   bool pv_read_pending_[NHB] = {};
   std::map<int, hipGraphExec_t> pv_graphs_;
