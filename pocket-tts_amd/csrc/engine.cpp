@@ -1602,6 +1602,19 @@ void Engine::wait_unless_done(hipStream_t s, hipEvent_t e) {
   PTTS_HIP(hipStreamWaitEvent(s, e, 0));
 }
 
+// The frame(s) a back part decoded leave HBM by a copy enqueued right after its graph on the same
+// stream (fetch() reads host memory): a DMA-engine transfer, not a blit-kernel node of the graph,
+// whose workgroups held CUs beside the front part while the host writes drained.
+void Engine::copy_out(int B, int hb, hipStream_t s) {
+  if (nfr_ > 1) {  // every frame of the pass (PCM and meta) in one copy
+    const size_t n = (size_t)max_slots_ * nfr_ * FRAME + nfr_ * ((meta_floats_ + 31) / 32 * 32);
+    PTTS_HIP(hipMemcpyAsync(h_pcmp_[hb / nfr_], pcmp_[hb / nfr_], sizeof(float) * n, hipMemcpyDeviceToHost, s));
+  } else {
+    PTTS_HIP(hipMemcpyAsync(h_pcm_[hb], pcm_[hb], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, s));
+    PTTS_HIP(hipMemcpyAsync(h_meta_[hb], meta_[hb], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost, s));
+  }
+}
+
 hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp, int nfr) {
   if (part == 0) qp = nfr = 0;  // the front part does not use the quantizer history
   const int key = (((B * 2 + part) * NHB + hb) * 2 + qp) * (NFR_MAX + 1) + nfr;
@@ -1652,16 +1665,8 @@ hipGraphExec_t Engine::part_graph(int part, int B, int hb, int qp, int nfr) {
       op.fn(cs);
     }
     // part 0: the hand-off timeout word (read by fetch() without a device round trip) and the
-    // flags of rows past B are front_commit's side jobs, not copy / fill nodes of the graph
-    if (part == 0) {
-    } else if (nfr_ > 1) {  // every frame of the pass (PCM and meta) leaves HBM in one copy
-      const size_t n = (size_t)max_slots_ * nfr_ * FRAME + nfr_ * ((meta_floats_ + 31) / 32 * 32);
-      PTTS_HIP(hipMemcpyAsync(h_pcmp_[hb / nfr_], pcmp_[hb / nfr_], sizeof(float) * n, hipMemcpyDeviceToHost, cs));
-    } else {  // the frame of this buffer leaves HBM inside the step (fetch() reads host memory)
-      PTTS_HIP(hipMemcpyAsync(h_pcm_[hb], pcm_[hb], sizeof(float) * B * FRAME, hipMemcpyDeviceToHost, cs));
-      PTTS_HIP(hipMemcpyAsync(h_meta_[hb], meta_[hb], sizeof(float) * meta_floats_, hipMemcpyDeviceToHost,
-                              cs));
-    }
+    // flags of rows past B are front_commit's side jobs; part 1: the frames leave HBM by copy_out()
+    // after the graph (no copy nodes in either graph)
 #ifdef PTTS_PROBES
     if (stamp_ring_) stamp(stamp_ring_, stamp_ctr_, (unsigned)(part << 8 | hb << 1 | 1), cs);
 #endif
@@ -1737,6 +1742,7 @@ void Engine::call_async(int B, bool run_front) {
     hipGraphExec_t back = part_graph(1, B, hb, qp, 1);
     run_front_part();
     PTTS_HIP(hipGraphLaunch(back, stream_));
+    copy_out(B, hb, stream_);
     out_hb_ = hb;
     out_rows_ = B;
   } else if (nfr_ > 1) {
@@ -1783,6 +1789,7 @@ void Engine::call_async(int B, bool run_front) {
           admit_pending_ = false;
         }
         PTTS_HIP(hipGraphLaunch(back, stream_be_));
+        copy_out(rows, h0, stream_be_);
       }
       PTTS_HIP(hipEventRecord(ev_back_[h0], stream_be_));  // the pass over buffers h0 .. (fetch waits)
     }
@@ -1804,6 +1811,7 @@ void Engine::call_async(int B, bool run_front) {
         admit_pending_ = false;
       }
       PTTS_HIP(hipGraphLaunch(back, stream_be_));
+      copy_out(prev_rows, hb1, stream_be_);
     }
     PTTS_HIP(hipEventRecord(ev_back_[hb1], stream_be_));
     out_hb_ = hb1;

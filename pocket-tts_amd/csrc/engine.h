@@ -119,6 +119,7 @@ class Engine {
   // calls started (nfr in part_graph's key)
   hipGraphExec_t part_graph(int part, int B, int hb, int qp, int nfr);
   void wait_unless_done(hipStream_t s, hipEvent_t e);
+  void copy_out(int B, int hb, hipStream_t s);
   void push_rr(std::vector<Op>& ops, const std::string& name, const RowReduceArgs& r);
   void flow_layers(std::vector<Op>& ops, int M, RowMap map, int qg, bool out_norm, const std::string& tag);
   void linear_split(std::vector<Op>& ops, const std::string& name, const float* X, long ldx, int M, const float* Wt,

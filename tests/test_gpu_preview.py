@@ -143,3 +143,31 @@ def test_closed_slot_drops_its_preview(oracle):
         assert [s for s, _ in got] == [0]
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("back_frames", [2, 4])
+def test_front_done_tracks_calls_from_its_first_use(back_frames):
+    """ptts_front_done: calls issued before an engine's first front_done are answered from the front
+    stream as a whole, later calls from their own event (a driver that never asks puts no event
+    marker on the front stream per call). Both answers are consistent with the call order, and the
+    frames of the stepping are unaffected."""
+    import pocket_tts_amd as pt
+
+    d = load_golden("e2e_lsd1.safetensors")
+    eng = pt.Engine(device=0, max_slots=4, max_ctx=256, lsd_decode_steps=1, seed=0x5EED, pipeline=True,
+                    back_frames=back_frames)
+    try:
+        v = eng.voice_from_prompt(d["prompt"][:8])
+        eng.open_many([0, 1], [v, v], [np.array([260, 2994, 262], np.int32)] * 2, [params(max_frames=40)] * 2)
+        for _ in range(6):  # untracked calls
+            eng.step_async(2)
+        assert eng.front_done(3, wait=True)  # an untracked call: the stream as a whole
+        assert eng.front_done(0, wait=False) in (True, False)
+        for _ in range(6):  # tracked from here on
+            eng.step_async(2)
+            assert eng.front_done(1, wait=True)
+        eng.sync()
+        assert all(eng.front_done(k, wait=False) for k in range(4))
+        eng.fetch(2)
+    finally:
+        eng.close()
