@@ -189,6 +189,7 @@ Engine::Engine(const ptts_engine_config& cfg) {
   vlen_ = (int*)dalloc(B + 1);
   slot_voice_.assign(B, nullptr);
   drained_.assign(B, 1);
+  admit_call_.assign(B, -1);
   share_voice_ = probe_env("PTTS_NO_SHARED_VOICE") == nullptr;
 #ifdef PTTS_PROBES
   if (probe_env("PTTS_STAMPS")) {
@@ -1725,6 +1726,7 @@ void Engine::call_async(int B, bool run_front) {
   admitted_since_call_ = false;
   prev_hb_ = out_hb_;
   prev_rows_ = out_rows_;
+  prev_k_ = out_k_;
   const int hb = (int)(k_ % nhb_), qp = (int)(k_ & 1);
   // the front part of this call, or (a flush) its hand-off buffer marked frame-less
   hipGraphExec_t front = B > 0 ? part_graph(0, B, hb, 0, 0) : nullptr;
@@ -1745,6 +1747,7 @@ void Engine::call_async(int B, bool run_front) {
     copy_out(B, hb, stream_);
     out_hb_ = hb;
     out_rows_ = B;
+    out_k_ = k_;
   } else if (nfr_ > 1) {
     // Multi-frame passes (nfr = 2 or 4): call k runs front(k) into buffer k % (3 nfr); at k % nfr
     // == 0, k >= nfr, one back pass decodes frames k-nfr .. k-1 (buffers (k-nfr) % (3 nfr) ..) on
@@ -1796,6 +1799,7 @@ void Engine::call_async(int B, bool run_front) {
     const int lag = 2 * nf - 1;
     out_hb_ = (int)((k_ + nhb_ - lag) % nhb_);
     out_rows_ = k_ >= lag ? rows_hb_[out_hb_] : 0;
+    out_k_ = k_ - lag;
   } else {
     const int prev_rows = k_ > 0 ? front_rows_ : B;  // 0: the previous call was a flush
     const int hb1 = (hb + nhb_ - 1) % nhb_, qp1 = qp ^ 1;  // frame k-1
@@ -1816,6 +1820,7 @@ void Engine::call_async(int B, bool run_front) {
     PTTS_HIP(hipEventRecord(ev_back_[hb1], stream_be_));
     out_hb_ = hb1;
     out_rows_ = prev_rows;
+    out_k_ = k_ - 1;
   }
   front_rows_ = B;
   ++k_;
@@ -1836,6 +1841,7 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
   // the host copies of a call's frame stay intact for two more calls (three hand-off buffers)
   const int q = calls_back ? prev_hb_ : out_hb_;
   const int rows = calls_back ? prev_rows_ : out_rows_;
+  const long long fk = calls_back ? prev_k_ : out_k_;  // the call that produced the frame
   // Pipelined: wait only for the back part that produced this call's frame. The front part of
   // the next frame keeps running, so the front stream never idles across calls (the next call's
   // front graph is queued behind it while this one still runs).
@@ -1861,7 +1867,11 @@ void Engine::fetch(int B, float* pcm, uint8_t* valid, uint8_t* last, float* eos,
   };
   for (int b = 0; b < B; ++b) {
     const bool ok = b < n && hf[b].valid;
-    if (ok && hf[b].last) drained_[b] = 1;  // its last frame's pass has completed (waited above)
+    // its last frame's pass has completed (waited above) - unless the slot was admitted again
+    // after that frame's call (a driver that admits the next utterance before fetching the last
+    // frame of the previous one, as bench.py does): then the frame is the previous utterance's and
+    // the new one's back passes are still to come
+    if (ok && hf[b].last && fk >= admit_call_[b]) drained_[b] = 1;
     if (valid) valid[b] = ok;
     if (last) last[b] = ok && hf[b].last;
     if (pcm) {
@@ -2660,7 +2670,10 @@ void Engine::slots_open(int n, const int* slots, const ptts_voice* const* voices
     PTTS_HIP(hipEventRecord(ev_be_tail_, stream_be_));
     PTTS_HIP(hipStreamWaitEvent(stream_, ev_be_tail_, 0));
   }
-  for (int i = 0; i < n; ++i) drained_[slots[i]] = 0;
+  for (int i = 0; i < n; ++i) {
+    drained_[slots[i]] = 0;
+    admit_call_[slots[i]] = k_;
+  }
   // fresh Mimi decoder state (init_states(1, 1000) per segment, tts_model.rs:941) + slot states
   std::vector<SlotState> st(n);
   std::vector<int> fp(n);

@@ -280,6 +280,10 @@ class Engine {
   int out_hb_ = 0;           // hand-off buffer of the frame the last call produced
   int out_rows_ = 0;         // rows that frame covers
   int prev_hb_ = 0, prev_rows_ = 0;  // the same for the call before (fetch with calls_back = 1)
+  long long out_k_ = -1, prev_k_ = -1;  // the call index of those frames
+  // per slot: the index of the first call of its current utterance (the admission's k_): a fetched
+  // frame of an earlier call belongs to the slot's previous utterance and does not drain the slot
+  std::vector<long long> admit_call_;
   int front_rows_ = 0;       // rows of the last front part (0: the call was a flush)
   bool admitted_since_call_ = false;  // an admission since the last step / flush call
   // x_ / h_ / lat_in_ written outside the step graphs since the last front part (refresh_xh)
