@@ -179,3 +179,46 @@ def test_bench_exact_input_shared_voice_matches_oracle(oracle, back_frames):
             assert err[0] <= LAT_TOL and err[1] <= LAT_TOL and err[2] <= PCM_TOL, (b, i, err)
     print(f"bench input (shared voice, temp {temp}, back_frames {back_frames}): worst |d| eos/latent/pcm vs oracle "
           f"{worst}")
+
+
+@pytest.mark.parametrize("back_frames", [2, 4])
+def test_overlapped_admission_job_loop_completes_every_job(back_frames):
+    """bench.py's job loop: the next job's batched admission is issued before the previous job's
+    last frame is fetched (its prefill runs beside that job's last back passes). Every job's last
+    frame must come back valid and last for all 32 rows. Regression for the drained-slot race
+    (DESIGN.md 14.8): the fetch of job j's last frame marked the slots of job j + 1 drained, so
+    job j + 2's admission could reset their state ahead of job j + 1's queued back passes.
+    (tools/race_probe.py runs the same loop for many more jobs.)"""
+    import sys
+
+    from conftest import ROOT
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    import pocket_tts_amd as pt
+
+    K = 24
+    eng = pt.Engine(device=0, max_slots=B, max_ctx=bench.PROMPT_FRAMES + bench.TEXT_TOKENS + K + 8,
+                    lsd_decode_steps=1, seed=0x5EED, pipeline=True, back_frames=back_frames)
+    try:
+        v = eng.voice_from_prompt(bench.synth_prompt())
+
+        def admit(j):
+            eng.open_many(list(range(B)), [v] * B, [bench.text_ids(b) for b in range(B)],
+                          [pt.GenerationParams(temp=0.7, eos_threshold=float("inf"), max_frames=K,
+                                               seed=bench.slot_seed(j, 0, b)) for b in range(B)])
+
+        admit(0)
+        for j in range(24):
+            lag, delay = eng.frame_lag()
+            for _ in range(K + delay):
+                eng.step_async(B)
+            for _ in range(lag):
+                eng.flush_async(B)
+            if j + 1 < 24:
+                admit(j + 1)
+            r = eng.fetch(B)
+            assert r.valid.all() and r.last.all(), (j, np.nonzero(~r.valid)[0][:8])
+            assert np.isfinite(r.pcm).all()
+    finally:
+        eng.close()
